@@ -1,0 +1,104 @@
+/*
+ * zcrc.h -- C ABI of libzcrc, the MI355X batched CRC-32 engine for ZIPsFS.
+ *
+ * Drop-in boundary.  ZIPsFS computes the CRC of a fully preloaded ZIP entry
+ * with the *static* function
+ *     static uint32_t cg_crc32(const void *data, size_t n_bytes, uint32_t crc,
+ *                              pthread_mutex_t *mutex);          src/cg_crc32.c:26
+ * textually included by src/ZIPsFS_preloadfileram.c:11 and called once, in
+ * fhandle_check_crc32 (src/ZIPsFS_preloadfileram.c:243).  The replacement
+ * zipsfs_amd/cg_crc32.c keeps that exact static signature and include guard
+ * and forwards to zcrc32() below (INTEGRATION.md shows the one-line build
+ * change).  Everything else here is new surface with no reference caller:
+ * batched host- and device-resident entry points and the GF(2) combine.
+ *
+ * Semantics of every CRC entry point: zlib crc32(crc, data, n) -- CRC-32/
+ * ISO-HDLC, reflected poly 0xEDB88320, pre/post inverted, `crc` is the value
+ * of a previous call (0 for a fresh CRC) -- bit-exact to src/cg_crc32.c.
+ *
+ * Errors.  The reference has no error path (src/cg_crc32.c always returns).
+ * This engine has NO CPU fallback: every CRC is computed on the GPU.
+ * Functions returning int return 0 on success and a negative code on
+ * failure (zcrc_last_error() gives the text); zcrc32() itself cannot report
+ * an error through its return value, so on a GPU failure it prints the
+ * reason to stderr and aborts -- loudly, never a silent wrong answer.
+ *
+ * Threading: all functions are thread-safe; device initialisation happens
+ * once per process (pthread_once semantics).  Host-pointer functions are
+ * synchronous.  Device-pointer functions are asynchronous on `stream`
+ * (a hipStream_t passed as void*, NULL = default stream).
+ */
+#ifndef ZCRC_H
+#define ZCRC_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define ZCRC_OK 0
+#define ZCRC_ERR_HIP (-1)      /* HIP runtime error (no device, launch, copy) */
+#define ZCRC_ERR_ARG (-2)      /* invalid argument                              */
+#define ZCRC_ERR_TOO_BIG (-3)  /* one launch limited to 4 TiB of payload        */
+
+/* Replaces cg_crc32(data, n_bytes, crc, mutex), src/cg_crc32.c:26.
+ * `data` is host memory, borrowed for the call.  Aborts on GPU failure. */
+uint32_t zcrc32(const void *data, size_t n_bytes, uint32_t crc);
+
+/* Same as zcrc32 but reports failure instead of aborting. */
+int zcrc32_checked(const void *data, size_t n_bytes, uint32_t crc, uint32_t *out_crc);
+
+/* Host-resident batch: out[i] = crc32(seeds ? seeds[i] : 0, ptrs[i], lens[i]).
+ * Buffers are staged through pinned memory and checksummed on the GPU in
+ * as few launches as fit the staging area.  flags: reserved, pass 0. */
+int zcrc32_batch(const void *const *ptrs, const size_t *lens, const uint32_t *seeds_or_null,
+                 uint32_t *out, size_t n, unsigned flags);
+
+/* Device-resident batch.  d_ptrs: device array of n device pointers;
+ * d_lens: device array of n byte counts; d_seeds_or_null: device array or
+ * NULL; d_out: device array of n results.  Asynchronous on `stream`; uses a
+ * stream-ordered scratch allocation of 8*(n+1) + 8*ceil(n/8192) bytes. */
+int zcrc32_batch_device(const void *const *d_ptrs, const uint64_t *d_lens,
+                        const uint32_t *d_seeds_or_null, uint32_t *d_out, size_t n, void *stream);
+
+/* Same, with caller-owned scratch (graph-capturable: no allocation inside).
+ * Needs zcrc32_batch_device_scratch_bytes(n) bytes of device memory. */
+size_t zcrc32_batch_device_scratch_bytes(size_t n);
+int zcrc32_batch_device_ws(const void *const *d_ptrs, const uint64_t *d_lens,
+                           const uint32_t *d_seeds_or_null, uint32_t *d_out, size_t n,
+                           void *d_scratch, size_t scratch_bytes, void *stream);
+
+/* Device-resident batch of equal-size chunks: buffer i = d_base + i*stride,
+ * each `len` bytes (fixed-size cache chunks).  No scratch, one launch (plus a
+ * memset of d_out when chunks may be split across waves). */
+int zcrc32_batch_device_strided(const void *d_base, uint64_t stride, uint64_t len, size_t n,
+                                const uint32_t *d_seeds_or_null, uint32_t *d_out, void *stream);
+
+/* GF(2) algebra (pure integer math, no data access):
+ * crc32(A||B) == zcrc32_combine(crc32(A), crc32(B), |B|)   (zlib semantics). */
+uint32_t zcrc32_combine(uint32_t crc_a, uint32_t crc_b, uint64_t len_b);
+
+/* Synthetic payload (bench/test data, not a CRC path): fills device buffer
+ * d_ptrs[i] (d_lens[i] bytes) with the counter-based payload of SURVEY.md
+ * 8(d) for payload index index0 + i*index_step:
+ *   word j = splitmix64(seed ^ (index << 32 | j)), little-endian. */
+int zcrc_fill_synthetic(const uint64_t *d_ptrs, const uint64_t *d_lens, size_t n, uint64_t index0,
+                        uint64_t index_step, uint64_t seed, void *stream);
+
+/* Diagnostics / measurement. */
+const char *zcrc_last_error(void);
+const char *zcrc_version(void);
+int zcrc_device_info(int *num_cus, int *arch_major, int *arch_minor);
+/* When enabled, each device launch of the main CRC kernel is bracketed by
+ * HIP events recorded on the launch stream; zcrc_profile_read returns the
+ * summed kernel milliseconds and launch count since the last reset. */
+void zcrc_profile_enable(int on);
+int zcrc_profile_read(double *total_ms, int *launches);
+void zcrc_profile_reset(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* ZCRC_H */

@@ -1,0 +1,258 @@
+"""CPU model of zcrc_kernels.hip's decomposition (TEST INFRASTRUCTURE).
+
+Re-executes, with numpy over the 64 lanes x 4 dword streams, exactly the
+arithmetic the HIP kernel performs -- wave-range partition and boundary
+snapping, 16-B aligned 1 KiB blocks with out-of-range zero fill, edge
+fix-ups (mask + seed injection), the braided MCT(x^8192) stream update, the
+in-lane / cross-lane combine tree, the x^(-8t) alignment shift, split-piece
+x^(8d) shifts and xor combine.  Checked against the oracle on CPU so that
+decomposition bugs are caught without a GPU; the GPU tests then check the
+real kernel against the oracle.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+POLY = 0xEDB88320
+ONE = 0x80000000
+
+# constants mirrored from zcrc_internal.h
+K_WAVES = 16
+K_MIN_RANGE = 256 << 10
+K_SPLIT_GRAIN = 64 << 10
+K_SPLIT_MIN = 2 * K_SPLIT_GRAIN
+K_MIN_PIECE = 4096
+
+
+def times_x(r: int) -> int:
+    return (r >> 1) ^ (POLY if r & 1 else 0)
+
+
+def times_xinv(r: int) -> int:
+    return (((r ^ POLY) << 1) | 1) & 0xFFFFFFFF if r & 0x80000000 else (r << 1) & 0xFFFFFFFF
+
+
+def gf2_mul(a: int, b: int) -> int:
+    p = 0
+    for i in range(32):
+        if (a >> (31 - i)) & 1:
+            p ^= b
+        b = times_x(b)
+    return p
+
+
+def xpow8(nbytes: int) -> int:
+    acc, v, k = ONE, ONE >> 1, 0
+    x2k = [v]
+    for _ in range(70):
+        v = gf2_mul(v, v)
+        x2k.append(v)
+    k = 3
+    while nbytes:
+        if nbytes & 1:
+            acc = gf2_mul(acc, x2k[k])
+        nbytes >>= 1
+        k += 1
+    return acc
+
+
+def xinvpow8(nbytes: int) -> int:
+    r = ONE
+    for _ in range(8 * nbytes):
+        r = times_xinv(r)
+    return r
+
+
+def mct(c: int) -> np.ndarray:
+    t = np.zeros((4, 256), dtype=np.uint32)
+    # linearity: build from the 32 single-bit products
+    bits = [gf2_mul(c, 1 << b) for b in range(32)]
+    for j in range(4):
+        for v in range(256):
+            acc = 0
+            for b in range(8):
+                if (v >> b) & 1:
+                    acc ^= bits[8 * j + b]
+            t[j, v] = acc
+    return t
+
+
+def mct_apply(t: np.ndarray, r):
+    r = np.asarray(r, dtype=np.uint32)
+    return (t[0][r & 0xFF] ^ t[1][(r >> 8) & 0xFF] ^ t[2][(r >> 16) & 0xFF] ^ t[3][r >> 24]).astype(np.uint32)
+
+
+class Tables:
+    def __init__(self):
+        self.braid = mct(xpow8(1024))
+        self.comb = [mct(xinvpow8(b)) for b in (4, 8, 16, 32, 64, 128, 256, 512)]
+        self.tshift = [mct(xinvpow8(t)) for t in range(16)]
+        std = np.zeros(256, dtype=np.uint32)
+        for v in range(256):
+            r = v
+            for _ in range(8):
+                r = times_x(r)
+            std[v] = r
+        self.stdtab = std
+
+
+_TABLES = None
+
+
+def tables() -> Tables:
+    global _TABLES
+    if _TABLES is None:
+        _TABLES = Tables()
+    return _TABLES
+
+
+# ------------------------------------------------------------ partition
+
+class Batch:
+    """Buffers as (address, length) into one flat numpy 'memory'."""
+
+    def __init__(self, memory: np.ndarray, addrs, lens, seeds=None):
+        self.mem = memory
+        self.addrs = [int(a) for a in addrs]
+        self.lens = [int(n) for n in lens]
+        self.seeds = [0] * len(self.lens) if seeds is None else [int(s) & 0xFFFFFFFF for s in seeds]
+        self.prefix = np.concatenate([[0], np.cumsum(np.asarray(self.lens, dtype=np.uint64))]).astype(np.uint64)
+        self.n = len(self.lens)
+        self.total = int(self.prefix[-1])
+
+    def lower_bound(self, t: int) -> int:
+        return int(np.searchsorted(self.prefix, np.uint64(t), side="left"))
+
+    def snap(self, t: int) -> int:
+        tot = self.total
+        if t == 0 or t >= tot:
+            return tot if t >= tot else 0
+        i = self.lower_bound(t)
+        pi = int(self.prefix[i])
+        if pi == t:
+            return t
+        b0 = int(self.prefix[i - 1])
+        n, p = pi - b0, t - b0
+        if n < K_SPLIT_MIN:
+            return pi
+        q = n - K_SPLIT_GRAIN * ((n - p) // K_SPLIT_GRAIN)
+        if q < K_MIN_PIECE:
+            return b0
+        return b0 + q
+
+
+def wave_ranges(batch: Batch, num_cus: int):
+    total = batch.total
+    want = max(1, (total + K_MIN_RANGE - 1) // K_MIN_RANGE)
+    W = min(want, num_cus * K_WAVES)
+    q, r = divmod(total, W)
+    out = []
+    for w in range(W):
+        s0 = batch.snap(q * w + (r * w) // W)
+        s1 = total if w + 1 == W else batch.snap(q * (w + 1) + (r * (w + 1)) // W)
+        out.append((s0, s1, w + 1 == W))
+    return out
+
+
+def wave_pieces(batch: Batch, s0: int, s1: int, last: bool):
+    """(buffer, rel_lo, rel_hi) pieces of one wave, as the kernel walks them."""
+    if s0 >= s1 and not last:
+        return []
+    i = batch.lower_bound(s0)
+    if 0 < i <= batch.n and int(batch.prefix[i]) > s0:
+        i -= 1
+    pieces = []
+    while i < batch.n:
+        b0, b1 = int(batch.prefix[i]), int(batch.prefix[i + 1])
+        if b0 >= s1 and not last:
+            break
+        n = b1 - b0
+        rel_lo = s0 - b0 if s0 > b0 else 0
+        rel_hi = n if (b1 < s1 or last) else s1 - b0
+        pieces.append((i, rel_lo, rel_hi))
+        i += 1
+    return pieces
+
+
+# ------------------------------------------------------------ one piece
+
+def _lowmask(k):
+    k = np.asarray(k, dtype=np.int64)
+    kk = np.clip(k, 0, 3).astype(np.uint64)
+    part = (np.uint64(1) << (np.uint64(8) * kk)) - np.uint64(1)
+    return np.where(k <= 0, np.uint64(0), np.where(k >= 4, np.uint64(0xFFFFFFFF), part)).astype(np.uint64)
+
+
+def _inj_word(inj: int, o):
+    """Bits of the 4-byte injection landing in a dword at relative byte offset o."""
+    o = np.asarray(o, dtype=np.int64)
+    inj = np.uint64(inj)
+    shl = (inj << (np.uint64(8) * np.clip(o, 0, 3).astype(np.uint64))) & np.uint64(0xFFFFFFFF)
+    shr = inj >> (np.uint64(8) * np.clip(-o, 0, 3).astype(np.uint64))
+    return np.where((o >= 0) & (o < 4), shl, np.where((o < 0) & (o > -4), shr, np.uint64(0))).astype(np.uint64)
+
+
+def crc_piece(mem: np.ndarray, pstart: int, pend: int, inj: int, T: Tables) -> int:
+    lanes = np.arange(64, dtype=np.int64)
+    astart = pstart & ~15
+    aend = (pend + 15) & ~15
+    span = aend - astart
+    K = (span + 1023) >> 10
+    tpad = aend - pend
+    c0 = span - 1024 * K + 16 * lanes
+    rs, re = pstart - astart, pend - astart
+    s = np.zeros((64, 4), dtype=np.uint32)
+    for it in range(K):
+        c = c0 + 1024 * it
+        data = np.zeros((64, 16), dtype=np.uint8)
+        ok = (c >= 0) & (c < span)
+        for l in np.nonzero(ok)[0]:
+            data[l] = mem[astart + c[l]: astart + c[l] + 16]
+        words = data.view("<u4").astype(np.uint64)  # (64, 4)
+        if it <= 1 or it + 1 == K:
+            lo = np.clip(rs - c, -64, 64)
+            hi = np.clip(re - c, -64, 64)
+            io = lo.copy()
+            for q in range(4):
+                m = _lowmask(hi - 4 * q) & ~_lowmask(lo - 4 * q) & np.uint64(0xFFFFFFFF)
+                words[:, q] = ((words[:, q] & m) ^ _inj_word(inj, io - 4 * q)) & np.uint64(0xFFFFFFFF)
+        x = (s.astype(np.uint64) ^ words).astype(np.uint32)
+        s = mct_apply(T.braid, x)
+    s0, s1, s2, s3 = s[:, 0], s[:, 1], s[:, 2], s[:, 3]
+    r = (s0 ^ mct_apply(T.comb[0], s1)) ^ mct_apply(T.comb[1], s2 ^ mct_apply(T.comb[0], s3))
+    for j in range(6):
+        moved = mct_apply(T.comb[2 + j], r)
+        d = 1 << j
+        shifted = np.concatenate([moved[d:], moved[64 - d:]])  # shfl_down: out of range keeps own
+        shifted[64 - d:] = moved[64 - d:]
+        r = r ^ shifted
+    r0 = int(r[0])
+    if tpad:
+        r0 = int(mct_apply(T.tshift[tpad], np.array([r0], dtype=np.uint32))[0])
+    return r0
+
+
+def run_batch(batch: Batch, num_cus: int = 256) -> np.ndarray:
+    """CRCs of every buffer, computed the way the kernel computes them."""
+    T = tables()
+    out = np.zeros(batch.n, dtype=np.uint32)
+    for (s0, s1, last) in wave_ranges(batch, num_cus):
+        for (i, rel_lo, rel_hi) in wave_pieces(batch, s0, s1, last):
+            n = batch.lens[i]
+            seed = batch.seeds[i]
+            whole = rel_lo == 0 and rel_hi == n
+            if n < 4:
+                r = (~seed) & 0xFFFFFFFF
+                for p in range(n):
+                    r = (r >> 8) ^ int(T.stdtab[(r ^ int(batch.mem[batch.addrs[i] + p])) & 0xFF])
+                out[i] = (~r) & 0xFFFFFFFF
+                continue
+            inj = (~seed) & 0xFFFFFFFF if rel_lo == 0 else 0
+            r = crc_piece(batch.mem, batch.addrs[i] + rel_lo, batch.addrs[i] + rel_hi, inj, T)
+            if whole:
+                out[i] = (~r) & 0xFFFFFFFF
+            else:
+                d = n - rel_hi
+                contrib = gf2_mul(xpow8(d), r) if d else r ^ 0xFFFFFFFF
+                out[i] ^= np.uint32(contrib)
+    return out

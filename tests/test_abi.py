@@ -1,0 +1,79 @@
+"""C-ABI boundary checks that need no GPU: libzcrc loads, exports every
+function include/zcrc.h declares, the host-only GF(2) combine is right, the
+drop-in cg_crc32.c compiles as C and C++ against the header, and the product
+package contains no CPU CRC path."""
+import os
+import random
+import subprocess
+import zlib
+
+import pytest
+
+import zipsfs_amd
+from zipsfs_amd import _lib
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_library_exports_header_symbols():
+    names = _lib.exported_symbols_from_header()
+    assert "zcrc32" in names and "zcrc32_batch_device" in names
+    lib = _lib.lib()
+    for n in names:
+        assert hasattr(lib, n), n
+    out = subprocess.run(["nm", "-D", "--defined-only", _lib.LIB_PATH], capture_output=True, text=True,
+                         check=True).stdout
+    exported = {line.split()[-1] for line in out.splitlines()}
+    assert set(names) <= exported
+
+
+def test_combine_matches_zlib():
+    rnd = random.Random(1)
+    for _ in range(200):
+        a = bytes(rnd.getrandbits(8) for _ in range(rnd.randint(0, 300)))
+        b = bytes(rnd.getrandbits(8) for _ in range(rnd.randint(0, 300)))
+        assert zipsfs_amd.crc32_combine(zlib.crc32(a), zlib.crc32(b), len(b)) == zlib.crc32(a + b)
+    # large length: combine with 2^40 zero bytes is consistent with repeated squaring
+    z = zipsfs_amd.crc32_combine(0x12345678, 0, 1 << 40)
+    assert isinstance(z, int)
+
+
+def test_version_and_gfx950_only():
+    assert "gfx950" in zipsfs_amd.version()
+
+
+@pytest.mark.parametrize("compiler,lang", [("gcc", "c"), ("g++", "c++")])
+def test_dropin_compiles(tmp_path, compiler, lang):
+    src = tmp_path / ("main.c" if lang == "c" else "main.cpp")
+    src.write_text(
+        '#include "cg_crc32.c"\n'
+        "#include <stdio.h>\n"
+        "int main(void){ pthread_mutex_t m = PTHREAD_MUTEX_INITIALIZER;\n"
+        '  printf("%08x\\n", cg_crc32("123456789", 9, 0, &m)); return 0; }\n')
+    exe = tmp_path / "a.out"
+    cmd = [compiler, "-Wall", "-Werror", "-I", os.path.join(ROOT, "zipsfs_amd"), "-I", os.path.join(ROOT, "include"),
+           str(src), "-o", str(exe), "-L", os.path.join(ROOT, "zipsfs_amd"), "-lzcrc",
+           "-Wl,-rpath," + os.path.join(ROOT, "zipsfs_amd"), "-pthread"]
+    subprocess.run(cmd, check=True)
+    assert exe.exists()
+
+
+def test_product_has_no_cpu_crc_path():
+    """The shipped package must not import the oracle or compute CRCs on the CPU."""
+    pkg = os.path.join(ROOT, "zipsfs_amd")
+    for dirpath, _, files in os.walk(pkg):
+        for f in files:
+            if f.endswith((".py", ".hip", ".h", ".c", ".cpp")):
+                text = open(os.path.join(dirpath, f)).read()
+                for bad in ("from oracle", "import oracle", "liboracle", "libref_cg_crc32", "import zlib",
+                            "binascii", "crc32_port"):
+                    assert bad not in text, (f, bad)
+
+
+def test_missing_gpu_fails_loudly():
+    """Without a device the API raises; it never answers from the CPU."""
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    with pytest.raises(zipsfs_amd.ZcrcError):
+        zipsfs_amd.cg_crc32(b"123456789")

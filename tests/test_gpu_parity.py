@@ -1,0 +1,238 @@
+"""GPU parity: libzcrc's HIP kernels vs the oracle / reference golden vectors.
+
+Every test calls the product through its C ABI (ctypes over libzcrc.so) and
+compares bit-exactly with (a) golden vectors produced by the reference's own
+src/cg_crc32.c (tests/golden/) or (b) the CPU restatement oracle/ on the
+same bytes.  Run on the MI355X box:  pytest -m gpu
+"""
+import random
+import zlib
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+import zipsfs_amd as z  # noqa: E402
+from oracle import oracle as o  # noqa: E402
+
+DEV = "cuda:0"
+SEED = o.PAYLOAD_SEED
+
+
+def u32(t):
+    return t.cpu().numpy().view(np.uint32)
+
+
+def dev_buffers_from_host(chunks, align=16, gap=0, lead=0):
+    """Pack host byte strings into one device allocation; return (mem, ptrs, lens, addrs)."""
+    offs, pos = [], lead
+    for c in chunks:
+        offs.append(pos)
+        pos += len(c) + gap
+        pos = (pos + align - 1) // align * align if align > 1 else pos
+    host = np.zeros(max(pos, 1), dtype=np.uint8)
+    for off, c in zip(offs, chunks):
+        host[off:off + len(c)] = np.frombuffer(c, dtype=np.uint8)
+    mem = torch.from_numpy(host).to(DEV)
+    base = mem.data_ptr()
+    ptrs = torch.tensor([base + off for off in offs], dtype=torch.int64, device=DEV)
+    lens = torch.tensor([len(c) for c in chunks], dtype=torch.int64, device=DEV)
+    return mem, ptrs, lens
+
+
+def test_device_visible():
+    assert torch.cuda.is_available()
+    info = z.device_info()
+    assert info["num_cus"] >= 1
+
+
+def test_kats_host_api(golden):
+    for k in golden["meta"]["kats"]:
+        if "text_seq" in k:
+            a, b = k["text_seq"]
+            data = "".join(f"{i}\n" for i in range(a, b + 1)).encode()
+        else:
+            data = bytes.fromhex(k["hex"])
+        assert z.cg_crc32(data) == k["crc"], k["name"]
+    assert z.cg_crc32(b"123456789") == 0xCBF43926
+    assert z.cg_crc32(b"123456789", 4) == zlib.crc32(b"1234")
+    assert z.fhandle_check_crc32(b"123456789", 0xCBF43926)
+    assert not z.fhandle_check_crc32(b"123456789", 0xCBF43927)
+
+
+def test_lengths_offsets_device(golden):
+    """Every length 0..1100 (and a sweep to 4096) at every 16-B misalignment."""
+    lo = golden["lo"]
+    base = o.payload(int(lo["payload_len"]), int(lo["payload_index"]))
+    mem = torch.from_numpy(np.concatenate([np.zeros(64, np.uint8), base, np.zeros(64, np.uint8)])).to(DEV)
+    b0 = mem.data_ptr() + 64
+    lengths = lo["lengths"].astype(np.int64)
+    L = np.repeat(lengths, 16)
+    off = np.tile(np.arange(16, dtype=np.int64), len(lengths))
+    ptrs = torch.tensor(b0 + off, dtype=torch.int64, device=DEV)
+    lens = torch.tensor(L, dtype=torch.int64, device=DEV)
+    got = u32(z.crc32_batch_device(ptrs, lens)).reshape(len(lengths), 16)
+    np.testing.assert_array_equal(got, lo["crc"])
+
+
+def test_seeds_and_chain_splits(golden):
+    chains = golden["meta"]["chains"]
+    datas = [o.payload(c["len"], c["index"]).tobytes() for c in chains]
+    mem, ptrs, lens = dev_buffers_from_host(datas, align=1, gap=3, lead=5)
+    seeds = torch.tensor(np.array([c["seed"] for c in chains], dtype=np.uint32).view(np.int32), device=DEV)
+    got = u32(z.crc32_batch_device(ptrs, lens, seeds=seeds))
+    assert list(got) == [c["crc"] for c in chains]
+    # chaining across two device calls: crc(tail, crc(head, seed))
+    cuts = [c["cut"] for c in chains]
+    heads = [d[:k] for d, k in zip(datas, cuts)]
+    tails = [d[k:] for d, k in zip(datas, cuts)]
+    m1, p1, l1 = dev_buffers_from_host(heads, align=1, gap=1)
+    h = z.crc32_batch_device(p1, l1, seeds=seeds)
+    m2, p2, l2 = dev_buffers_from_host(tails, align=1, gap=1)
+    got2 = u32(z.crc32_batch_device(p2, l2, seeds=h))
+    assert list(got2) == [c["crc"] for c in chains]
+
+
+def _strided_fill(n, length, stride=None, index0=0, index_step=1):
+    stride = stride or length
+    mem = torch.empty(max(n * stride, 1), dtype=torch.uint8, device=DEV)
+    ptrs = mem.data_ptr() + torch.arange(n, dtype=torch.int64, device=DEV) * stride
+    lens = torch.full((n,), length, dtype=torch.int64, device=DEV)
+    z.fill_synthetic(ptrs, lens, index0=index0, index_step=index_step, seed=SEED)
+    return mem, ptrs, lens
+
+
+def test_config2_full_bitexact(golden):
+    """Config 2: 4096 x 64 KiB, every CRC vs the reference's golden vector."""
+    mem, ptrs, lens = _strided_fill(4096, 65536)
+    exp = golden["cfg"]["cfg2"]
+    np.testing.assert_array_equal(u32(z.crc32_batch_device(ptrs, lens)), exp)
+    np.testing.assert_array_equal(u32(z.crc32_batch_strided(mem, 65536, 65536, 4096)), exp)
+    # the generator itself matches the CPU regeneration
+    host = mem[:65536 * 3].cpu().numpy()
+    for i in range(3):
+        np.testing.assert_array_equal(host[i * 65536:(i + 1) * 65536], o.payload(65536, i))
+
+
+def test_config1_and_config3_sample(golden):
+    meta, cfg = golden["meta"], golden["cfg"]
+    mem, ptrs, lens = _strided_fill(1, 1 << 20)
+    assert u32(z.crc32_batch_device(ptrs, lens))[0] == meta["config1"]["crc"]
+    idx = cfg["cfg3_idx"].astype(np.int64)
+    n = len(idx)
+    mem = torch.empty(n << 20, dtype=torch.uint8, device=DEV)
+    ptrs = mem.data_ptr() + (torch.arange(n, dtype=torch.int64, device=DEV) << 20)
+    lens = torch.full((n,), 1 << 20, dtype=torch.int64, device=DEV)
+    for k in range(n):  # payload index per buffer
+        z.fill_synthetic(ptrs[k:k + 1], lens[k:k + 1], index0=int(idx[k]), seed=SEED)
+    np.testing.assert_array_equal(u32(z.crc32_batch_device(ptrs, lens)), cfg["cfg3"])
+
+
+def test_config4_sample_zipf(golden):
+    """Config-4 size law: ragged lengths 1 KiB..16 MiB, packed unaligned."""
+    cfg = golden["cfg"]
+    idx = cfg["cfg4_idx"].astype(np.int64)
+    L = cfg["cfg4_len"].astype(np.int64)
+    offs = np.zeros(len(L), dtype=np.int64)
+    offs[1:] = np.cumsum(L + 3)[:-1]  # 3-byte gaps: starts are not 16-B aligned
+    mem = torch.empty(int(offs[-1] + L[-1] + 16), dtype=torch.uint8, device=DEV)
+    ptrs = mem.data_ptr() + 1 + torch.tensor(offs, device=DEV)
+    lens = torch.tensor(L, device=DEV)
+    for k in range(len(idx)):
+        z.fill_synthetic(ptrs[k:k + 1], lens[k:k + 1], index0=int(idx[k]), seed=SEED)
+    np.testing.assert_array_equal(u32(z.crc32_batch_device(ptrs, lens)), cfg["cfg4"])
+
+
+@pytest.mark.parametrize("n_bytes,lead", [(64 << 20, 0), ((64 << 20) + 3, 5), (300_000_007, 11)])
+def test_single_large_buffer_split_across_waves(n_bytes, lead):
+    mem = torch.empty(n_bytes + 64, dtype=torch.uint8, device=DEV)
+    ptrs = torch.tensor([mem.data_ptr() + lead], dtype=torch.int64, device=DEV)
+    lens = torch.tensor([n_bytes], dtype=torch.int64, device=DEV)
+    z.fill_synthetic(ptrs, lens, index0=42, seed=SEED)
+    got = int(u32(z.crc32_batch_device(ptrs, lens))[0])
+    assert got == o.payload_crc(n_bytes, 42)
+    seeds = torch.tensor([0x1234567], dtype=torch.int32, device=DEV)
+    got_s = int(u32(z.crc32_batch_device(ptrs, lens, seeds=seeds))[0])
+    assert got_s == o.payload_crc(n_bytes, 42, crc=0x1234567)
+
+
+def test_empty_and_tiny_buffers():
+    datas = [b"", b"a", b"ab", b"abc", b"abcd", b"", b"\xff" * 5, b""]
+    mem, ptrs, lens = dev_buffers_from_host(datas, align=1)
+    seeds_np = np.array([0, 1, 0xFFFFFFFF, 7, 0, 99, 3, 0xDEADBEEF], dtype=np.uint32)
+    seeds = torch.tensor(seeds_np.view(np.int32), device=DEV)
+    got = u32(z.crc32_batch_device(ptrs, lens, seeds=seeds))
+    assert list(got) == [zlib.crc32(d, int(s)) for d, s in zip(datas, seeds_np)]
+    # a batch of only empty buffers returns the seeds
+    e = torch.zeros(3, dtype=torch.int64, device=DEV)
+    got = u32(z.crc32_batch_device(e + mem.data_ptr(), e, seeds=seeds[:3]))
+    assert list(got) == list(seeds_np[:3])
+
+
+def test_random_mixed_batches_vs_oracle():
+    rnd = random.Random(7)
+    for trial in range(4):
+        n = rnd.choice([1, 17, 500, 3000])
+        lens = [rnd.choice([rnd.randint(0, 40), rnd.randint(0, 5000), rnd.randint(0, 300_000),
+                            rnd.randint(0, 3_000_000)]) for _ in range(n)]
+        total = sum(lens) + 64 * n + 64
+        mem = torch.randint(0, 256, (total,), dtype=torch.uint8, device=DEV)
+        offs, pos = [], 0
+        for L in lens:
+            pos += rnd.randint(0, 48)
+            offs.append(pos)
+            pos += L
+        ptrs = torch.tensor([mem.data_ptr() + q for q in offs], dtype=torch.int64, device=DEV)
+        lt = torch.tensor(lens, dtype=torch.int64, device=DEV)
+        seeds_np = np.array([rnd.getrandbits(32) for _ in lens], dtype=np.uint32)
+        seeds = torch.tensor(seeds_np.view(np.int32), device=DEV)
+        got = u32(z.crc32_batch_device(ptrs, lt, seeds=seeds))
+        host = mem.cpu().numpy()
+        ap = np.array([host.ctypes.data + q for q in offs], dtype=np.uint64)
+        exp = o.crc32_batch(ap, np.array(lens, dtype=np.uint64), seeds_np, nthreads=8)
+        np.testing.assert_array_equal(got, exp, err_msg=f"trial {trial}")
+
+
+def test_strided_api_seeds_and_stride():
+    n, L, stride = 300, 200_000, 200_064
+    mem, ptrs, lens = _strided_fill(n, L, stride=stride, index0=1000)
+    seeds_np = np.arange(n, dtype=np.uint32) * 2654435761
+    seeds = torch.tensor(seeds_np.view(np.int32), device=DEV)
+    got = u32(z.crc32_batch_strided(mem, stride, L, n, seeds=seeds))
+    exp = [o.payload_crc(L, 1000 + i, crc=int(seeds_np[i])) for i in range(n)]
+    assert list(got) == exp
+
+
+def test_host_batch_api_staging_and_continuation():
+    """zcrc32_batch: pinned staging, several launches, a >64 MiB buffer split
+    into continuation parts (seed chained on the device)."""
+    rnd = random.Random(3)
+    bufs = [o.payload(L, i) for i, L in enumerate([0, 5, 70_000, 3_000_000, 100 << 20, 17, (64 << 20) - 5, 999])]
+    seeds = [rnd.getrandbits(32) for _ in bufs]
+    got = z.crc32_batch(bufs, seeds=seeds)
+    exp = [zlib.crc32(b.tobytes(), s) for b, s in zip(bufs, seeds)]
+    assert list(got) == exp
+    many = [o.payload(rnd.randint(0, 3000), 50 + i) for i in range(70_000)]  # > kStageItems per launch
+    got = z.crc32_batch(many)
+    assert list(got) == [zlib.crc32(b.tobytes()) for b in many]
+
+
+def test_tensors_helper_and_verify_entries():
+    ts = [torch.randint(0, 256, (L,), dtype=torch.uint8, device=DEV) for L in (0, 10, 4096, 123457)]
+    got = u32(z.crc32_tensors(ts))
+    assert list(got) == [zlib.crc32(t.cpu().numpy().tobytes()) for t in ts]
+    entries = [t.cpu().numpy() for t in ts]
+    exp = [zlib.crc32(e.tobytes()) for e in entries]
+    exp[2] ^= 1
+    assert list(z.verify_entries(entries, exp)) == [True, True, False, True]
+
+
+def test_profile_counts_launches():
+    mem, ptrs, lens = _strided_fill(64, 65536)
+    with z.profile() as p:
+        z.crc32_batch_device(ptrs, lens)
+        torch.cuda.synchronize()
+    assert p.launches == 1 and p.total_ms > 0

@@ -1,0 +1,82 @@
+"""CPU checks of the kernel's decomposition (tests/kernel_model.py mirrors
+zcrc_kernels.hip step by step) against the oracle, plus partition
+invariants of the wave-range snapping.  No GPU needed."""
+import random
+import zlib
+
+import numpy as np
+import pytest
+
+import kernel_model as km
+from oracle import oracle as o
+
+
+def _mk_batch(rnd, mem_size, lens, seeded=True, gap=40):
+    addrs, pos = [], rnd.randint(0, 15)
+    for L in lens:
+        addrs.append(pos)
+        pos += L + rnd.randint(0, gap)
+    assert pos <= mem_size
+    seeds = [rnd.getrandbits(32) for _ in lens] if seeded else None
+    return addrs, seeds
+
+
+@pytest.mark.parametrize("num_cus", [1, 2, 256])
+def test_model_matches_oracle(num_cus):
+    rnd = random.Random(num_cus)
+    mem = np.random.default_rng(num_cus).integers(0, 256, size=4_500_000, dtype=np.uint8)
+    lens = [0, 1, 2, 3, 4, 5, 15, 16, 17, 1023, 1024, 1025, 4095, 4097, 65535, 65536, 131071, 131072,
+            131073, 262145, 1_200_007] + [rnd.randint(0, 9000) for _ in range(40)] + [2_000_000]
+    addrs, seeds = _mk_batch(rnd, mem.size, lens)
+    b = km.Batch(mem, addrs, lens, seeds)
+    got = km.run_batch(b, num_cus=num_cus)
+    exp = [o.cg_crc32(mem[a:a + L], s) for a, L, s in zip(addrs, lens, seeds)]
+    assert list(got) == exp
+
+
+def test_model_all_empty_and_single():
+    mem = np.zeros(64, dtype=np.uint8)
+    b = km.Batch(mem, [0, 0, 0], [0, 0, 0], [0, 5, 0xFFFFFFFF])
+    assert list(km.run_batch(b)) == [0, 5, 0xFFFFFFFF]
+    b = km.Batch(mem, [3], [9], [0])
+    assert list(km.run_batch(b)) == [zlib.crc32(mem[3:12].tobytes())]
+
+
+def _check_partition(b, num_cus):
+    cover = {i: [] for i in range(b.n)}
+    for (s0, s1, last) in km.wave_ranges(b, num_cus):
+        for (i, lo, hi) in km.wave_pieces(b, s0, s1, last):
+            cover[i].append((lo, hi))
+    for i in range(b.n):
+        n = b.lens[i]
+        pcs = sorted(cover[i])
+        assert pcs, f"buffer {i} not visited"
+        assert pcs[0][0] == 0 and pcs[-1][1] == n
+        for (a0, a1), (c0, c1) in zip(pcs, pcs[1:]):
+            assert a1 == c0, "pieces must tile the buffer"
+        if len(pcs) > 1:
+            assert n >= km.K_SPLIT_MIN, "small buffers are never split"
+            for lo, hi in pcs:
+                assert hi - lo >= km.K_MIN_PIECE
+                assert (n - hi) % km.K_SPLIT_GRAIN == 0
+        else:
+            assert pcs[0] == (0, n)
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_partition_invariants(seed):
+    rnd = random.Random(100 + seed)
+    n = rnd.choice([1, 5, 300, 3000])
+    kinds = [lambda: 0, lambda: rnd.randint(0, 64), lambda: rnd.randint(0, 70000),
+             lambda: rnd.randint(100000, 3_000_000), lambda: 1 << 20]
+    lens = [rnd.choice(kinds)() for _ in range(n)]
+    mem = np.zeros(1, dtype=np.uint8)
+    b = km.Batch(mem, [0] * n, lens)
+    for num_cus in (1, 3, 256):
+        _check_partition(b, num_cus)
+
+
+def test_partition_config4_shape():
+    lens = [int(x) for x in o.zipf_lens(100000)]
+    b = km.Batch(np.zeros(1, dtype=np.uint8), [0] * len(lens), lens)
+    _check_partition(b, 256)

@@ -1,0 +1,234 @@
+"""Host-side mirror of ZIPsFS's CRC-32 interface, backed by libzcrc (GPU only).
+
+Reference interface (christophgil/ZIPsFS):
+  * ``static uint32_t cg_crc32(const void *data, size_t n_bytes, uint32_t crc,
+    pthread_mutex_t *mutex)`` -- src/cg_crc32.c:26; zlib crc32 semantics,
+    ``crc`` = previous CRC (0 for fresh), ``mutex`` only guards lazy table
+    init (src/cg_crc32.c:31-36) and is accepted and ignored here.
+  * ``static bool fhandle_check_crc32(fHandle_t *d)`` --
+    src/ZIPsFS_preloadfileram.c:237-250: CRC of the fully preloaded entry
+    (seed 0) compared with the central-directory CRC; mismatch -> warning
+    and ``false``, never an exception.
+
+Everything is computed on the MI355X by libzcrc's HIP kernels.  Missing
+library or GPU errors raise ``ZcrcError``: there is no CPU fallback.
+"""
+from __future__ import annotations
+
+import ctypes
+import sys
+from typing import Iterable, Optional, Sequence
+
+import numpy as np
+
+from ._lib import ZcrcError, check, lib
+
+__all__ = [
+    "ZcrcError", "cg_crc32", "crc32_batch", "crc32_batch_device", "crc32_batch_device_ws",
+    "crc32_batch_strided", "crc32_tensors", "crc32_combine", "fhandle_check_crc32",
+    "verify_entries", "fill_synthetic", "profile", "device_info", "version",
+]
+
+
+def _host_view(data) -> tuple:
+    """(keepalive, address, nbytes) of a bytes-like / numpy host buffer."""
+    if isinstance(data, np.ndarray):
+        arr = np.ascontiguousarray(data)
+        return arr, arr.ctypes.data, arr.nbytes
+    mv = memoryview(data)
+    if not mv.contiguous:
+        raise ValueError("buffer must be contiguous")
+    nbytes = mv.nbytes
+    if nbytes == 0:
+        return mv, None, 0
+    if mv.readonly:
+        arr = np.frombuffer(mv, dtype=np.uint8)
+        return arr, arr.ctypes.data, nbytes
+    buf = (ctypes.c_char * nbytes).from_buffer(mv)
+    return (mv, buf), ctypes.addressof(buf), nbytes
+
+
+def cg_crc32(data, n_bytes: Optional[int] = None, crc: int = 0, mutex=None) -> int:
+    """Mirror of ``cg_crc32(data, n_bytes, crc, mutex)`` (src/cg_crc32.c:26).
+
+    ``data`` is host memory (bytes, bytearray, memoryview, numpy array).
+    ``n_bytes`` defaults to the whole buffer; ``mutex`` is ignored.
+    """
+    del mutex
+    keep, addr, nbytes = _host_view(data)
+    n = nbytes if n_bytes is None else int(n_bytes)
+    if n < 0 or n > nbytes:
+        raise ValueError(f"n_bytes={n} outside buffer of {nbytes} bytes")
+    out = ctypes.c_uint32(0)
+    check(lib().zcrc32_checked(addr, n, crc & 0xFFFFFFFF, ctypes.byref(out)), "zcrc32")
+    del keep
+    return int(out.value)
+
+
+def crc32_batch(buffers: Sequence, seeds: Optional[Iterable[int]] = None) -> np.ndarray:
+    """CRC of many host buffers in as few GPU launches as the staging allows."""
+    views = [_host_view(b) for b in buffers]
+    n = len(views)
+    ptrs = (ctypes.c_void_p * max(n, 1))(*[v[1] for v in views])
+    lens = (ctypes.c_size_t * max(n, 1))(*[v[2] for v in views])
+    out = np.zeros(n, dtype=np.uint32)
+    sp = None
+    if seeds is not None:
+        s = np.ascontiguousarray(np.asarray(list(seeds), dtype=np.uint64) & 0xFFFFFFFF, dtype=np.uint32)
+        if s.size != n:
+            raise ValueError("seeds length mismatch")
+        sp = s.ctypes.data
+    check(lib().zcrc32_batch(ptrs, lens, sp, out.ctypes.data, n, 0), "zcrc32_batch")
+    del views
+    return out
+
+
+def fhandle_check_crc32(entry, zipcrc32: int, path: str = "") -> bool:
+    """Mirror of fhandle_check_crc32 (src/ZIPsFS_preloadfileram.c:237-250)."""
+    computed = cg_crc32(entry, None, 0)
+    if computed != (zipcrc32 & 0xFFFFFFFF):
+        print(f"crc32-mismatch!  ZIP: {zipcrc32:x} != computed: {computed:x} size={len(memoryview(entry))} {path}",
+              file=sys.stderr)
+        return False
+    return True
+
+
+def verify_entries(entries: Sequence, expected: Sequence[int]) -> np.ndarray:
+    """Batched fhandle_check_crc32: one GPU pass over many preloaded entries."""
+    got = crc32_batch(entries)
+    return got == (np.asarray(expected, dtype=np.uint64) & 0xFFFFFFFF).astype(np.uint32)
+
+
+def crc32_combine(crc_a: int, crc_b: int, len_b: int) -> int:
+    """crc32(A||B) from crc32(A), crc32(B), |B| (zlib crc32_combine)."""
+    return int(lib().zcrc32_combine(crc_a & 0xFFFFFFFF, crc_b & 0xFFFFFFFF, int(len_b)))
+
+
+# ------------------------------------------------------------ device API
+
+def _torch():
+    import torch
+    return torch
+
+
+def _stream_ptr(stream):
+    torch = _torch()
+    if stream is None:
+        stream = torch.cuda.current_stream()
+    return ctypes.c_void_p(stream.cuda_stream)
+
+
+def _check_dev(t, name, dtype=None):
+    torch = _torch()
+    if not isinstance(t, torch.Tensor) or not t.is_cuda:
+        raise TypeError(f"{name} must be a CUDA (HIP) tensor")
+    if not t.is_contiguous():
+        raise ValueError(f"{name} must be contiguous")
+    if dtype is not None and t.dtype != dtype:
+        raise TypeError(f"{name} must be {dtype}, got {t.dtype}")
+
+
+def crc32_batch_device(ptrs, lens, seeds=None, out=None, stream=None):
+    """Device-resident batch.  ``ptrs``/``lens``: int64 device tensors of n
+    device addresses / byte counts; ``seeds``: optional int32/uint32 device
+    tensor; returns (or fills) an int32 device tensor of CRCs (uint32 bits)."""
+    torch = _torch()
+    _check_dev(ptrs, "ptrs", torch.int64)
+    _check_dev(lens, "lens", torch.int64)
+    n = ptrs.numel()
+    if lens.numel() != n:
+        raise ValueError("ptrs/lens length mismatch")
+    if out is None:
+        out = torch.empty(n, dtype=torch.int32, device=ptrs.device)
+    _check_dev(out, "out")
+    sp = None
+    if seeds is not None:
+        _check_dev(seeds, "seeds")
+        sp = seeds.data_ptr()
+    check(lib().zcrc32_batch_device(ptrs.data_ptr(), lens.data_ptr(), sp, out.data_ptr(), n, _stream_ptr(stream)),
+          "zcrc32_batch_device")
+    return out
+
+
+def crc32_batch_device_ws(ptrs, lens, scratch, seeds=None, out=None, stream=None):
+    """As crc32_batch_device with caller-owned scratch (graph-capturable)."""
+    torch = _torch()
+    _check_dev(ptrs, "ptrs", torch.int64)
+    _check_dev(lens, "lens", torch.int64)
+    _check_dev(scratch, "scratch")
+    n = ptrs.numel()
+    if out is None:
+        out = torch.empty(n, dtype=torch.int32, device=ptrs.device)
+    sp = None if seeds is None else seeds.data_ptr()
+    check(lib().zcrc32_batch_device_ws(ptrs.data_ptr(), lens.data_ptr(), sp, out.data_ptr(), n,
+                                       scratch.data_ptr(), scratch.numel() * scratch.element_size(),
+                                       _stream_ptr(stream)), "zcrc32_batch_device_ws")
+    return out
+
+
+def scratch_bytes(n: int) -> int:
+    return int(lib().zcrc32_batch_device_scratch_bytes(n))
+
+
+def crc32_batch_strided(base, stride: int, length: int, n: int, seeds=None, out=None, stream=None,
+                        base_offset: int = 0):
+    """Equal-size chunks: buffer i = base + base_offset + i*stride, ``length`` bytes."""
+    torch = _torch()
+    _check_dev(base, "base")
+    need = base_offset + (n - 1) * stride + length if n else 0
+    if need > base.numel() * base.element_size():
+        raise ValueError("strided batch exceeds the base tensor")
+    if out is None:
+        out = torch.empty(n, dtype=torch.int32, device=base.device)
+    sp = None if seeds is None else seeds.data_ptr()
+    check(lib().zcrc32_batch_device_strided(base.data_ptr() + base_offset, stride, length, n, sp, out.data_ptr(),
+                                            _stream_ptr(stream)), "zcrc32_batch_device_strided")
+    return out
+
+
+def crc32_tensors(tensors: Sequence, seeds=None, stream=None):
+    """CRC of each device tensor's bytes (one batched launch)."""
+    torch = _torch()
+    if not tensors:
+        return torch.empty(0, dtype=torch.int32)
+    dev = tensors[0].device
+    ptrs = torch.tensor([t.data_ptr() for t in tensors], dtype=torch.int64, device=dev)
+    lens = torch.tensor([t.numel() * t.element_size() for t in tensors], dtype=torch.int64, device=dev)
+    return crc32_batch_device(ptrs, lens, seeds=seeds, stream=stream)
+
+
+def fill_synthetic(ptrs, lens, index0: int = 0, index_step: int = 1, seed: int = 0xC0FFEE, stream=None) -> None:
+    """Fill device buffers with the SURVEY 8(d) counter-based payload."""
+    torch = _torch()
+    _check_dev(ptrs, "ptrs", torch.int64)
+    _check_dev(lens, "lens", torch.int64)
+    check(lib().zcrc_fill_synthetic(ptrs.data_ptr(), lens.data_ptr(), ptrs.numel(), index0, index_step, seed,
+                                    _stream_ptr(stream)), "zcrc_fill_synthetic")
+
+
+class profile:
+    """Context manager: HIP-event timing of the main CRC kernel launches."""
+
+    def __enter__(self):
+        lib().zcrc_profile_reset()
+        lib().zcrc_profile_enable(1)
+        return self
+
+    def __exit__(self, *exc):
+        lib().zcrc_profile_enable(0)
+        ms = ctypes.c_double(0)
+        cnt = ctypes.c_int(0)
+        check(lib().zcrc_profile_read(ctypes.byref(ms), ctypes.byref(cnt)), "zcrc_profile_read")
+        self.total_ms = float(ms.value)
+        self.launches = int(cnt.value)
+        return False
+
+
+def device_info() -> dict:
+    a, b, c = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+    check(lib().zcrc_device_info(ctypes.byref(a), ctypes.byref(b), ctypes.byref(c)), "zcrc_device_info")
+    return {"num_cus": a.value, "major": b.value, "minor": c.value}
+
+
+def version() -> str:
+    return lib().zcrc_version().decode()

@@ -1,0 +1,54 @@
+// zcrc_internal.h -- shared constants and launch interfaces (not public ABI).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace zcrc {
+
+constexpr int kWaves = 16;                     // waves per workgroup (one WG per CU)
+constexpr int kThreads = kWaves * 64;          // 1024
+constexpr uint32_t kDepth = 6;                 // 1 KiB blocks in flight per wave
+constexpr uint64_t kMinRange = 256ull << 10;   // minimum bytes per wave range
+constexpr uint64_t kSplitGrain = 64ull << 10;  // split points: end-relative multiples
+constexpr uint64_t kSplitMin = 2 * kSplitGrain;  // buffers below this are never split
+constexpr uint64_t kMinPiece = 4096;           // no split piece shorter than this
+constexpr uint32_t kLdsBytes = 163840;         // all 160 KiB of the CU's LDS
+constexpr uint32_t kLdsCombDword = 32768;      // combine tables start at 128 KiB
+constexpr uint32_t kPlanPerThread = 8;
+constexpr uint64_t kPlanTile = 1024 * kPlanPerThread;
+// one launch covers at most this many bytes (keeps every piece < 2 GiB)
+constexpr uint64_t kMaxLaunchBytes = 1ull << 42;
+
+// Multiply-by-constant tables, uploaded once per device (~101 KiB).
+struct TableBlob {
+  uint32_t braid[4 * 256];       // MCT(x^(8*1024)): the hot-loop table
+  uint32_t comb[8 * 4 * 256];    // x^-32, x^-64, x^-128 .. x^-4096 (combine tree)
+  uint32_t tshift[16 * 4 * 256]; // x^(-8t), t = 0..15 (16-B alignment padding)
+  uint32_t stdtab[256];          // standard byte table (buffers < 4 bytes)
+  uint32_t x8pow[64];            // x^(8 * 2^k)
+};
+
+struct BatchArgs {
+  // general form: device array of device pointers + exclusive prefix of lens
+  const uint8_t *const *ptrs;
+  const uint64_t *prefix;  // n+1 entries
+  // strided form: buffer i = base + i*stride, length len
+  const uint8_t *base;
+  uint64_t stride;
+  uint64_t len;
+  const uint32_t *seeds;  // nullable: all-zero seeds (fresh CRC)
+  uint32_t *out;
+  uint64_t n;
+  const TableBlob *tab;
+};
+
+hipError_t launch_batch(const BatchArgs &args, bool strided, int num_cus, hipStream_t stream);
+hipError_t launch_plan(const uint64_t *d_lens, uint64_t n, uint64_t *d_prefix, uint64_t *d_tile_sum,
+                       uint32_t *d_out, hipStream_t stream);
+
+}  // namespace zcrc
+
+namespace zcrc {
+hipError_t launch_fill_synthetic(const uint64_t *d_ptrs, const uint64_t *d_lens, uint64_t n, uint64_t index0,
+                                 uint64_t index_step, uint64_t seed, hipStream_t stream);
+}  // namespace zcrc

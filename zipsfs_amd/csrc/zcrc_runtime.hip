@@ -1,0 +1,490 @@
+// zcrc_runtime.hip -- host runtime and C ABI of libzcrc (include/zcrc.h).
+//
+// Owns: per-device table upload (once, thread-safe), per-thread pinned staging
+// for host-resident batches, stream-ordered scratch for device batches, and
+// optional HIP-event profiling of the main kernel.  There is deliberately no
+// CPU CRC anywhere in this library: every byte is checksummed on the GPU and
+// every failure is reported (or, for the void-error zcrc32(), aborts).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <algorithm>
+#include <atomic>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "../../include/zcrc.h"
+#include "zcrc_gf2.h"
+#include "zcrc_internal.h"
+
+namespace zcrc {
+namespace {
+
+thread_local std::string t_last_error;
+
+int fail(int code, const std::string &msg) {
+  t_last_error = msg;
+  return code;
+}
+
+#define ZCRC_HIP_TRY(expr)                                                                       \
+  do {                                                                                           \
+    hipError_t e_ = (expr);                                                                      \
+    if (e_ != hipSuccess)                                                                        \
+      return fail(ZCRC_ERR_HIP, std::string(#expr " -> ") + hipGetErrorString(e_));              \
+  } while (0)
+
+// ------------------------------------------------------------- tables
+
+void build_tables(TableBlob &tb) {
+  XPowTable xp;
+  build_xpow_table(xp);
+  build_mct(gf2_xpow8(xp, 1024), tb.braid);
+  const uint32_t comb_bytes[8] = {4, 8, 16, 32, 64, 128, 256, 512};
+  for (int c = 0; c < 8; c++) build_mct(gf2_xinvpow8_small(comb_bytes[c]), tb.comb + c * 1024);
+  for (int t = 0; t < 16; t++) build_mct(gf2_xinvpow8_small((uint32_t)t), tb.tshift + t * 1024);
+  build_std_table(tb.stdtab);
+  for (int k = 0; k < 64; k++) tb.x8pow[k] = xp.x2k[k + 3];
+}
+
+const TableBlob &host_tables() {
+  static TableBlob tb;
+  static std::once_flag once;
+  std::call_once(once, [] { build_tables(tb); });
+  return tb;
+}
+
+const XPowTable &host_xpow() {
+  static XPowTable xp;
+  static std::once_flag once;
+  std::call_once(once, [] { build_xpow_table(xp); });
+  return xp;
+}
+
+// ------------------------------------------------------------- devices
+
+struct DeviceCtx {
+  bool ready = false;
+  int num_cus = 0;
+  int arch_major = 0, arch_minor = 0;
+  TableBlob *d_tab = nullptr;
+};
+
+std::mutex g_dev_mu;
+std::vector<DeviceCtx> g_devs;
+
+int device_ctx(DeviceCtx **out) {
+  int dev = 0;
+  ZCRC_HIP_TRY(hipGetDevice(&dev));
+  std::lock_guard<std::mutex> lk(g_dev_mu);
+  if (g_devs.empty()) {
+    int n = 0;
+    ZCRC_HIP_TRY(hipGetDeviceCount(&n));
+    if (n <= 0) return fail(ZCRC_ERR_HIP, "no HIP device visible");
+    g_devs.resize((size_t)n);
+  }
+  if (dev < 0 || (size_t)dev >= g_devs.size()) return fail(ZCRC_ERR_HIP, "bad current device");
+  DeviceCtx &c = g_devs[(size_t)dev];
+  if (!c.ready) {
+    hipDeviceProp_t prop;
+    ZCRC_HIP_TRY(hipGetDeviceProperties(&prop, dev));
+    if (strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+      return fail(ZCRC_ERR_HIP, std::string("libzcrc is built for gfx950 only, device is ") + prop.gcnArchName);
+    if (prop.sharedMemPerBlock < kLdsBytes)
+      return fail(ZCRC_ERR_HIP, "device LDS per workgroup below 160 KiB");
+    c.num_cus = prop.multiProcessorCount;
+    c.arch_major = prop.major;
+    c.arch_minor = prop.minor;
+    TableBlob *d = nullptr;
+    ZCRC_HIP_TRY(hipMalloc(&d, sizeof(TableBlob)));
+    hipError_t e = hipMemcpy(d, &host_tables(), sizeof(TableBlob), hipMemcpyHostToDevice);
+    if (e != hipSuccess) {
+      (void)hipFree(d);
+      return fail(ZCRC_ERR_HIP, std::string("table upload: ") + hipGetErrorString(e));
+    }
+    c.d_tab = d;
+    c.ready = true;
+  }
+  *out = &c;
+  return ZCRC_OK;
+}
+
+// ------------------------------------------------------------- profiling
+
+std::atomic<int> g_prof_on{0};
+std::mutex g_prof_mu;
+std::vector<std::pair<hipEvent_t, hipEvent_t>> g_prof_pending;
+double g_prof_ms = 0.0;
+int g_prof_count = 0;
+
+int launch_main(const BatchArgs &args, bool strided, const DeviceCtx &dc, hipStream_t stream) {
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+  const bool prof = g_prof_on.load(std::memory_order_relaxed) != 0;
+  if (prof) {
+    ZCRC_HIP_TRY(hipEventCreate(&e0));
+    ZCRC_HIP_TRY(hipEventCreate(&e1));
+    ZCRC_HIP_TRY(hipEventRecord(e0, stream));
+  }
+  ZCRC_HIP_TRY(launch_batch(args, strided, dc.num_cus, stream));
+  if (prof) {
+    ZCRC_HIP_TRY(hipEventRecord(e1, stream));
+    std::lock_guard<std::mutex> lk(g_prof_mu);
+    g_prof_pending.emplace_back(e0, e1);
+  }
+  return ZCRC_OK;
+}
+
+// ------------------------------------------------------------- device batch
+
+int batch_device_ws(const void *const *d_ptrs, const uint64_t *d_lens, const uint32_t *d_seeds,
+                    uint32_t *d_out, size_t n, void *scratch, size_t scratch_bytes, hipStream_t stream) {
+  if (n == 0) return ZCRC_OK;
+  if (!d_ptrs || !d_lens || !d_out || !scratch) return fail(ZCRC_ERR_ARG, "null argument");
+  if (scratch_bytes < zcrc32_batch_device_scratch_bytes(n)) return fail(ZCRC_ERR_ARG, "scratch too small");
+  DeviceCtx *dc = nullptr;
+  int rc = device_ctx(&dc);
+  if (rc) return rc;
+  uint64_t *d_prefix = static_cast<uint64_t *>(scratch);
+  uint64_t *d_tiles = d_prefix + (n + 1);
+  ZCRC_HIP_TRY(launch_plan(d_lens, n, d_prefix, d_tiles, d_out, stream));
+  BatchArgs a{};
+  a.ptrs = reinterpret_cast<const uint8_t *const *>(d_ptrs);
+  a.prefix = d_prefix;
+  a.seeds = d_seeds;
+  a.out = d_out;
+  a.n = n;
+  a.tab = dc->d_tab;
+  return launch_main(a, false, *dc, stream);
+}
+
+// ------------------------------------------------------------- host batch
+// Per-thread staging: two slots, each a pinned host area + a device area of
+// kStageBytes for payload and metadata.  Slot s is filled by the CPU while
+// the GPU works on slot s^1 (own stream per slot).
+
+constexpr size_t kStageBytes = 64ull << 20;
+constexpr size_t kStageItems = 1u << 16;
+
+struct StageSlot {
+  hipStream_t stream = nullptr;
+  hipEvent_t done = nullptr;    // slot reusable after this
+  hipEvent_t kernel = nullptr;  // kernel finished (continuation seeds)
+  uint8_t *h_data = nullptr, *d_data = nullptr;
+  // metadata: ptrs[kStageItems] | prefix[kStageItems+1] | seeds[kStageItems] | res[kStageItems]
+  uint8_t *h_meta = nullptr, *d_meta = nullptr;
+  bool busy = false;
+  // pending result scatter: (out index, slot item) after `done`
+  std::vector<std::pair<size_t, uint32_t>> scatter;
+};
+
+constexpr size_t kMetaPtrs = 0;
+constexpr size_t kMetaPrefix = kMetaPtrs + 8 * kStageItems;
+constexpr size_t kMetaSeeds = kMetaPrefix + 8 * (kStageItems + 1);
+constexpr size_t kMetaRes = kMetaSeeds + 4 * kStageItems;
+constexpr size_t kMetaBytes = kMetaRes + 4 * kStageItems;
+
+struct HostCtx {
+  int dev = -1;
+  StageSlot slot[2];
+  ~HostCtx() {
+    for (auto &s : slot) {
+      if (s.stream) (void)hipStreamSynchronize(s.stream);
+      if (s.h_data) (void)hipHostFree(s.h_data);
+      if (s.h_meta) (void)hipHostFree(s.h_meta);
+      if (s.d_data) (void)hipFree(s.d_data);
+      if (s.d_meta) (void)hipFree(s.d_meta);
+      if (s.done) (void)hipEventDestroy(s.done);
+      if (s.kernel) (void)hipEventDestroy(s.kernel);
+      if (s.stream) (void)hipStreamDestroy(s.stream);
+    }
+  }
+};
+
+thread_local HostCtx t_host;
+
+int host_ctx_init() {
+  int dev = 0;
+  ZCRC_HIP_TRY(hipGetDevice(&dev));
+  if (t_host.dev == dev) return ZCRC_OK;
+  if (t_host.dev != -1) return fail(ZCRC_ERR_ARG, "host staging bound to another device in this thread");
+  for (auto &s : t_host.slot) {
+    ZCRC_HIP_TRY(hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking));
+    ZCRC_HIP_TRY(hipEventCreateWithFlags(&s.done, hipEventDisableTiming));
+    ZCRC_HIP_TRY(hipEventCreateWithFlags(&s.kernel, hipEventDisableTiming));
+    ZCRC_HIP_TRY(hipHostMalloc(reinterpret_cast<void **>(&s.h_data), kStageBytes, hipHostMallocDefault));
+    ZCRC_HIP_TRY(hipHostMalloc(reinterpret_cast<void **>(&s.h_meta), kMetaBytes, hipHostMallocDefault));
+    ZCRC_HIP_TRY(hipMalloc(reinterpret_cast<void **>(&s.d_data), kStageBytes));
+    ZCRC_HIP_TRY(hipMalloc(reinterpret_cast<void **>(&s.d_meta), kMetaBytes));
+  }
+  t_host.dev = dev;
+  return ZCRC_OK;
+}
+
+// Parallel memcpy into pinned staging (large copies use a few threads).
+void stage_copy(uint8_t *dst, const uint8_t *src, size_t bytes) {
+  constexpr size_t kPar = 8ull << 20;
+  if (bytes < kPar) {
+    memcpy(dst, src, bytes);
+    return;
+  }
+  const int nt = 4;
+  const size_t part = ((bytes / nt) + 4095) & ~size_t(4095);
+  std::thread th[nt - 1];
+  for (int t = 1; t < nt; t++) {
+    const size_t off = part * (size_t)t;
+    if (off >= bytes) break;
+    const size_t len = std::min(part, bytes - off);
+    th[t - 1] = std::thread([=] { memcpy(dst + off, src + off, len); });
+  }
+  memcpy(dst, src, std::min(part, bytes));
+  for (auto &x : th)
+    if (x.joinable()) x.join();
+}
+
+int slot_finish(StageSlot &s, uint32_t *out) {
+  if (!s.busy) return ZCRC_OK;
+  ZCRC_HIP_TRY(hipEventSynchronize(s.done));
+  const uint32_t *res = reinterpret_cast<const uint32_t *>(s.h_meta + kMetaRes);
+  for (auto &p : s.scatter) out[p.first] = res[p.second];
+  s.scatter.clear();
+  s.busy = false;
+  return ZCRC_OK;
+}
+
+int batch_host(const void *const *ptrs, const size_t *lens, const uint32_t *seeds, uint32_t *out, size_t n) {
+  if (n == 0) return ZCRC_OK;
+  if (!ptrs || !lens || !out) return fail(ZCRC_ERR_ARG, "null argument");
+  DeviceCtx *dc = nullptr;
+  int rc = device_ctx(&dc);
+  if (rc) return rc;
+  rc = host_ctx_init();
+  if (rc) return rc;
+
+  int cur = 0;
+  size_t i = 0;          // next buffer
+  size_t part_off = 0;   // bytes of buffer i already submitted (large buffers)
+  int prev_slot = -1;    // slot of the previous launch
+  uint32_t prev_item = 0;  // its last item (continuation source)
+  while (i < n) {
+    StageSlot &s = t_host.slot[cur];
+    rc = slot_finish(s, out);
+    if (rc) return rc;
+    uint64_t *h_ptrs = reinterpret_cast<uint64_t *>(s.h_meta + kMetaPtrs);
+    uint64_t *h_prefix = reinterpret_cast<uint64_t *>(s.h_meta + kMetaPrefix);
+    uint32_t *h_seeds = reinterpret_cast<uint32_t *>(s.h_meta + kMetaSeeds);
+    size_t used = 0, items = 0;
+    bool continuation = false;  // item 0 continues the previous launch's last item
+    uint64_t pos = 0;
+    while (i < n && items < kStageItems) {
+      const uint8_t *src = static_cast<const uint8_t *>(ptrs[i]);
+      const size_t len = lens[i];
+      const size_t remaining = len - part_off;
+      const size_t room = kStageBytes - used;
+      if (remaining > room && items > 0) break;  // next launch
+      const size_t take = std::min(remaining, room);
+      if (take && !src) return fail(ZCRC_ERR_ARG, "null buffer pointer");
+      if (take) stage_copy(s.h_data + used, src + part_off, take);
+      h_ptrs[items] = reinterpret_cast<uint64_t>(s.d_data + used);
+      h_prefix[items] = pos;
+      h_seeds[items] = (part_off == 0 && seeds) ? seeds[i] : 0u;
+      if (part_off != 0) continuation = true;  // only ever item 0
+      pos += take;
+      used = (used + take + 15) & ~size_t(15);
+      const bool done_buf = (take == remaining);
+      if (done_buf) {
+        s.scatter.emplace_back(i, (uint32_t)items);
+        i++;
+        part_off = 0;
+      } else {
+        part_off += take;
+      }
+      items++;
+      if (!done_buf) break;  // a partial buffer always ends its launch
+    }
+    h_prefix[items] = pos;
+    ZCRC_HIP_TRY(hipMemcpyAsync(s.d_data, s.h_data, used, hipMemcpyHostToDevice, s.stream));
+    ZCRC_HIP_TRY(hipMemcpyAsync(s.d_meta, s.h_meta, kMetaRes, hipMemcpyHostToDevice, s.stream));
+    uint32_t *d_seeds = reinterpret_cast<uint32_t *>(s.d_meta + kMetaSeeds);
+    uint32_t *d_res = reinterpret_cast<uint32_t *>(s.d_meta + kMetaRes);
+    // The copies above overlap the previous launch's kernel; everything below
+    // is ordered after it (kernels use the whole GPU anyway).  This also keeps
+    // a continuation's read of the other slot's results ahead of that slot's
+    // next memset.
+    if (prev_slot >= 0) ZCRC_HIP_TRY(hipStreamWaitEvent(s.stream, t_host.slot[prev_slot].kernel, 0));
+    if (continuation) {
+      StageSlot &p = t_host.slot[prev_slot];
+      ZCRC_HIP_TRY(hipMemcpyAsync(d_seeds, reinterpret_cast<uint32_t *>(p.d_meta + kMetaRes) + prev_item, 4,
+                                  hipMemcpyDeviceToDevice, s.stream));
+    }
+    BatchArgs a{};
+    a.ptrs = reinterpret_cast<const uint8_t *const *>(s.d_meta + kMetaPtrs);
+    a.prefix = reinterpret_cast<const uint64_t *>(s.d_meta + kMetaPrefix);
+    a.seeds = d_seeds;
+    a.out = d_res;
+    a.n = items;
+    a.tab = dc->d_tab;
+    // split pieces xor into d_res: zero it first
+    ZCRC_HIP_TRY(hipMemsetAsync(d_res, 0, 4 * items, s.stream));
+    rc = launch_main(a, false, *dc, s.stream);
+    if (rc) return rc;
+    ZCRC_HIP_TRY(hipEventRecord(s.kernel, s.stream));
+    ZCRC_HIP_TRY(hipMemcpyAsync(s.h_meta + kMetaRes, d_res, 4 * items, hipMemcpyDeviceToHost, s.stream));
+    ZCRC_HIP_TRY(hipEventRecord(s.done, s.stream));
+    s.busy = true;
+    prev_slot = cur;
+    prev_item = (uint32_t)(items - 1);
+    cur ^= 1;
+  }
+  rc = slot_finish(t_host.slot[cur], out);
+  if (rc) return rc;
+  return slot_finish(t_host.slot[cur ^ 1], out);
+}
+
+}  // namespace
+}  // namespace zcrc
+
+// ================================================================= C ABI
+
+using namespace zcrc;
+
+extern "C" {
+
+const char *zcrc_last_error(void) { return t_last_error.c_str(); }
+
+const char *zcrc_version(void) { return "zcrc 0.1 (gfx950, braided slice-by-4, LDS x32)"; }
+
+int zcrc32_checked(const void *data, size_t n_bytes, uint32_t crc, uint32_t *out_crc) {
+  if (!out_crc) return fail(ZCRC_ERR_ARG, "null out_crc");
+  if (n_bytes && !data) return fail(ZCRC_ERR_ARG, "null data");
+  const void *ptrs[1] = {data};
+  const size_t lens[1] = {n_bytes};
+  const uint32_t seeds[1] = {crc};
+  return batch_host(ptrs, lens, seeds, out_crc, 1);
+}
+
+uint32_t zcrc32(const void *data, size_t n_bytes, uint32_t crc) {
+  uint32_t r = 0;
+  const int rc = zcrc32_checked(data, n_bytes, crc, &r);
+  if (rc != ZCRC_OK) {
+    fprintf(stderr, "libzcrc: GPU CRC-32 failed (%d): %s -- aborting (no CPU fallback)\n", rc,
+            t_last_error.c_str());
+    abort();
+  }
+  return r;
+}
+
+int zcrc32_batch(const void *const *ptrs, const size_t *lens, const uint32_t *seeds_or_null, uint32_t *out,
+                 size_t n, unsigned flags) {
+  (void)flags;
+  return batch_host(ptrs, lens, seeds_or_null, out, n);
+}
+
+size_t zcrc32_batch_device_scratch_bytes(size_t n) {
+  const size_t tiles = n == 0 ? 1 : (n + kPlanTile - 1) / kPlanTile;
+  return 8 * (n + 1) + 8 * tiles;
+}
+
+int zcrc32_batch_device_ws(const void *const *d_ptrs, const uint64_t *d_lens, const uint32_t *d_seeds_or_null,
+                           uint32_t *d_out, size_t n, void *d_scratch, size_t scratch_bytes, void *stream) {
+  return batch_device_ws(d_ptrs, d_lens, d_seeds_or_null, d_out, n, d_scratch, scratch_bytes,
+                         static_cast<hipStream_t>(stream));
+}
+
+int zcrc32_batch_device(const void *const *d_ptrs, const uint64_t *d_lens, const uint32_t *d_seeds_or_null,
+                        uint32_t *d_out, size_t n, void *stream) {
+  if (n == 0) return ZCRC_OK;
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  const size_t bytes = zcrc32_batch_device_scratch_bytes(n);
+  void *scratch = nullptr;
+  ZCRC_HIP_TRY(hipMallocAsync(&scratch, bytes, st));
+  const int rc = batch_device_ws(d_ptrs, d_lens, d_seeds_or_null, d_out, n, scratch, bytes, st);
+  const hipError_t e = hipFreeAsync(scratch, st);
+  if (rc) return rc;
+  if (e != hipSuccess) return fail(ZCRC_ERR_HIP, std::string("hipFreeAsync: ") + hipGetErrorString(e));
+  return ZCRC_OK;
+}
+
+int zcrc32_batch_device_strided(const void *d_base, uint64_t stride, uint64_t len, size_t n,
+                                const uint32_t *d_seeds_or_null, uint32_t *d_out, void *stream) {
+  if (n == 0) return ZCRC_OK;
+  if (!d_base || !d_out) return fail(ZCRC_ERR_ARG, "null argument");
+  if (n > 1 && stride < len) return fail(ZCRC_ERR_ARG, "stride < len");
+  DeviceCtx *dc = nullptr;
+  int rc = device_ctx(&dc);
+  if (rc) return rc;
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  // keep every launch under kMaxLaunchBytes of payload
+  const size_t per = len ? (size_t)std::max<uint64_t>(1, kMaxLaunchBytes / len) : n;
+  for (size_t first = 0; first < n; first += per) {
+    const size_t cnt = std::min(per, n - first);
+    BatchArgs a{};
+    a.base = static_cast<const uint8_t *>(d_base) + first * stride;
+    a.stride = stride;
+    a.len = len;
+    a.seeds = d_seeds_or_null ? d_seeds_or_null + first : nullptr;
+    a.out = d_out + first;
+    a.n = cnt;
+    a.tab = dc->d_tab;
+    if (len >= kSplitMin) ZCRC_HIP_TRY(hipMemsetAsync(a.out, 0, 4 * cnt, st));
+    rc = launch_main(a, true, *dc, st);
+    if (rc) return rc;
+  }
+  return ZCRC_OK;
+}
+
+uint32_t zcrc32_combine(uint32_t crc_a, uint32_t crc_b, uint64_t len_b) {
+  return gf2_crc_combine(host_xpow(), crc_a, crc_b, len_b);
+}
+
+int zcrc_device_info(int *num_cus, int *arch_major, int *arch_minor) {
+  DeviceCtx *dc = nullptr;
+  const int rc = device_ctx(&dc);
+  if (rc) return rc;
+  if (num_cus) *num_cus = dc->num_cus;
+  if (arch_major) *arch_major = dc->arch_major;
+  if (arch_minor) *arch_minor = dc->arch_minor;
+  return ZCRC_OK;
+}
+
+int zcrc_fill_synthetic(const uint64_t *d_ptrs, const uint64_t *d_lens, size_t n, uint64_t index0,
+                        uint64_t index_step, uint64_t seed, void *stream) {
+  ZCRC_HIP_TRY(launch_fill_synthetic(d_ptrs, d_lens, n, index0, index_step, seed, static_cast<hipStream_t>(stream)));
+  return ZCRC_OK;
+}
+
+void zcrc_profile_enable(int on) { g_prof_on.store(on ? 1 : 0); }
+
+int zcrc_profile_read(double *total_ms, int *launches) {
+  std::lock_guard<std::mutex> lk(g_prof_mu);
+  for (auto &p : g_prof_pending) {
+    hipError_t e = hipEventSynchronize(p.second);
+    if (e != hipSuccess) return fail(ZCRC_ERR_HIP, std::string("profile sync: ") + hipGetErrorString(e));
+    float ms = 0.f;
+    e = hipEventElapsedTime(&ms, p.first, p.second);
+    if (e != hipSuccess) return fail(ZCRC_ERR_HIP, std::string("profile elapsed: ") + hipGetErrorString(e));
+    g_prof_ms += ms;
+    g_prof_count++;
+    (void)hipEventDestroy(p.first);
+    (void)hipEventDestroy(p.second);
+  }
+  g_prof_pending.clear();
+  if (total_ms) *total_ms = g_prof_ms;
+  if (launches) *launches = g_prof_count;
+  return ZCRC_OK;
+}
+
+void zcrc_profile_reset(void) {
+  double ms;
+  int c;
+  (void)zcrc_profile_read(&ms, &c);
+  std::lock_guard<std::mutex> lk(g_prof_mu);
+  g_prof_ms = 0.0;
+  g_prof_count = 0;
+}
+
+}  // extern "C"
