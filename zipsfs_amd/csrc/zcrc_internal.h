@@ -7,8 +7,8 @@ namespace zcrc {
 
 constexpr int kWaves = 16;                     // waves per workgroup (one WG per CU)
 constexpr int kThreads = kWaves * 64;          // 1024
-constexpr uint32_t kDepth = 6;                 // 1 KiB blocks in flight per wave
-constexpr uint64_t kMinRange = 256ull << 10;   // minimum bytes per wave range
+constexpr uint32_t kDepth = 4;                 // 1 KiB blocks in flight per wave
+constexpr uint64_t kMinRange = 64ull << 10;    // default minimum bytes per wave range
 constexpr uint64_t kSplitGrain = 64ull << 10;  // split points: end-relative multiples
 constexpr uint64_t kSplitMin = 2 * kSplitGrain;  // buffers below this are never split
 constexpr uint64_t kMinPiece = 4096;           // no split piece shorter than this
@@ -40,6 +40,7 @@ struct BatchArgs {
   uint32_t *out;
   uint64_t n;
   const TableBlob *tab;
+  uint64_t min_range;  // bytes per wave at least (0 = kMinRange)
 };
 
 hipError_t launch_batch(const BatchArgs &args, bool strided, int num_cus, hipStream_t stream);

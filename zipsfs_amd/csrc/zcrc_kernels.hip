@@ -1,347 +1,12 @@
-// zcrc_kernels.hip -- MI355X (gfx950) batched CRC-32 kernels.
-//
-// Replaces the hot loop of ZIPsFS src/cg_crc32.c:37-47 (slice-by-8 table CRC
-// over one contiguous RAM buffer, called from fhandle_check_crc32,
-// src/ZIPsFS_preloadfileram.c:243) with one persistent launch that checksums
-// a whole batch of independent buffers, bit-exact to zlib crc32(seed, ...).
-//
-// Design (DESIGN.md has the full derivation):
-//   * One 1024-thread workgroup per CU (16 waves); the whole 160 KiB LDS holds
-//     - a *braided* slice-by-4 table, MCT(x^(8*1024)), replicated 32x so that
-//       every lookup of a 32-lane LDS group hits its own bank (conflict-free
-//       ds_read_b32 for any data), laid out so that ONE v_perm_b32 turns a
-//       data byte into a ready LDS address;
-//     - 8 small multiply-by-constant tables for the end-of-piece combine.
-//   * Each wave streams 1 KiB blocks: lane l loads 16 B at block + 16 l with
-//     one buffer_load_dwordx4 (fully coalesced), 8 blocks in flight.  Lane l
-//     runs 4 independent CRC streams (one per dword); every stream advances
-//     by exactly 1024 bytes per block, so one table serves all 256 streams:
-//         s <- (s xor word) * x^(8*1024)      (4 lookups)
-//   * At the end of a piece the 256 stream registers are folded with
-//     constant shifts (in-lane x^-32/x^-64, then a 6-level cross-lane tree of
-//     x^(-128*2^j)) into one raw register, moved to the piece end with a
-//     global-memory MCT (x^(-8t), t = bytes of 16-B alignment padding).
-//   * Work split: the concatenated batch (sum of lengths T) is cut into W
-//     equal byte ranges, one per wave, with boundaries snapped so that small
-//     buffers are never split and split points in large buffers sit at an
-//     end-relative 64 KiB grid.  Pieces of a split buffer are moved to the
-//     buffer end (x^(8d)) and xor-combined with one atomicXor each.
-//   * Bytes outside [piece start, piece end) inside the two boundary 16-B
-//     chunks are zeroed in-register; leading padding is free in the raw
-//     domain, trailing padding is undone by x^(-8t).  The seed (~crc) is
-//     xored into the buffer's first four bytes (zlib chaining semantics).
+// zcrc_kernels.hip -- instantiations of the batched CRC-32 kernel, the plan
+// (prefix-scan) kernels and their launchers.  The kernel itself lives in
+// zcrc_batch_kernel.h (shared with the measurement tools under tools/).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
-#include "zcrc_gf2.h"
-#include "zcrc_internal.h"
+#include "zcrc_batch_kernel.h"
 
 namespace zcrc {
-
-// ----------------------------------------------------------------- helpers
-
-__device__ __forceinline__ uint32_t lds_u32(const uint32_t *lds, uint32_t byte_addr) {
-  return *reinterpret_cast<const uint32_t *>(reinterpret_cast<const char *>(lds) + byte_addr);
-}
-
-// Braided table lookup address for table j (byte j of x):
-//   LDS byte address = (j>>1)*65536 + v*256 + (j&1)*128 + (lane&31)*4
-// laneoff[j] carries bytes 0 and 2; v_perm drops data byte j into byte 1.
-#define ZCRC_SEL(j) (0x0C020400u + ((uint32_t)(j) << 8))
-
-__device__ __forceinline__ uint32_t braid_step(const uint32_t *lds, uint32_t x, uint32_t o0, uint32_t o1,
-                                               uint32_t o2, uint32_t o3) {
-  const uint32_t a0 = __builtin_amdgcn_perm(x, o0, ZCRC_SEL(0));
-  const uint32_t a1 = __builtin_amdgcn_perm(x, o1, ZCRC_SEL(1));
-  const uint32_t a2 = __builtin_amdgcn_perm(x, o2, ZCRC_SEL(2));
-  const uint32_t a3 = __builtin_amdgcn_perm(x, o3, ZCRC_SEL(3));
-  return lds_u32(lds, a0) ^ lds_u32(lds, a1) ^ lds_u32(lds, a2) ^ lds_u32(lds, a3);
-}
-
-// r * c for one of the 8 combine constants resident in LDS.
-__device__ __forceinline__ uint32_t comb_apply(const uint32_t *lds, int c, uint32_t r) {
-  const uint32_t *t = lds + kLdsCombDword + c * 1024;
-  return t[r & 0xFFu] ^ t[256 + ((r >> 8) & 0xFFu)] ^ t[512 + ((r >> 16) & 0xFFu)] ^ t[768 + (r >> 24)];
-}
-
-// r * c for a multiply-by-constant table in global memory (L2-resident).
-__device__ __forceinline__ uint32_t mct_apply_global(const uint32_t *t, uint32_t r) {
-  return t[r & 0xFFu] ^ t[256 + ((r >> 8) & 0xFFu)] ^ t[512 + ((r >> 16) & 0xFFu)] ^ t[768 + (r >> 24)];
-}
-
-// r * x^(8*nbytes), nbytes arbitrary (split pieces only: once per wave range).
-__device__ uint32_t shift_bytes(const TableBlob *tab, uint32_t r, uint64_t nbytes) {
-  int k = 0;
-  while (nbytes) {
-    if (nbytes & 1u) r = gf2_mul(tab->x8pow[k], r);
-    nbytes >>= 1;
-    k++;
-  }
-  return r;
-}
-
-__device__ __forceinline__ uint32_t lowmask_bytes(int k) {
-  return k <= 0 ? 0u : (k >= 4 ? 0xFFFFFFFFu : ((1u << (8 * k)) - 1u));
-}
-
-// Zero the bytes of a 16-B lane chunk outside [lo, hi) (chunk-relative byte
-// offsets) and xor the 4-byte seed injection at chunk offset io.
-__device__ __forceinline__ uint4 fix_chunk(uint4 d, int lo, int hi, int io, uint32_t inj) {
-  uint32_t w[4] = {d.x, d.y, d.z, d.w};
-#pragma unroll
-  for (int q = 0; q < 4; q++) {
-    const uint32_t m = lowmask_bytes(hi - 4 * q) & ~lowmask_bytes(lo - 4 * q);
-    uint32_t v = w[q] & m;
-    const int o = io - 4 * q;
-    if (o >= 0 && o < 4) v ^= inj << (8 * o);
-    if (o < 0 && o > -4) v ^= inj >> (-8 * o);
-    w[q] = v;
-  }
-  return make_uint4(w[0], w[1], w[2], w[3]);
-}
-
-__device__ __forceinline__ int clamp_rel(int32_t v) { return v < -64 ? -64 : (v > 64 ? 64 : v); }
-
-// Wave-uniform broadcast (lets hipcc keep descriptors and loop bounds in
-// SGPRs; without it every buffer_load gets a waterfall loop -- guide T20).
-__device__ __forceinline__ uint32_t uni32(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
-__device__ __forceinline__ uint64_t uni64(uint64_t v) {
-  return (uint64_t)uni32((uint32_t)v) | ((uint64_t)uni32((uint32_t)(v >> 32)) << 32);
-}
-
-// ------------------------------------------------------------ batch access
-
-template <bool kStrided>
-struct BatchView {
-  const BatchArgs &a;
-  __device__ uint64_t prefix(uint64_t i) const { return kStrided ? i * a.len : a.prefix[i]; }
-  __device__ const uint8_t *ptr(uint64_t i) const { return kStrided ? a.base + i * a.stride : a.ptrs[i]; }
-  __device__ uint32_t seed(uint64_t i) const { return a.seeds ? a.seeds[i] : 0u; }
-  __device__ uint64_t total() const { return kStrided ? a.n * a.len : a.prefix[a.n]; }
-
-  // First i in [0, n] with prefix(i) >= t (prefix(n) = total >= t).  Wave-wide
-  // 64-ary search; every lane returns the same value.
-  __device__ uint64_t lower_bound(uint64_t t) const {
-    if (kStrided) {
-      if (a.len == 0) return t == 0 ? 0 : a.n;
-      const uint64_t i = (t + a.len - 1) / a.len;
-      return i < a.n ? i : a.n;
-    }
-    const uint32_t lane = threadIdx.x & 63u;
-    uint64_t lo = 0, hi = a.n;
-    while (hi - lo > 63) {
-      const uint64_t step = (hi - lo + 63) / 64;
-      uint64_t idx = lo + (uint64_t)(lane + 1) * step;
-      if (idx > hi) idx = hi;
-      const uint64_t m = __ballot(a.prefix[idx] >= t);
-      const uint32_t f = (uint32_t)__builtin_ctzll(m);
-      const uint64_t nhi = (lo + (uint64_t)(f + 1) * step) < hi ? (lo + (uint64_t)(f + 1) * step) : hi;
-      const uint64_t nlo = f == 0 ? lo : lo + (uint64_t)f * step + 1;
-      lo = uni64(nlo);
-      hi = uni64(nhi);
-    }
-    const uint64_t idx = lo + lane;
-    const bool ok = idx <= hi && a.prefix[idx <= hi ? idx : hi] >= t;
-    const uint64_t m = __ballot(ok);
-    return uni64(lo + (uint64_t)__builtin_ctzll(m));
-  }
-
-  // Snap a nominal wave boundary t so that buffers shorter than kSplitMin are
-  // never split and split points sit at end-relative multiples of kSplitGrain.
-  // Monotone non-decreasing in t, so snapped ranges stay ordered.
-  __device__ uint64_t snap(uint64_t t) const {
-    const uint64_t tot = total();
-    if (t == 0 || t >= tot) return t >= tot ? tot : 0;
-    const uint64_t i = lower_bound(t);
-    const uint64_t pi = prefix(i);
-    if (pi == t) return t;
-    const uint64_t b0 = prefix(i - 1);
-    const uint64_t n = pi - b0, p = t - b0;
-    if (n < kSplitMin) return pi;
-    const uint64_t q = n - kSplitGrain * ((n - p) / kSplitGrain);
-    if (q < kMinPiece) return b0;
-    return b0 + q;
-  }
-};
-
-// ------------------------------------------------------------ the kernel
-
-template <bool kStrided>
-__global__ __launch_bounds__(kThreads) void crc32_batch_kernel(BatchArgs args) {
-  __shared__ __attribute__((aligned(16))) uint32_t s_lds[kLdsBytes / 4];
-  const BatchView<kStrided> bv{args};
-  const TableBlob *tab = args.tab;
-
-  const uint64_t total = bv.total();
-  const uint64_t max_waves = (uint64_t)gridDim.x * kWaves;
-  uint64_t want = (total + kMinRange - 1) / kMinRange;
-  if (want < 1) want = 1;
-  const uint64_t W = want < max_waves ? want : max_waves;
-  if ((uint64_t)blockIdx.x * kWaves >= W) return;  // whole workgroup idle (uniform)
-
-  // ---- LDS fill: braided table x32 replicas + 8 combine tables ----------
-  {
-    const uint32_t tid = threadIdx.x;  // 0..1023 = (table j, byte v)
-    const uint32_t j = tid >> 8, v = tid & 255u;
-    const uint32_t val = tab->braid[tid];
-    const uint4 q = make_uint4(val, val, val, val);
-    char *dst = reinterpret_cast<char *>(s_lds) + (j >> 1) * 65536u + v * 256u + (j & 1u) * 128u;
-#pragma unroll
-    for (int r = 0; r < 8; r++) *reinterpret_cast<uint4 *>(dst + 16 * r) = q;
-    const uint4 *src = reinterpret_cast<const uint4 *>(tab->comb) + tid * 2;
-    uint4 *cdst = reinterpret_cast<uint4 *>(s_lds + kLdsCombDword) + tid * 2;
-    cdst[0] = src[0];
-    cdst[1] = src[1];
-  }
-  __syncthreads();
-
-  const uint32_t lane = threadIdx.x & 63u;
-  const uint64_t w = (uint64_t)blockIdx.x * kWaves + (threadIdx.x >> 6);
-  if (w >= W) return;  // no barrier after this point
-
-  // nominal boundary of wave k: floor(k * total / W), without 128-bit math
-  const uint64_t q_tot = total / W, r_tot = total % W;
-  const uint64_t S0 = uni64(bv.snap(q_tot * w + (r_tot * w) / W));
-  const uint64_t S1 = uni64((w + 1 == W) ? total : bv.snap(q_tot * (w + 1) + (r_tot * (w + 1)) / W));
-  const bool last_wave = (w + 1 == W);
-  if (S0 >= S1 && !last_wave) return;
-
-  // lane constants for the braided lookups
-  const uint32_t lo0 = (lane & 31u) * 4u;
-  const uint32_t o0 = lo0, o1 = lo0 + 128u, o2 = lo0 + 65536u, o3 = lo0 + 65536u + 128u;
-
-  uint64_t i = bv.lower_bound(S0);
-  if (i > 0 && i <= args.n && bv.prefix(i) > S0) i--;  // S0 strictly inside buffer i-1
-
-  i = uni64(i);
-  for (; i < args.n; i++) {
-    const uint64_t b0 = uni64(bv.prefix(i)), b1 = uni64(bv.prefix(i + 1));
-    if (b0 >= S1 && !last_wave) break;
-    const uint64_t n = b1 - b0;
-    const uint64_t rel_lo = (S0 > b0 ? S0 - b0 : 0);
-    const uint64_t rel_hi = (b1 < S1 || last_wave) ? n : S1 - b0;
-    const bool whole = (rel_lo == 0 && rel_hi == n);
-    const uint32_t seed = uni32(bv.seed(i));
-    const uint8_t *bptr = reinterpret_cast<const uint8_t *>(uni64(reinterpret_cast<uint64_t>(bv.ptr(i))));
-
-    if (n < 4) {  // tiny buffer: bytewise with the standard table (never split)
-      uint32_t r = ~seed;
-      for (uint32_t p = 0; p < (uint32_t)n; p++) r = (r >> 8) ^ tab->stdtab[(r ^ bptr[p]) & 0xFFu];
-      if (lane == 0) args.out[i] = ~r;
-      continue;
-    }
-
-    // ---- one piece: bytes [pstart, pend) of buffer i ----------------------
-    const uint64_t pstart = (uint64_t)bptr + rel_lo;
-    const uint64_t pend = (uint64_t)bptr + rel_hi;
-    const uint64_t astart = uni64(pstart & ~(uint64_t)15);
-    const uint64_t aend = uni64((pend + 15) & ~(uint64_t)15);
-    const uint32_t span = uni32((uint32_t)(aend - astart));  // < 2^31 (kMaxLaunchBytes)
-    const uint32_t K = uni32((span + 1023u) >> 10);
-    const uint32_t tpad = uni32((uint32_t)(aend - pend));
-    const uint32_t inj = uni32((rel_lo == 0) ? ~seed : 0u);
-    // chunk-relative bounds of lane's chunk in block 0: chunk address
-    // c(it) = astart + (span - 1024K) + 1024 it + 16 lane
-    // all chunk-relative offsets fit in int32 because span < 2^31
-    const int32_t c0 = (int32_t)span - 1024 * (int32_t)K + 16 * (int32_t)lane;  // rel. to astart
-    const int32_t rs = (int32_t)uni32((uint32_t)(pstart - astart));
-    const int32_t re = (int32_t)uni32((uint32_t)(pend - astart));
-
-    __amdgpu_buffer_rsrc_t rsrc =
-        __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void *>(astart), (short)0, (int)span, 0x00020000);
-    const uint32_t voff0 = (uint32_t)c0;  // negative wraps -> out of range -> zeros
-
-    uint32_t s0 = 0, s1 = 0, s2 = 0, s3 = 0;
-    // Two register groups of kDepth blocks: one streams in while the other
-    // is consumed (no register rotation, no vmcnt(0) at group boundaries).
-    uint4 ga[kDepth], gb[kDepth];
-
-#define ZCRC_LOADG(G, g)                                                                        \
-  {                                                                                             \
-    _Pragma("unroll") for (uint32_t u_ = 0; u_ < kDepth; u_++) {                                \
-      auto v_ = __builtin_amdgcn_raw_buffer_load_b128(rsrc, voff0 + 1024u * ((g) * kDepth + u_), \
-                                                      0, 0);                                    \
-      G[u_] = make_uint4(v_[0], v_[1], v_[2], v_[3]);                                           \
-    }                                                                                           \
-  }
-#define ZCRC_CONSUME(d)                                  \
-  {                                                      \
-    s0 = braid_step(s_lds, s0 ^ (d).x, o0, o1, o2, o3);  \
-    s1 = braid_step(s_lds, s1 ^ (d).y, o0, o1, o2, o3);  \
-    s2 = braid_step(s_lds, s2 ^ (d).z, o0, o1, o2, o3);  \
-    s3 = braid_step(s_lds, s3 ^ (d).w, o0, o1, o2, o3);  \
-  }
-  // plain group: every block strictly before block K-1, no fix-up needed
-#define ZCRC_PLAIN(G)                                                   \
-  {                                                                     \
-    _Pragma("unroll") for (uint32_t u_ = 0; u_ < kDepth; u_++) ZCRC_CONSUME(G[u_]); \
-  }
-  // edge group: bounds-checked, fix-ups on blocks 0, 1 and K-1
-#define ZCRC_EDGE(G, g)                                                                         \
-  {                                                                                             \
-    _Pragma("unroll") for (uint32_t u_ = 0; u_ < kDepth; u_++) {                                \
-      const uint32_t it_ = (g) * kDepth + u_;                                                   \
-      if (it_ < K) {                                                                            \
-        uint4 dd_ = G[u_];                                                                      \
-        if (it_ <= 1u || it_ + 1u == K) {                                                       \
-          const int32_t c_ = c0 + 1024 * (int32_t)it_;                                          \
-          dd_ = fix_chunk(dd_, clamp_rel(rs - c_), clamp_rel(re - c_), clamp_rel(rs - c_), inj); \
-        }                                                                                       \
-        ZCRC_CONSUME(dd_);                                                                      \
-      }                                                                                         \
-    }                                                                                           \
-  }
-
-    // Groups of kDepth blocks: group 0 and the last group are "edge" groups
-    // (bounds + fix-ups), groups 1..ngroups-2 are plain.  Loop invariant: gb
-    // holds group g, loaded; ga is free.
-    const uint32_t ngroups = (K + kDepth - 1) / kDepth;  // >= 1
-    ZCRC_LOADG(ga, 0u);
-    if (ngroups > 1) ZCRC_LOADG(gb, 1u);
-    ZCRC_EDGE(ga, 0u);
-    if (ngroups > 1) {
-      const uint32_t nplain = ngroups - 2;
-      uint32_t g = 1;
-      for (uint32_t pr = 0; pr < nplain / 2; pr++) {
-        ZCRC_LOADG(ga, g + 1);
-        ZCRC_PLAIN(gb);
-        ZCRC_LOADG(gb, g + 2);
-        ZCRC_PLAIN(ga);
-        g += 2;
-      }
-      if (nplain & 1u) {
-        ZCRC_LOADG(ga, g + 1);
-        ZCRC_PLAIN(gb);
-        ZCRC_EDGE(ga, g + 1);
-      } else {
-        ZCRC_EDGE(gb, g);
-      }
-    }
-#undef ZCRC_LOADG
-#undef ZCRC_CONSUME
-#undef ZCRC_PLAIN
-#undef ZCRC_EDGE
-
-    // ---- fold 256 stream registers into one raw register at `aend` -------
-    // stream (lane l, dword q) sits at aend + 16 l + 4 q
-    uint32_t r = (s0 ^ comb_apply(s_lds, 0, s1)) ^ comb_apply(s_lds, 1, s2 ^ comb_apply(s_lds, 0, s3));
-#pragma unroll
-    for (int j = 0; j < 6; j++) {
-      const uint32_t moved = __shfl_down(comb_apply(s_lds, 2 + j, r), 1u << j, 64);
-      r ^= moved;
-    }
-    r = __builtin_amdgcn_readfirstlane(r);
-    if (tpad) r = mct_apply_global(tab->tshift + tpad * 1024u, r);  // -> register at pend
-
-    if (whole) {
-      if (lane == 0) args.out[i] = ~r;
-    } else {
-      const uint64_t d = n - rel_hi;  // bytes after this piece, multiple of kSplitGrain
-      uint32_t contrib = d ? shift_bytes(tab, r, d) : (r ^ 0xFFFFFFFFu);
-      if (lane == 0) atomicXor(args.out + i, contrib);
-    }
-  }
-}
 
 // ------------------------------------------------------------ plan kernels
 // Exclusive prefix over lengths: prefix[0..n] (prefix[n] = total), and zero
@@ -429,9 +94,9 @@ __global__ __launch_bounds__(1024) void plan_tile_scan(const uint64_t *lens, uin
 hipError_t launch_batch(const BatchArgs &args, bool strided, int num_cus, hipStream_t stream) {
   const dim3 grid((unsigned)num_cus), block(kThreads);
   if (strided)
-    hipLaunchKernelGGL(crc32_batch_kernel<true>, grid, block, 0, stream, args);
+    hipLaunchKernelGGL((crc32_batch_kernel<true, kDepth, 0>), grid, block, 0, stream, args);
   else
-    hipLaunchKernelGGL(crc32_batch_kernel<false>, grid, block, 0, stream, args);
+    hipLaunchKernelGGL((crc32_batch_kernel<false, kDepth, 0>), grid, block, 0, stream, args);
   return hipGetLastError();
 }
 

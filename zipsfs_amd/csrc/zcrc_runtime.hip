@@ -21,6 +21,7 @@
 #include "../../include/zcrc.h"
 #include "zcrc_gf2.h"
 #include "zcrc_internal.h"
+#include "zcrc_tables.h"
 
 namespace zcrc {
 namespace {
@@ -40,17 +41,6 @@ int fail(int code, const std::string &msg) {
   } while (0)
 
 // ------------------------------------------------------------- tables
-
-void build_tables(TableBlob &tb) {
-  XPowTable xp;
-  build_xpow_table(xp);
-  build_mct(gf2_xpow8(xp, 1024), tb.braid);
-  const uint32_t comb_bytes[8] = {4, 8, 16, 32, 64, 128, 256, 512};
-  for (int c = 0; c < 8; c++) build_mct(gf2_xinvpow8_small(comb_bytes[c]), tb.comb + c * 1024);
-  for (int t = 0; t < 16; t++) build_mct(gf2_xinvpow8_small((uint32_t)t), tb.tshift + t * 1024);
-  build_std_table(tb.stdtab);
-  for (int k = 0; k < 64; k++) tb.x8pow[k] = xp.x2k[k + 3];
-}
 
 const TableBlob &host_tables() {
   static TableBlob tb;
