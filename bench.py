@@ -88,6 +88,7 @@ class Workload:
             self.mem.append(mem)
             self.batches.append((ptrs, lens))
             self.n_local = len(L)
+            self.n_total = 100000
             self.bytes_local = int(L.sum())
             self.desc = ("config4: 100k ZIP-entry-like buffers, bounded power law 1 KiB-16 MiB "
                          "(sum 13,123,505,587 B), 16-B aligned, round-robin over ranks")
@@ -108,30 +109,25 @@ class Workload:
             self.mem.append(mem)
             self.batches.append((ptrs, lens))
         self.n_local = n
+        self.n_total = n * self.world
         self.bytes_local = n * L
 
 
-def golden_check(cfg: int, world: int, out_all_np: np.ndarray, n_local: int) -> str:
-    """Compare gathered CRCs with the reference-generated fixtures (data only)."""
+def golden_check(cfg: int, glob: np.ndarray) -> str:
+    """Compare CRCs (global buffer order) with the reference-generated fixtures."""
     path = os.path.join(ROOT, "tests", "golden", "configs.npz")
     if not os.path.exists(path):
         return "skipped (no fixtures)"
     g = np.load(path)
-    # out_all_np is [world, n_local]; global index i = r + world*k -> [k, r]
-    glob = out_all_np.reshape(world, n_local).T.reshape(-1)
     if cfg == 3:
         idx, exp = g["cfg3_idx"].astype(np.int64), g["cfg3"]
     elif cfg == 2:
-        idx, exp = np.arange(4096 // world * world), g["cfg2"][: 4096 // world * world]
+        k = min(4096, len(glob))
+        idx, exp = np.arange(k), g["cfg2"][:k]
     elif cfg == 4:
         idx, exp = g["cfg4_idx"].astype(np.int64), g["cfg4"]
-        # config 4 shards are ragged: rebuild the global order explicitly
-        per = [np.arange(r, 100000, world) for r in range(world)]
-        glob = np.zeros(100000, dtype=np.uint32)
-        for r in range(world):
-            glob[per[r]] = out_all_np[r][: len(per[r])]
-    elif cfg == 5:
-        return "no fixture for config 5 (indices differ from config 3); see tests/"
+    else:
+        return "no fixture for config 5 (see tests/test_gpu_parity.py)"
     ok = int((glob[idx] == exp).sum())
     if ok != len(idx):
         raise SystemExit(f"PARITY FAILURE: {len(idx) - ok} of {len(idx)} sampled CRCs differ from the reference")
@@ -193,6 +189,8 @@ def main() -> None:
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", type=int, default=3, choices=[2, 3, 4, 5])
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                    help="nccl = RCCL over xGMI (default); gloo only to rehearse ranks sharing one GPU")
     ap.add_argument("--cpu-budget-s", type=float, default=12.0)
     ap.add_argument("--pmc-traffic-bytes", type=float, default=None,
                     help="HBM bytes per launch from a separate rocprofv3 --pmc pass (corrected)")
@@ -201,35 +199,37 @@ def main() -> None:
     import torch
     import torch.distributed as dist
     import zipsfs_amd as z
+    from zipsfs_amd import shard
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+    ndev = torch.cuda.device_count()
+    gpu = local % max(ndev, 1)
+    torch.cuda.set_device(gpu)
+    dev = torch.device("cuda", gpu)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group("gloo")
 
     def barrier():
         if world > 1:
-            dist.barrier(device_ids=[local])
+            if args.dist_backend == "nccl":
+                dist.barrier(device_ids=[gpu])
+            else:
+                dist.barrier()
 
     wl = Workload(args.config, rank, world, dev)
     out = torch.empty(wl.n_local, dtype=torch.int32, device=dev)
-    n_max = wl.n_local
-    if world > 1:
-        nt = torch.tensor([wl.n_local], device=dev)
-        dist.all_reduce(nt, op=dist.ReduceOp.MAX)
-        n_max = int(nt.item())
-    out_pad = torch.zeros(n_max, dtype=torch.int32, device=dev)
-    out_all = torch.empty(world * n_max, dtype=torch.int32, device=dev)
+    result = {"global": out}
 
     def step(s: int) -> None:
         ptrs, lens = wl.batches[s % len(wl.batches)]
         z.crc32_batch_device(ptrs, lens, out=out)
-        if world > 1:
-            out_pad[: wl.n_local].copy_(out)
-            dist.all_gather_into_tensor(out_all, out_pad)
+        if world > 1:  # the one exchange: all-gather of the 32-bit CRCs
+            result["global"] = shard.gather_crcs(out, wl.n_total)
 
     for s in range(args.warmup):
         step(s)
@@ -245,10 +245,11 @@ def main() -> None:
     barrier()
     elapsed = t1 - t0
     if world > 1:
-        et = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        rdev = dev if args.dist_backend == "nccl" else torch.device("cpu")
+        et = torch.tensor([elapsed], dtype=torch.float64, device=rdev)
         dist.all_reduce(et, op=dist.ReduceOp.MAX)
         elapsed = float(et.item())
-        bt = torch.tensor([wl.bytes_local], dtype=torch.int64, device=dev)
+        bt = torch.tensor([wl.bytes_local], dtype=torch.int64, device=rdev)
         dist.all_reduce(bt, op=dist.ReduceOp.SUM)
         bytes_all = int(bt.item())
     else:
@@ -258,17 +259,21 @@ def main() -> None:
     # sampled CRCs with the reference-generated golden vectors (data only)
     step(0)
     torch.cuda.synchronize()
-    if world == 1:
-        check_np = out.cpu().numpy().view(np.uint32).reshape(1, -1)
-    else:
-        check_np = out_all.cpu().numpy().view(np.uint32).reshape(world, n_max)
-    parity = golden_check(args.config, world, check_np, n_max) if rank == 0 else None
+    glob = result["global"].cpu().numpy().view(np.uint32)
+    parity = golden_check(args.config, glob) if rank == 0 else None
 
     ms_per_step = elapsed / args.steps * 1e3
     value = bytes_all * args.steps / elapsed / GiB
     avg_kernel_ms = prof.total_ms / max(prof.launches, 1)
     achieved = wl.bytes_local / (avg_kernel_ms * 1e-3) / 1e9
     traffic = args.pmc_traffic_bytes
+    traffic_src = "--pmc-traffic-bytes" if traffic is not None else None
+    pmc_path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    if traffic is None and os.path.exists(pmc_path):
+        pm = json.load(open(pmc_path))
+        if pm.get("config") == args.config and pm.get("bytes_per_gpu_per_step") == wl.bytes_local:
+            traffic = pm["traffic_bytes_per_launch"]
+            traffic_src = pm["source"]
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(args.config, args.cpu_budget_s)
@@ -278,7 +283,8 @@ def main() -> None:
             "metric": METRIC,
             "value": round(value, 2),
             "unit": "GiB/s",
-            "n_gpus": world,
+            "n_gpus": world if args.dist_backend == "nccl" else min(world, ndev),
+            "ranks": world,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(ms_per_step, 4),
@@ -292,7 +298,8 @@ def main() -> None:
                 "buffers_per_gpu": wl.n_local,
                 "bytes_per_gpu_per_step": wl.bytes_local,
                 "api": "zcrc32_batch_device (plan scan + persistent CRC kernel)" +
-                       (" + RCCL all_gather of uint32 CRCs" if world > 1 else ""),
+                       (f" + {'RCCL' if args.dist_backend == 'nccl' else 'gloo'} all_gather of uint32 CRCs"
+                        if world > 1 else ""),
                 "parallelism": f"round-robin buffer sharding over {world} GPU(s)",
             },
             "roofline": {
@@ -301,8 +308,11 @@ def main() -> None:
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
-                "traffic": traffic,
-                "kernel": "zcrc::crc32_batch_kernel<false>",
+                "traffic": None if traffic is None else int(traffic),
+                "traffic_unit": "bytes per launch (HBM read+write, PMC)",
+                "traffic_source": traffic_src,
+                "algorithmic_bytes_per_launch": wl.bytes_local,
+                "kernel": "zcrc::crc32_batch_kernel<false, 4u, 0, true>",
                 "avg_kernel_ms": round(avg_kernel_ms, 4),
                 "launches_timed": prof.launches,
             },
