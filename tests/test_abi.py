@@ -77,3 +77,22 @@ def test_missing_gpu_fails_loudly():
         pytest.skip("GPU present")
     with pytest.raises(zipsfs_amd.ZcrcError):
         zipsfs_amd.cg_crc32(b"123456789")
+
+
+REF_SRC = "/root/reference/src"
+
+
+@pytest.mark.skipif(not os.path.exists(os.path.join(REF_SRC, "cg_crc32.c")), reason="reference tree absent")
+def test_dropin_shadows_reference(tmp_path):
+    """INTEGRATION.md recipe: -include the drop-in ahead of a TU that does
+    `#include "cg_crc32.c"` from the reference's own src/; the reference body
+    must vanish behind the shared include guard and the call go to zcrc32."""
+    tu = tmp_path / "tu.c"
+    tu.write_text('#include "cg_crc32.c"\n'
+                  "uint32_t check(const void *p, size_t n) { return cg_crc32(p, n, 0, NULL); }\n")
+    obj = tmp_path / "tu.o"
+    subprocess.run(["gcc", "-c", "-O0", "-I", REF_SRC, "-I", os.path.join(ROOT, "include"),
+                    "-include", os.path.join(ROOT, "zipsfs_amd", "cg_crc32.c"), str(tu), "-o", str(obj)], check=True)
+    syms = subprocess.run(["nm", str(obj)], capture_output=True, text=True, check=True).stdout
+    assert " U zcrc32" in syms
+    assert "crc32_for_byte" not in syms and "cg_crc32_init_tables" not in syms
