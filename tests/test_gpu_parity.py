@@ -236,3 +236,27 @@ def test_profile_counts_launches():
         z.crc32_batch_device(ptrs, lens)
         torch.cuda.synchronize()
     assert p.launches == 1 and p.total_ms > 0
+
+
+def test_prefix_and_pointers_beyond_2_31_and_2_32():
+    """Batch whose prefix sums cross 2^31 and 2^32 (and whose device pointers
+    span > 4 GiB): 64-bit descriptor handling (readlane halves, no sign
+    extension) and many whole pieces per wave."""
+    from concurrent.futures import ThreadPoolExecutor
+    lens_np = np.array([400 << 20] * 11 + [123_456_789, 3, 0, 1_048_577], dtype=np.int64)
+    offs = np.zeros_like(lens_np)
+    offs[1:] = np.cumsum(lens_np + 7)[:-1]
+    mem = torch.empty(int(offs[-1] + lens_np[-1] + 64), dtype=torch.uint8, device=DEV)
+    ptrs = mem.data_ptr() + 5 + torch.tensor(offs, device=DEV)
+    lens = torch.tensor(lens_np, device=DEV)
+    z.fill_synthetic(ptrs, lens, index0=900, seed=SEED)
+    got = u32(z.crc32_batch_device(ptrs, lens))
+    with ThreadPoolExecutor(16) as ex:
+        exp = list(ex.map(lambda a: o.payload_crc(int(a[1]), 900 + a[0]), enumerate(lens_np)))
+    assert list(got) == exp
+    # same bytes as 1 MiB pieces through the strided API (many whole pieces per wave)
+    n = int(lens_np[:11].sum()) >> 20
+    got_s = u32(z.crc32_batch_strided(mem, 1 << 20, 1 << 20, n, base_offset=5))
+    host_first = mem[5:5 + (3 << 20)].cpu().numpy()
+    assert int(got_s[0]) == zlib.crc32(host_first[: 1 << 20].tobytes())
+    assert int(got_s[2]) == zlib.crc32(host_first[2 << 20: 3 << 20].tobytes())

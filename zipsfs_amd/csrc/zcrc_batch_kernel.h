@@ -105,7 +105,7 @@ __device__ __forceinline__ int clamp_rel(int32_t v) { return v < -64 ? -64 : (v 
 
 // Wave-uniform broadcast (lets hipcc keep descriptors and loop bounds in
 // SGPRs; without it every buffer_load gets a waterfall loop -- guide T20).
-__device__ __forceinline__ uint32_t uni32(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
+__device__ __forceinline__ uint32_t uni32(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane(v); }
 __device__ __forceinline__ uint64_t uni64(uint64_t v) {
   return (uint64_t)uni32((uint32_t)v) | ((uint64_t)uni32((uint32_t)(v >> 32)) << 32);
 }
@@ -177,11 +177,98 @@ struct BatchView {
 
 // kD: 1 KiB blocks per register group (two groups in flight); kAblate != 0
 // replaces the table lookups with one VALU op (measurement builds only).
+// One piece = bytes [rel_lo, rel_hi) of buffer i, with everything the stream
+// loop needs precomputed (all wave-uniform).
+struct Piece {
+  uint64_t i, n, rel_lo, rel_hi;
+  const uint8_t *bptr;
+  uint32_t seed;
+  bool whole, tiny;          // tiny: n < 4, bytewise path
+  uint64_t astart, pend;
+  uint32_t span, K, tpad, inj, voff0;
+  int32_t c0, rs, re;
+};
+
+// Descriptor of buffer i as a per-lane vector: lane 0 = prefix[i], lane 1 =
+// prefix[i+1], lane 2 = ptrs[i], lane 3 = seed.  Vector loads (vmcnt, in
+// order with the data loads) so that a prefetched descriptor never makes an
+// LDS wait (lgkmcnt) stall on an outstanding scalar load.
+template <bool kStrided>
+__device__ __forceinline__ uint64_t fetch_desc(const BatchView<kStrided> &bv, uint64_t i, uint32_t lane) {
+  if (kStrided) return 0;
+  const BatchArgs &a = bv.a;
+  uint64_t v = 0;
+  if (lane == 0) v = a.prefix[i];
+  else if (lane == 1) v = a.prefix[i + 1];
+  else if (lane == 2) v = reinterpret_cast<uint64_t>(a.ptrs[i]);
+  else if (lane == 3) v = a.seeds ? (uint64_t)a.seeds[i] : 0ull;
+  return v;
+}
+
+// __builtin_amdgcn_readlane returns a signed int: go through uint32_t, or the
+// low half is sign-extended over the high half of the 64-bit value.
+__device__ __forceinline__ uint64_t readlane64(uint64_t v, int l) {
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((uint32_t)v, l);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((uint32_t)(v >> 32), l);
+  return (uint64_t)lo | ((uint64_t)hi << 32);
+}
+
+template <bool kStrided>
+__device__ __forceinline__ Piece make_piece(const BatchView<kStrided> &bv, uint64_t i, uint64_t desc, uint64_t S0,
+                                            uint64_t S1, bool last_wave, uint32_t lane) {
+  Piece P;
+  uint64_t b0, b1;
+  if (kStrided) {
+    b0 = bv.prefix(i);
+    b1 = b0 + bv.a.len;
+    P.bptr = bv.ptr(i);
+    P.seed = uni32(bv.seed(i));
+  } else {
+    b0 = readlane64(desc, 0);
+    b1 = readlane64(desc, 1);
+    P.bptr = reinterpret_cast<const uint8_t *>(readlane64(desc, 2));
+    P.seed = (uint32_t)readlane64(desc, 3);
+  }
+  P.i = i;
+  P.n = b1 - b0;
+  P.rel_lo = S0 > b0 ? S0 - b0 : 0;
+  P.rel_hi = (b1 < S1 || last_wave) ? P.n : S1 - b0;
+  P.whole = (P.rel_lo == 0 && P.rel_hi == P.n);
+  P.tiny = P.n < 4;
+  const uint64_t pstart = (uint64_t)P.bptr + P.rel_lo;
+  P.pend = (uint64_t)P.bptr + P.rel_hi;
+  P.astart = uni64(pstart & ~(uint64_t)15);
+  const uint64_t aend = uni64((P.pend + 15) & ~(uint64_t)15);
+  P.span = uni32((uint32_t)(aend - P.astart));  // < 2^31 (kMaxLaunchBytes)
+  P.K = uni32((P.span + 1023u) >> 10);
+  P.tpad = uni32((uint32_t)(aend - P.pend));
+  P.inj = uni32(P.rel_lo == 0 ? ~P.seed : 0u);
+  // chunk address of lane l in block it: astart + c0 + 1024 it, c0 = span -
+  // 1024 K + 16 l; all chunk-relative offsets fit in int32 (span < 2^31)
+  P.c0 = (int32_t)P.span - 1024 * (int32_t)P.K + 16 * (int32_t)lane;
+  P.rs = (int32_t)uni32((uint32_t)(pstart - P.astart));
+  P.re = (int32_t)uni32((uint32_t)(P.pend - P.astart));
+  P.voff0 = (uint32_t)P.c0;  // negative wraps -> out of range -> zeros
+  return P;
+}
+
+// The descriptor must be provably wave-uniform or hipcc wraps every buffer
+// load in a waterfall loop (guide T20); Piece values carried across the
+// piece loop lose that proof, so re-assert it here.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t piece_rsrc(const Piece &P) {
+  return __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void *>(uni64(P.astart)), (short)0, (int)uni32(P.span),
+                                           0x00020000);
+}
+
+// kD: 1 KiB blocks per register group; kAblate != 0 replaces the table
+// lookups with one VALU op (measurement builds only); kRotate: per-wave
+// rotated piece order.
 template <bool kStrided, uint32_t kD = kDepth, int kAblate = 0, bool kRotate = true>
 __global__ __launch_bounds__(kThreads) void crc32_batch_kernel(BatchArgs args) {
   __shared__ __attribute__((aligned(16))) uint32_t s_lds[kLdsBytes / 4];
   const BatchView<kStrided> bv{args};
   const TableBlob *tab = args.tab;
+  const uint32_t lane = threadIdx.x & 63u;
 
   const uint64_t total = bv.total();
   const uint64_t max_waves = (uint64_t)gridDim.x * kWaves;
@@ -190,6 +277,57 @@ __global__ __launch_bounds__(kThreads) void crc32_batch_kernel(BatchArgs args) {
   if (want < 1) want = 1;
   const uint64_t W = want < max_waves ? want : max_waves;
   if ((uint64_t)blockIdx.x * kWaves >= W) return;  // whole workgroup idle (uniform)
+
+  // ---- this wave's range, first piece and its first loads ----------------
+  // (issued before the LDS fill so HBM latency overlaps the table setup)
+  const uint64_t w = (uint64_t)blockIdx.x * kWaves + (threadIdx.x >> 6);
+  bool active = w < W;
+  uint64_t S0 = 0, S1 = 0, i_first = 0, npieces = 0, rot = 0;
+  const bool last_wave = (w + 1 == W);
+  if (active) {
+    // nominal boundary of wave k: floor(k * total / W), without 128-bit math
+    const uint64_t q_tot = total / W, r_tot = total % W;
+    S0 = uni64(bv.snap(q_tot * w + (r_tot * w) / W));
+    S1 = uni64(last_wave ? total : bv.snap(q_tot * (w + 1) + (r_tot * (w + 1)) / W));
+    if (S0 >= S1 && !last_wave) {
+      active = false;
+    } else {
+      // buffers [i_first, i_end) overlap [S0, S1)
+      i_first = bv.lower_bound(S0);
+      if (i_first > 0 && i_first <= args.n && bv.prefix(i_first) > S0) i_first--;
+      i_first = uni64(i_first);
+      const uint64_t i_end = last_wave ? args.n : uni64(bv.lower_bound(S1));
+      npieces = i_end > i_first ? i_end - i_first : 0;
+      // Rotated piece order: pieces are independent, and the rotation
+      // de-phases waves whose ranges start on large power-of-two boundaries
+      // (partition camping over the HBM channel interleave, tools/hbm_probe).
+      rot = (kRotate && npieces > 1) ? (uint64_t)(hash32((uint32_t)w) % (uint32_t)npieces) : 0;
+      if (npieces == 0) active = false;
+    }
+  }
+
+  // piece k -> buffer index (rotated)
+#define ZCRC_IDX(k) (i_first + (((k) + rot) < npieces ? ((k) + rot) : ((k) + rot - npieces)))
+
+  uint4 gc[kD];  // group 0 of the current piece (prefetched)
+  Piece P;
+  // lane constants for the braided lookups
+  const uint32_t lo0 = (lane & 31u) * 4u;
+  const uint32_t o0 = lo0, o1 = lo0 + 128u, o2 = lo0 + 65536u, o3 = lo0 + 65536u + 128u;
+
+#define ZCRC_LOADG(G, Q, g)                                                                     \
+  {                                                                                             \
+    const __amdgpu_buffer_rsrc_t rs_ = piece_rsrc(Q);                                           \
+    _Pragma("unroll") for (uint32_t u_ = 0; u_ < kD; u_++) {                                    \
+      auto v_ = __builtin_amdgcn_raw_buffer_load_b128(rs_, (Q).voff0 + 1024u * ((g) * kD + u_), 0, 0);    \
+      G[u_] = make_uint4(v_[0], v_[1], v_[2], v_[3]);                                           \
+    }                                                                                           \
+  }
+
+  if (active) {
+    P = make_piece(bv, uni64(ZCRC_IDX(0)), fetch_desc(bv, ZCRC_IDX(0), lane), S0, S1, last_wave, lane);
+    if (!P.tiny) ZCRC_LOADG(gc, P, 0u);
+  }
 
   // ---- LDS fill: braided table x32 replicas + 8 combine tables ----------
   {
@@ -206,86 +344,10 @@ __global__ __launch_bounds__(kThreads) void crc32_batch_kernel(BatchArgs args) {
     cdst[1] = src[1];
   }
   __syncthreads();
+  if (!active) return;  // no barrier after this point
 
-  const uint32_t lane = threadIdx.x & 63u;
-  const uint64_t w = (uint64_t)blockIdx.x * kWaves + (threadIdx.x >> 6);
-  if (w >= W) return;  // no barrier after this point
+  uint4 ga[kD], gb[kD];
 
-  // nominal boundary of wave k: floor(k * total / W), without 128-bit math
-  const uint64_t q_tot = total / W, r_tot = total % W;
-  const uint64_t S0 = uni64(bv.snap(q_tot * w + (r_tot * w) / W));
-  const uint64_t S1 = uni64((w + 1 == W) ? total : bv.snap(q_tot * (w + 1) + (r_tot * (w + 1)) / W));
-  const bool last_wave = (w + 1 == W);
-  if (S0 >= S1 && !last_wave) return;
-
-  // lane constants for the braided lookups
-  const uint32_t lo0 = (lane & 31u) * 4u;
-  const uint32_t o0 = lo0, o1 = lo0 + 128u, o2 = lo0 + 65536u, o3 = lo0 + 65536u + 128u;
-
-  // Buffers [i_first, i_end) overlap this wave's range [S0, S1).
-  uint64_t i_first = bv.lower_bound(S0);
-  if (i_first > 0 && i_first <= args.n && bv.prefix(i_first) > S0) i_first--;  // S0 inside buffer i-1
-  i_first = uni64(i_first);
-  const uint64_t i_end = last_wave ? args.n : uni64(bv.lower_bound(S1));
-  const uint64_t npieces = i_end > i_first ? i_end - i_first : 0;
-  // Visit the pieces in a per-wave rotated order.  Pieces are independent,
-  // and the rotation de-phases waves whose ranges start on large power-of-two
-  // boundaries (uniform batches), which otherwise walk the HBM channel
-  // interleave in lockstep ("partition camping", tools/hbm_probe: up to -13%).
-  const uint64_t rot = (kRotate && npieces > 1) ? (uint64_t)(hash32((uint32_t)w) % (uint32_t)npieces) : 0;
-
-  for (uint64_t k = 0; k < npieces; k++) {
-    uint64_t i = i_first + k + rot;
-    if (i >= i_end) i -= npieces;
-    i = uni64(i);
-    const uint64_t b0 = uni64(bv.prefix(i)), b1 = uni64(bv.prefix(i + 1));
-    const uint64_t n = b1 - b0;
-    const uint64_t rel_lo = (S0 > b0 ? S0 - b0 : 0);
-    const uint64_t rel_hi = (b1 < S1 || last_wave) ? n : S1 - b0;
-    const bool whole = (rel_lo == 0 && rel_hi == n);
-    const uint32_t seed = uni32(bv.seed(i));
-    const uint8_t *bptr = reinterpret_cast<const uint8_t *>(uni64(reinterpret_cast<uint64_t>(bv.ptr(i))));
-
-    if (n < 4) {  // tiny buffer: bytewise with the standard table (never split)
-      uint32_t r = ~seed;
-      for (uint32_t p = 0; p < (uint32_t)n; p++) r = (r >> 8) ^ tab->stdtab[(r ^ bptr[p]) & 0xFFu];
-      if (lane == 0) args.out[i] = ~r;
-      continue;
-    }
-
-    // ---- one piece: bytes [pstart, pend) of buffer i ----------------------
-    const uint64_t pstart = (uint64_t)bptr + rel_lo;
-    const uint64_t pend = (uint64_t)bptr + rel_hi;
-    const uint64_t astart = uni64(pstart & ~(uint64_t)15);
-    const uint64_t aend = uni64((pend + 15) & ~(uint64_t)15);
-    const uint32_t span = uni32((uint32_t)(aend - astart));  // < 2^31 (kMaxLaunchBytes)
-    const uint32_t K = uni32((span + 1023u) >> 10);
-    const uint32_t tpad = uni32((uint32_t)(aend - pend));
-    const uint32_t inj = uni32((rel_lo == 0) ? ~seed : 0u);
-    // chunk-relative bounds of lane's chunk in block 0: chunk address
-    // c(it) = astart + (span - 1024K) + 1024 it + 16 lane
-    // all chunk-relative offsets fit in int32 because span < 2^31
-    const int32_t c0 = (int32_t)span - 1024 * (int32_t)K + 16 * (int32_t)lane;  // rel. to astart
-    const int32_t rs = (int32_t)uni32((uint32_t)(pstart - astart));
-    const int32_t re = (int32_t)uni32((uint32_t)(pend - astart));
-
-    __amdgpu_buffer_rsrc_t rsrc =
-        __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void *>(astart), (short)0, (int)span, 0x00020000);
-    const uint32_t voff0 = (uint32_t)c0;  // negative wraps -> out of range -> zeros
-
-    uint32_t s0 = 0, s1 = 0, s2 = 0, s3 = 0;
-    // Two register groups of kD blocks: one streams in while the other
-    // is consumed (no register rotation, no vmcnt(0) at group boundaries).
-    uint4 ga[kD], gb[kD];
-
-#define ZCRC_LOADG(G, g)                                                                        \
-  {                                                                                             \
-    _Pragma("unroll") for (uint32_t u_ = 0; u_ < kD; u_++) {                                \
-      auto v_ = __builtin_amdgcn_raw_buffer_load_b128(rsrc, voff0 + 1024u * ((g) * kD + u_), \
-                                                      0, 0);                                    \
-      G[u_] = make_uint4(v_[0], v_[1], v_[2], v_[3]);                                           \
-    }                                                                                           \
-  }
 #define ZCRC_STEP(x) (kAblate ? __builtin_amdgcn_alignbit((x), (x), 5) : braid_step(s_lds, (x), o0, o1, o2, o3))
 #define ZCRC_CONSUME(d)         \
   {                             \
@@ -295,56 +357,74 @@ __global__ __launch_bounds__(kThreads) void crc32_batch_kernel(BatchArgs args) {
     s3 = ZCRC_STEP(s3 ^ (d).w); \
   }
   // plain group: every block strictly before block K-1, no fix-up needed
-#define ZCRC_PLAIN(G)                                                   \
-  {                                                                     \
-    _Pragma("unroll") for (uint32_t u_ = 0; u_ < kD; u_++) ZCRC_CONSUME(G[u_]); \
+#define ZCRC_PLAIN(G)                                                                \
+  {                                                                                  \
+    _Pragma("unroll") for (uint32_t u_ = 0; u_ < kD; u_++) ZCRC_CONSUME(G[u_]);     \
   }
   // edge group: bounds-checked, fix-ups on blocks 0, 1 and K-1
-#define ZCRC_EDGE(G, g)                                                                         \
-  {                                                                                             \
-    _Pragma("unroll") for (uint32_t u_ = 0; u_ < kD; u_++) {                                \
-      const uint32_t it_ = (g) * kD + u_;                                                   \
-      if (it_ < K) {                                                                            \
-        uint4 dd_ = G[u_];                                                                      \
-        if (it_ <= 1u || it_ + 1u == K) {                                                       \
-          const int32_t c_ = c0 + 1024 * (int32_t)it_;                                          \
-          dd_ = fix_chunk(dd_, clamp_rel(rs - c_), clamp_rel(re - c_), clamp_rel(rs - c_), inj); \
-        }                                                                                       \
-        ZCRC_CONSUME(dd_);                                                                      \
-      }                                                                                         \
-    }                                                                                           \
+#define ZCRC_EDGE(G, g)                                                                               \
+  {                                                                                                   \
+    _Pragma("unroll") for (uint32_t u_ = 0; u_ < kD; u_++) {                                          \
+      const uint32_t it_ = (g) * kD + u_;                                                             \
+      if (it_ < P.K) {                                                                                \
+        uint4 dd_ = G[u_];                                                                            \
+        if (it_ <= 1u || it_ + 1u == P.K) {                                                           \
+          const int32_t c_ = P.c0 + 1024 * (int32_t)it_;                                              \
+          dd_ = fix_chunk(dd_, clamp_rel(P.rs - c_), clamp_rel(P.re - c_), clamp_rel(P.rs - c_), P.inj); \
+        }                                                                                             \
+        ZCRC_CONSUME(dd_);                                                                            \
+      }                                                                                               \
+    }                                                                                                 \
   }
 
-    // Groups of kD blocks: group 0 and the last group are "edge" groups
-    // (bounds + fix-ups), groups 1..ngroups-2 are plain.  Loop invariant: gb
-    // holds group g, loaded; ga is free.
-    const uint32_t ngroups = (K + kD - 1) / kD;  // >= 1
-    ZCRC_LOADG(ga, 0u);
-    if (ngroups > 1) ZCRC_LOADG(gb, 1u);
-    ZCRC_EDGE(ga, 0u);
+  for (uint64_t k = 0; k < npieces; k++) {
+    const bool has_next = k + 1 < npieces;
+    const uint64_t inext = ZCRC_IDX(has_next ? k + 1 : k);
+    const uint64_t dnext = fetch_desc(bv, inext, lane);  // in flight during this piece
+    Piece Pn;
+
+    if (P.tiny) {  // n < 4: bytewise with the standard table (never split)
+      uint32_t r = ~P.seed;
+      for (uint32_t p = 0; p < (uint32_t)P.n; p++) r = (r >> 8) ^ tab->stdtab[(r ^ P.bptr[p]) & 0xFFu];
+      if (lane == 0) args.out[P.i] = ~r;
+      if (has_next) {
+        Pn = make_piece(bv, uni64(inext), dnext, S0, S1, last_wave, lane);
+        if (!Pn.tiny) ZCRC_LOADG(gc, Pn, 0u);
+        P = Pn;
+      }
+      continue;
+    }
+
+    // ---- stream piece P: bytes [pstart, pend) of buffer P.i ---------------
+    uint32_t s0 = 0, s1 = 0, s2 = 0, s3 = 0;
+    const uint32_t ngroups = (P.K + kD - 1) / kD;  // >= 1
+    if (ngroups > 1) ZCRC_LOADG(ga, P, 1u);
+    ZCRC_EDGE(gc, 0u);
+    // gc is free: prefetch the next piece's first group behind this one
+    if (has_next) {
+      Pn = make_piece(bv, uni64(inext), dnext, S0, S1, last_wave, lane);
+      if (!Pn.tiny) ZCRC_LOADG(gc, Pn, 0u);
+    }
     if (ngroups > 1) {
+      // groups 1..ngroups-2 are plain, the last one is an edge group;
+      // invariant at the loop head: ga holds group g (loaded), gb is free
       const uint32_t nplain = ngroups - 2;
       uint32_t g = 1;
       for (uint32_t pr = 0; pr < nplain / 2; pr++) {
-        ZCRC_LOADG(ga, g + 1);
-        ZCRC_PLAIN(gb);
-        ZCRC_LOADG(gb, g + 2);
+        ZCRC_LOADG(gb, P, g + 1);
         ZCRC_PLAIN(ga);
+        ZCRC_LOADG(ga, P, g + 2);
+        ZCRC_PLAIN(gb);
         g += 2;
       }
       if (nplain & 1u) {
-        ZCRC_LOADG(ga, g + 1);
-        ZCRC_PLAIN(gb);
-        ZCRC_EDGE(ga, g + 1);
+        ZCRC_LOADG(gb, P, g + 1);
+        ZCRC_PLAIN(ga);
+        ZCRC_EDGE(gb, g + 1);
       } else {
-        ZCRC_EDGE(gb, g);
+        ZCRC_EDGE(ga, g);
       }
     }
-#undef ZCRC_LOADG
-#undef ZCRC_STEP
-#undef ZCRC_CONSUME
-#undef ZCRC_PLAIN
-#undef ZCRC_EDGE
 
     // ---- fold 256 stream registers into one raw register at `aend` -------
     // stream (lane l, dword q) sits at aend + 16 l + 4 q
@@ -354,17 +434,24 @@ __global__ __launch_bounds__(kThreads) void crc32_batch_kernel(BatchArgs args) {
       const uint32_t moved = __shfl_down(comb_apply(s_lds, 2 + j, r), 1u << j, 64);
       r ^= moved;
     }
-    r = __builtin_amdgcn_readfirstlane(r);
-    if (tpad) r = mct_apply_global(tab->tshift + tpad * 1024u, r);  // -> register at pend
+    r = uni32(r);
+    if (P.tpad) r = mct_apply_global(tab->tshift + P.tpad * 1024u, r);  // -> register at pend
 
-    if (whole) {
-      if (lane == 0) args.out[i] = ~r;
+    if (P.whole) {
+      if (lane == 0) args.out[P.i] = ~r;
     } else {
-      const uint64_t d = n - rel_hi;  // bytes after this piece, multiple of kSplitGrain
-      uint32_t contrib = d ? shift_bytes(tab, r, d) : (r ^ 0xFFFFFFFFu);
-      if (lane == 0) atomicXor(args.out + i, contrib);
+      const uint64_t d = P.n - P.rel_hi;  // bytes after this piece, multiple of kSplitGrain
+      const uint32_t contrib = d ? shift_bytes(tab, r, d) : (r ^ 0xFFFFFFFFu);
+      if (lane == 0) atomicXor(args.out + P.i, contrib);
     }
+    if (has_next) P = Pn;
   }
+#undef ZCRC_IDX
+#undef ZCRC_LOADG
+#undef ZCRC_STEP
+#undef ZCRC_CONSUME
+#undef ZCRC_PLAIN
+#undef ZCRC_EDGE
 }
 
 }  // namespace zcrc
