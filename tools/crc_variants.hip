@@ -6,8 +6,11 @@
 #include <stdio.h>
 #include <stdlib.h>
 
+#include <vector>
+
 #include "../zipsfs_amd/csrc/zcrc_batch_kernel.h"
 #include "../zipsfs_amd/csrc/zcrc_tables.h"
+#include "kernel_v1.h"
 
 #define CHECK(x)                                                                               \
   do {                                                                                         \
@@ -47,14 +50,32 @@ int main(int argc, char **argv) {
   TableBlob *d_tab;
   static TableBlob tb;
   build_tables(tb);
-  CHECK(hipMalloc(&data, nbuf * len));
+  const bool zipf = (len == 0);
+  std::vector<uint64_t> zl(nbuf);
+  uint64_t tot = 0;
+  for (uint64_t i = 0; i < nbuf; i++) {
+    if (zipf) {  // SURVEY 8(d) config-4 law
+      uint64_t z = (0x5A1F5EEDull ^ ((i + 1) * 0xD1B54A32D192ED03ull)) + 0x9E3779B97F4A7C15ull;
+      z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+      z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+      z ^= z >> 31;
+      const double u = (double)(z >> 11) * (1.0 / 9007199254740992.0), t = 1.0 - u * 127.0 / 128.0;
+      double L = 1024.0 / (t * t);
+      L = L < 1024.0 ? 1024.0 : (L > 16777216.0 ? 16777216.0 : L);
+      zl[i] = (uint64_t)L;
+    } else {
+      zl[i] = len;
+    }
+    tot += (zl[i] + 15) & ~15ull;
+  }
+  CHECK(hipMalloc(&data, tot));
   CHECK(hipMalloc(&out, nbuf * 4));
   CHECK(hipMalloc(&ref, nbuf * 4));
   CHECK(hipMalloc(&d_tab, sizeof(TableBlob)));
   CHECK(hipMemcpy(d_tab, &tb, sizeof(TableBlob), hipMemcpyHostToDevice));
   // payload: any non-trivial bytes will do for timing
   uint64_t *hp = (uint64_t *)malloc(nbuf * 8), *hl = (uint64_t *)malloc(nbuf * 8);
-  for (uint64_t i = 0; i < nbuf; i++) hp[i] = (uint64_t)(data + i * len), hl[i] = len;
+  for (uint64_t i = 0, off = 0; i < nbuf; i++) hp[i] = (uint64_t)(data + off), hl[i] = zl[i], off += (zl[i] + 15) & ~15ull;
   uint64_t *dp, *dl;
   CHECK(hipMalloc(&dp, nbuf * 8));
   CHECK(hipMalloc(&dl, nbuf * 8));
@@ -62,27 +83,32 @@ int main(int argc, char **argv) {
   CHECK(hipMemcpy(dl, hl, nbuf * 8, hipMemcpyHostToDevice));
   CHECK(launch_fill_synthetic(dp, dl, nbuf, 0, 1, 0xC0FFEE, 0));
   CHECK(hipDeviceSynchronize());
+  // general (pointer-array) form with a host-computed prefix, like
+  // zcrc32_batch_device after its plan kernel
+  std::vector<uint64_t> hprefix(nbuf + 1, 0);
+  for (uint64_t i = 0; i < nbuf; i++) hprefix[i + 1] = hprefix[i] + hl[i];
+  uint64_t *dprefix;
+  CHECK(hipMalloc(&dprefix, (nbuf + 1) * 8));
+  CHECK(hipMemcpy(dprefix, hprefix.data(), (nbuf + 1) * 8, hipMemcpyHostToDevice));
   BatchArgs a{};
-  a.base = data;
-  a.stride = len;
-  a.len = len;
+  a.ptrs = reinterpret_cast<const uint8_t *const *>(dp);
+  a.prefix = dprefix;
   a.n = nbuf;
   a.tab = d_tab;
-  const double bytes = (double)nbuf * len;
-  printf("crc_variants: %llu x %llu B (%.1f GiB), %d CUs, %d reps\n", (unsigned long long)nbuf,
-         (unsigned long long)len, bytes / (1 << 30), cus, reps);
+  const double bytes = (double)hprefix[nbuf];
+  printf("crc_variants: %llu buffers, %.2f GiB (%s), %d CUs, %d reps\n", (unsigned long long)nbuf,
+         bytes / (1 << 30), zipf ? "zipf" : "uniform", cus, reps);
   struct V {
     const char *name;
     kfn k;
     bool check;
   } vs[] = {
-      {"D=4", crc32_batch_kernel<true, 4, 0, true>, true},
-      {"D=3", crc32_batch_kernel<true, 3, 0, true>, true},
-      {"D=4 ablate", crc32_batch_kernel<true, 4, 1, true>, false},
+      {"v2 (pipelined)", crc32_batch_kernel<false, 4, 0, true>, true},
+      {"v1 (0f98a60)", v1::crc32_batch_kernel<false, 4, 0, true>, true},
   };
-  const uint64_t ranges[] = {16384, 32768, 65536, 262144};
+  const uint64_t ranges[] = {65536};
   a.out = ref;
-  hipLaunchKernelGGL((crc32_batch_kernel<true, 4, 0, false>), dim3(cus), dim3(kThreads), 0, 0, a);
+  hipLaunchKernelGGL((v1::crc32_batch_kernel<false, 4, 0, true>), dim3(cus), dim3(kThreads), 0, 0, a);
   CHECK(hipDeviceSynchronize());
   uint32_t *h_ref = (uint32_t *)malloc(nbuf * 4), *h_out = (uint32_t *)malloc(nbuf * 4);
   CHECK(hipMemcpy(h_ref, ref, nbuf * 4, hipMemcpyDeviceToHost));

@@ -31,13 +31,14 @@
 //     domain, trailing padding is undone by x^(-8t).  The seed (~crc) is
 //     xored into the buffer's first four bytes (zlib chaining semantics).
 #pragma once
+// tools/kernel_v1.h -- previous kernel revision (git 0f98a60), for in-process A/B only.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
-#include "zcrc_gf2.h"
-#include "zcrc_internal.h"
+#include "../zipsfs_amd/csrc/zcrc_gf2.h"
+#include "../zipsfs_amd/csrc/zcrc_internal.h"
 
-namespace zcrc {
+namespace zcrc { namespace v1 {
 
 // ----------------------------------------------------------------- helpers
 
@@ -50,7 +51,7 @@ __device__ __forceinline__ uint32_t lds_u32(const uint32_t *lds, uint32_t byte_a
 // laneoff[j] carries bytes 0 and 2; v_perm drops data byte j into byte 1.
 #define ZCRC_SEL(j) (0x0C020400u + ((uint32_t)(j) << 8))
 
-__device__ __forceinline__ uint32_t braid_step(const uint32_t *lds, uint32_t x, uint32_t o0, uint32_t o1,
+__device__ __forceinline__ uint32_t braid_step_v1(const uint32_t *lds, uint32_t x, uint32_t o0, uint32_t o1,
                                                uint32_t o2, uint32_t o3) {
   const uint32_t a0 = __builtin_amdgcn_perm(x, o0, ZCRC_SEL(0));
   const uint32_t a1 = __builtin_amdgcn_perm(x, o1, ZCRC_SEL(1));
@@ -60,18 +61,18 @@ __device__ __forceinline__ uint32_t braid_step(const uint32_t *lds, uint32_t x, 
 }
 
 // r * c for one of the 8 combine constants resident in LDS.
-__device__ __forceinline__ uint32_t comb_apply(const uint32_t *lds, int c, uint32_t r) {
+__device__ __forceinline__ uint32_t comb_apply_v1(const uint32_t *lds, int c, uint32_t r) {
   const uint32_t *t = lds + kLdsCombDword + c * 1024;
   return t[r & 0xFFu] ^ t[256 + ((r >> 8) & 0xFFu)] ^ t[512 + ((r >> 16) & 0xFFu)] ^ t[768 + (r >> 24)];
 }
 
 // r * c for a multiply-by-constant table in global memory (L2-resident).
-__device__ __forceinline__ uint32_t mct_apply_global(const uint32_t *t, uint32_t r) {
+__device__ __forceinline__ uint32_t mct_apply_global_v1(const uint32_t *t, uint32_t r) {
   return t[r & 0xFFu] ^ t[256 + ((r >> 8) & 0xFFu)] ^ t[512 + ((r >> 16) & 0xFFu)] ^ t[768 + (r >> 24)];
 }
 
 // r * x^(8*nbytes), nbytes arbitrary (split pieces only: once per wave range).
-__device__ uint32_t shift_bytes(const TableBlob *tab, uint32_t r, uint64_t nbytes) {
+__device__ uint32_t shift_bytes_v1(const TableBlob *tab, uint32_t r, uint64_t nbytes) {
   int k = 0;
   while (nbytes) {
     if (nbytes & 1u) r = gf2_mul(tab->x8pow[k], r);
@@ -87,7 +88,7 @@ __device__ __forceinline__ uint32_t lowmask_bytes(int k) {
 
 // Zero the bytes of a 16-B lane chunk outside [lo, hi) (chunk-relative byte
 // offsets) and xor the 4-byte seed injection at chunk offset io.
-__device__ __forceinline__ uint4 fix_chunk(uint4 d, int lo, int hi, int io, uint32_t inj) {
+__device__ __forceinline__ uint4 fix_chunk_v1(uint4 d, int lo, int hi, int io, uint32_t inj) {
   uint32_t w[4] = {d.x, d.y, d.z, d.w};
 #pragma unroll
   for (int q = 0; q < 4; q++) {
@@ -105,9 +106,7 @@ __device__ __forceinline__ int clamp_rel(int32_t v) { return v < -64 ? -64 : (v 
 
 // Wave-uniform broadcast (lets hipcc keep descriptors and loop bounds in
 // SGPRs; without it every buffer_load gets a waterfall loop -- guide T20).
-// (__builtin_amdgcn_readfirstlane returns a signed int: convert through
-// uint32_t before widening, never sign-extend into the high half.)
-__device__ __forceinline__ uint32_t uni32(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane(v); }
+__device__ __forceinline__ uint32_t uni32(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
 __device__ __forceinline__ uint64_t uni64(uint64_t v) {
   return (uint64_t)uni32((uint32_t)v) | ((uint64_t)uni32((uint32_t)(v >> 32)) << 32);
 }
@@ -288,7 +287,7 @@ __global__ __launch_bounds__(kThreads) void crc32_batch_kernel(BatchArgs args) {
       G[u_] = make_uint4(v_[0], v_[1], v_[2], v_[3]);                                           \
     }                                                                                           \
   }
-#define ZCRC_STEP(x) (kAblate ? __builtin_amdgcn_alignbit((x), (x), 5) : braid_step(s_lds, (x), o0, o1, o2, o3))
+#define ZCRC_STEP(x) (kAblate ? __builtin_amdgcn_alignbit((x), (x), 5) : braid_step_v1(s_lds, (x), o0, o1, o2, o3))
 #define ZCRC_CONSUME(d)         \
   {                             \
     s0 = ZCRC_STEP(s0 ^ (d).x); \
@@ -310,7 +309,7 @@ __global__ __launch_bounds__(kThreads) void crc32_batch_kernel(BatchArgs args) {
         uint4 dd_ = G[u_];                                                                      \
         if (it_ <= 1u || it_ + 1u == K) {                                                       \
           const int32_t c_ = c0 + 1024 * (int32_t)it_;                                          \
-          dd_ = fix_chunk(dd_, clamp_rel(rs - c_), clamp_rel(re - c_), clamp_rel(rs - c_), inj); \
+          dd_ = fix_chunk_v1(dd_, clamp_rel(rs - c_), clamp_rel(re - c_), clamp_rel(rs - c_), inj); \
         }                                                                                       \
         ZCRC_CONSUME(dd_);                                                                      \
       }                                                                                         \
@@ -350,23 +349,23 @@ __global__ __launch_bounds__(kThreads) void crc32_batch_kernel(BatchArgs args) {
 
     // ---- fold 256 stream registers into one raw register at `aend` -------
     // stream (lane l, dword q) sits at aend + 16 l + 4 q
-    uint32_t r = (s0 ^ comb_apply(s_lds, 0, s1)) ^ comb_apply(s_lds, 1, s2 ^ comb_apply(s_lds, 0, s3));
+    uint32_t r = (s0 ^ comb_apply_v1(s_lds, 0, s1)) ^ comb_apply_v1(s_lds, 1, s2 ^ comb_apply_v1(s_lds, 0, s3));
 #pragma unroll
     for (int j = 0; j < 6; j++) {
-      const uint32_t moved = __shfl_down(comb_apply(s_lds, 2 + j, r), 1u << j, 64);
+      const uint32_t moved = __shfl_down(comb_apply_v1(s_lds, 2 + j, r), 1u << j, 64);
       r ^= moved;
     }
-    r = uni32(r);
-    if (tpad) r = mct_apply_global(tab->tshift + tpad * 1024u, r);  // -> register at pend
+    r = __builtin_amdgcn_readfirstlane(r);
+    if (tpad) r = mct_apply_global_v1(tab->tshift + tpad * 1024u, r);  // -> register at pend
 
     if (whole) {
       if (lane == 0) args.out[i] = ~r;
     } else {
       const uint64_t d = n - rel_hi;  // bytes after this piece, multiple of kSplitGrain
-      uint32_t contrib = d ? shift_bytes(tab, r, d) : (r ^ 0xFFFFFFFFu);
+      uint32_t contrib = d ? shift_bytes_v1(tab, r, d) : (r ^ 0xFFFFFFFFu);
       if (lane == 0) atomicXor(args.out + i, contrib);
     }
   }
 }
 
-}  // namespace zcrc
+}}  // namespace zcrc::v1
