@@ -76,6 +76,57 @@ int zcrc32_batch_device_ws(const void *const *d_ptrs, const uint64_t *d_lens,
 int zcrc32_batch_device_strided(const void *d_base, uint64_t stride, uint64_t len, size_t n,
                                 const uint32_t *d_seeds_or_null, uint32_t *d_out, void *stream);
 
+/* Streaming / incremental CRC.  ZIPsFS fills a preload
+ * buffer in <= 16 MiB zip_fread() chunks (src/ZIPsFS_preloadfileram.c:286-306)
+ * and only then CRCs the whole entry under mutex_fhandle (:309-321).  A
+ * stream checksums each chunk as it lands: update() copies the chunk to
+ * pinned staging and enqueues H2D + kernel on the stream's own HIP stream
+ * (the running CRC stays on the device), so the GPU work overlaps the next
+ * inflate; final() waits and returns crc32(seed, all bytes so far).
+ * One thread at a time per stream; streams are independent. */
+typedef struct zcrc32_stream zcrc32_stream;
+zcrc32_stream *zcrc32_stream_open(uint32_t seed);            /* NULL on failure */
+int zcrc32_stream_update(zcrc32_stream *s, const void *data, size_t n_bytes);
+int zcrc32_stream_final(zcrc32_stream *s, uint32_t *crc);      /* stream stays usable */
+void zcrc32_stream_close(zcrc32_stream *s);
+
+/* Batched ZIP verification.  ZIPsFS takes each
+ * entry's expected CRC from the central directory (libzip zip_stat, st.crc:
+ * src/ZIPsFS.c:998; exposed as <entry>@ARCHIVECRC32.TXT,
+ * src/ZIPsFS_special_file.c:155-163) and checks it after a full preload.
+ * zcrc_zip_scan parses the central directory of an archive image (ZIP64
+ * included) on the host; zcrc_zip_verify_* checksum the data of every
+ * stored (method 0) entry in ONE batched GPU launch and compare.  Entries
+ * that need inflating or decrypting are reported as UNVERIFIED. */
+#define ZCRC_ZIP_OK 1
+#define ZCRC_ZIP_MISMATCH 0
+#define ZCRC_ZIP_UNVERIFIED (-1)  /* compressed or encrypted: not checksummed here */
+#define ZCRC_ZIP_BAD (-2)         /* local header or data range outside the archive */
+typedef struct zcrc_zip_entry {
+  uint64_t data_offset;  /* first byte of the entry's stored data in the archive */
+  uint64_t comp_size;    /* bytes of entry data in the archive */
+  uint64_t uncomp_size;
+  uint64_t name_offset;  /* file name (central directory copy) in the archive */
+  uint32_t name_len;
+  uint32_t crc_expected; /* central directory CRC-32 */
+  uint32_t crc_computed; /* set by zcrc_zip_verify_* for stored entries */
+  uint16_t method;       /* 0 stored, 8 deflate, ... */
+  uint16_t flags;        /* general purpose bit flags */
+  int32_t status;        /* ZCRC_ZIP_* */
+  uint32_t reserved;
+} zcrc_zip_entry;
+
+/* Parse the central directory.  entries may be NULL to count; *n_entries
+ * receives the number of entries (even when it exceeds `capacity`). */
+int zcrc_zip_scan(const void *archive, size_t archive_len, zcrc_zip_entry *entries, size_t capacity,
+                  size_t *n_entries);
+/* Verify with the archive image in host memory (staged to the GPU). */
+int zcrc_zip_verify_host(const void *archive, size_t archive_len, zcrc_zip_entry *entries, size_t n);
+/* Verify with the archive image resident in device memory (d_archive);
+ * synchronous on `stream`. */
+int zcrc_zip_verify_device(const void *d_archive, size_t archive_len, zcrc_zip_entry *entries, size_t n,
+                           void *stream);
+
 /* GF(2) algebra (pure integer math, no data access):
  * crc32(A||B) == zcrc32_combine(crc32(A), crc32(B), |B|)   (zlib semantics). */
 uint32_t zcrc32_combine(uint32_t crc_a, uint32_t crc_b, uint64_t len_b);

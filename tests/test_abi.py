@@ -59,15 +59,36 @@ def test_dropin_compiles(tmp_path, compiler, lang):
 
 
 def test_product_has_no_cpu_crc_path():
-    """The shipped package must not import the oracle or compute CRCs on the CPU."""
+    """The shipped package must not import the oracle or compute CRCs on the CPU.
+
+    Source files may not reference the oracle; Python modules may import zlib
+    only for inflate and never call a zlib/binascii checksum (AST check)."""
+    import ast
     pkg = os.path.join(ROOT, "zipsfs_amd")
+    banned_attrs = {"crc32", "adler32", "crc_hqx", "crc32_combine"}
     for dirpath, _, files in os.walk(pkg):
         for f in files:
-            if f.endswith((".py", ".hip", ".h", ".c", ".cpp")):
-                text = open(os.path.join(dirpath, f)).read()
-                for bad in ("from oracle", "import oracle", "liboracle", "libref_cg_crc32", "import zlib",
-                            "binascii", "crc32_port"):
-                    assert bad not in text, (f, bad)
+            path = os.path.join(dirpath, f)
+            if not f.endswith((".py", ".hip", ".h", ".c", ".cpp")):
+                continue
+            text = open(path).read()
+            for bad in ("from oracle", "import oracle", "liboracle", "libref_cg_crc32", "crc32_port", "binascii"):
+                assert bad not in text, (f, bad)
+            if f.endswith(".py"):
+                tree = ast.parse(text)
+                aliases = set()
+                for node in ast.walk(tree):
+                    if isinstance(node, ast.Import):
+                        for a in node.names:
+                            if a.name in ("zlib", "binascii"):
+                                aliases.add(a.asname or a.name)
+                    if isinstance(node, ast.ImportFrom) and node.module in ("zlib", "binascii"):
+                        for a in node.names:
+                            assert a.name not in banned_attrs, (f, a.name)
+                for node in ast.walk(tree):
+                    if isinstance(node, ast.Attribute) and isinstance(node.value, ast.Name):
+                        if node.value.id in aliases:
+                            assert node.attr not in banned_attrs, (f, node.attr)
 
 
 def test_missing_gpu_fails_loudly():

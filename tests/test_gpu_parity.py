@@ -260,3 +260,55 @@ def test_prefix_and_pointers_beyond_2_31_and_2_32():
     host_first = mem[5:5 + (3 << 20)].cpu().numpy()
     assert int(got_s[0]) == zlib.crc32(host_first[: 1 << 20].tobytes())
     assert int(got_s[2]) == zlib.crc32(host_first[2 << 20: 3 << 20].tobytes())
+
+
+def test_stream_incremental_like_preloadram():
+    """Crc32Stream over zip_fread-sized chunks (16 MiB, src/ZIPsFS_preloadfileram.c:286-306),
+    ragged chunks, empty updates, intermediate final() and a seed."""
+    data = o.payload((40 << 20) + 12345, 77)
+    full = zlib.crc32(data.tobytes())
+    with z.Crc32Stream() as s:
+        for off in range(0, data.size, 16 << 20):
+            s.update(data[off:off + (16 << 20)])
+        assert s.final() == full
+    rnd = random.Random(11)
+    with z.Crc32Stream(seed=0xABCDEF01) as s:
+        pos, mid_checked = 0, False
+        while pos < data.size:
+            step = rnd.choice([0, 1, 3, 17, 4096, 65537, 1 << 20, 20 << 20])
+            s.update(data[pos:pos + step])
+            pos = min(pos + step, data.size)
+            if not mid_checked and pos > (5 << 20):
+                assert s.final() == zlib.crc32(data[:pos].tobytes(), 0xABCDEF01)
+                mid_checked = True
+        assert s.final() == zlib.crc32(data.tobytes(), 0xABCDEF01)
+    with z.Crc32Stream(seed=5) as s:
+        assert s.final() == 5  # no data: the seed, like zlib crc32(5, NULL, 0)
+
+
+@pytest.mark.parametrize("device", [True, False])
+def test_zip_verify_batched(device):
+    """Whole-archive verification: stored entries in one GPU batch vs the
+    central-directory CRCs zipfile wrote; a flipped byte is caught; deflated
+    entries are verified after host inflate."""
+    import io
+    import zipfile
+    from zipsfs_amd import zipverify as zv
+    rnd = random.Random(3)
+    buf = io.BytesIO()
+    with zipfile.ZipFile(buf, "w", allowZip64=True) as zf:
+        for i in range(300):
+            data = o.payload(rnd.choice([0, 1, 5, 4095, 65536, 300_000, 2_000_001]), i).tobytes()
+            zf.writestr(f"e{i}", data, compress_type=zipfile.ZIP_STORED if i % 3 else zipfile.ZIP_DEFLATED)
+    data = bytearray(buf.getvalue())
+    res = zv.verify(bytes(data), device=device)
+    stored = [r for r in res if r.method == 0]
+    assert stored and all(r.status == zv.ZIP_OK for r in stored)
+    assert all(r.status == zv.ZIP_UNVERIFIED for r in res if r.method == 8)
+    res = zv.verify(bytes(data), device=device, inflate=True)
+    assert all(r.status == zv.ZIP_OK for r in res)
+    victim = next(r for r in stored if r.comp_size > 1000)
+    data[victim.data_offset + 500] ^= 0x40
+    res = zv.verify(bytes(data), device=device)
+    bad = [r for r in res if r.status == zv.ZIP_MISMATCH]
+    assert [r.name for r in bad] == [victim.name]

@@ -8,7 +8,7 @@ interface.  GPU only: a missing library or device raises ZcrcError.
 """
 from ._lib import ZcrcError, lib  # noqa: F401
 from .crc32 import (  # noqa: F401
-    cg_crc32, crc32_batch, crc32_batch_device, crc32_batch_device_ws, crc32_batch_strided,
+    Crc32Stream, cg_crc32, crc32_batch, crc32_batch_device, crc32_batch_device_ws, crc32_batch_strided,
     crc32_combine, crc32_tensors, device_info, fhandle_check_crc32, fill_synthetic, profile,
     scratch_bytes, verify_entries, version,
 )

@@ -50,6 +50,9 @@ hipError_t launch_plan(const uint64_t *d_lens, uint64_t n, uint64_t *d_prefix, u
 }  // namespace zcrc
 
 namespace zcrc {
+// record an error for zcrc_last_error() (this thread) and return `code`
+int set_error(int code, const char *msg);
+
 hipError_t launch_fill_synthetic(const uint64_t *d_ptrs, const uint64_t *d_lens, uint64_t n, uint64_t index0,
                                  uint64_t index_step, uint64_t seed, hipStream_t stream);
 }  // namespace zcrc

@@ -15,6 +15,7 @@
 #include <atomic>
 #include <condition_variable>
 #include <mutex>
+#include <new>
 #include <string>
 #include <thread>
 #include <vector>
@@ -409,6 +410,96 @@ int batch_host(const void *const *ptrs, const size_t *lens, const uint32_t *seed
   return slot_finish(t_host.slot[cur ^ 1], out);
 }
 
+// ------------------------------------------------------------- streaming
+
+constexpr size_t kStreamChunk = 16ull << 20;  // ZIPsFS PRELOADRAM_READ_BYTES_NUM
+
+}  // namespace
+
+int set_error(int code, const char *msg) { return fail(code, msg); }
+
+}  // namespace zcrc
+
+struct zcrc32_stream {
+  int dev = -1;
+  hipStream_t stream = nullptr;
+  uint8_t *h_stage[2] = {nullptr, nullptr};
+  uint8_t *d_stage[2] = {nullptr, nullptr};
+  hipEvent_t staged[2] = {nullptr, nullptr};  // H2D from h_stage[b] finished
+  uint32_t *d_crc = nullptr;                  // [2] ping-pong running CRC
+  uint64_t parts = 0;                         // chunk launches so far
+  uint32_t seed = 0;
+  bool dirty = false;                         // any update since open/final
+};
+
+namespace zcrc {
+namespace {
+
+void stream_free(zcrc32_stream *s) {
+  if (!s) return;
+  if (s->stream) (void)hipStreamSynchronize(s->stream);
+  for (int b = 0; b < 2; b++) {
+    if (s->h_stage[b]) (void)hipHostFree(s->h_stage[b]);
+    if (s->d_stage[b]) (void)hipFree(s->d_stage[b]);
+    if (s->staged[b]) (void)hipEventDestroy(s->staged[b]);
+  }
+  if (s->d_crc) (void)hipFree(s->d_crc);
+  if (s->stream) (void)hipStreamDestroy(s->stream);
+  delete s;
+}
+
+int stream_init(zcrc32_stream *s, uint32_t seed) {
+  DeviceCtx *dc = nullptr;
+  int rc = device_ctx(&dc);
+  if (rc) return rc;
+  ZCRC_HIP_TRY(hipGetDevice(&s->dev));
+  ZCRC_HIP_TRY(hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking));
+  for (int b = 0; b < 2; b++) {
+    ZCRC_HIP_TRY(hipHostMalloc(reinterpret_cast<void **>(&s->h_stage[b]), kStreamChunk, hipHostMallocDefault));
+    ZCRC_HIP_TRY(hipMalloc(reinterpret_cast<void **>(&s->d_stage[b]), kStreamChunk));
+    ZCRC_HIP_TRY(hipEventCreateWithFlags(&s->staged[b], hipEventDisableTiming));
+  }
+  ZCRC_HIP_TRY(hipMalloc(reinterpret_cast<void **>(&s->d_crc), 2 * sizeof(uint32_t)));
+  s->seed = seed;
+  ZCRC_HIP_TRY(hipMemcpyAsync(s->d_crc, &s->seed, 4, hipMemcpyHostToDevice, s->stream));
+  ZCRC_HIP_TRY(hipStreamSynchronize(s->stream));
+  return ZCRC_OK;
+}
+
+int stream_update(zcrc32_stream *s, const uint8_t *data, size_t n) {
+  DeviceCtx *dc = nullptr;
+  int rc = device_ctx(&dc);
+  if (rc) return rc;
+  while (n > 0) {
+    const size_t take = std::min(n, kStreamChunk);
+    const int b = (int)(s->parts & 1u);
+    // pinned slot b is free once its previous H2D finished
+    ZCRC_HIP_TRY(hipEventSynchronize(s->staged[b]));
+    CopyPool::get().run({CopyJob{s->h_stage[b], data, take}});
+    ZCRC_HIP_TRY(hipMemcpyAsync(s->d_stage[b], s->h_stage[b], take, hipMemcpyHostToDevice, s->stream));
+    ZCRC_HIP_TRY(hipEventRecord(s->staged[b], s->stream));
+    // running CRC: seed from d_crc[cur], result to d_crc[cur ^ 1] (zeroed:
+    // split pieces xor into it).  One stream => chunks chain in order.
+    uint32_t *cur = s->d_crc + (s->parts & 1u), *nxt = s->d_crc + ((s->parts + 1) & 1u);
+    ZCRC_HIP_TRY(hipMemsetAsync(nxt, 0, 4, s->stream));
+    BatchArgs a{};
+    a.base = s->d_stage[b];
+    a.stride = take;
+    a.len = take;
+    a.n = 1;
+    a.seeds = cur;
+    a.out = nxt;
+    a.tab = dc->d_tab;
+    rc = launch_main(a, true, *dc, s->stream);
+    if (rc) return rc;
+    s->parts++;
+    data += take;
+    n -= take;
+  }
+  s->dirty = true;
+  return ZCRC_OK;
+}
+
 }  // namespace
 }  // namespace zcrc
 
@@ -500,6 +591,41 @@ int zcrc32_batch_device_strided(const void *d_base, uint64_t stride, uint64_t le
   }
   return ZCRC_OK;
 }
+
+zcrc32_stream *zcrc32_stream_open(uint32_t seed) {
+  zcrc32_stream *s = new (std::nothrow) zcrc32_stream();
+  if (!s) {
+    fail(ZCRC_ERR_HIP, "out of host memory");
+    return nullptr;
+  }
+  if (stream_init(s, seed) != ZCRC_OK) {
+    const std::string err = t_last_error;
+    stream_free(s);
+    t_last_error = err;
+    return nullptr;
+  }
+  return s;
+}
+
+int zcrc32_stream_update(zcrc32_stream *s, const void *data, size_t n_bytes) {
+  if (!s) return fail(ZCRC_ERR_ARG, "null stream");
+  if (n_bytes && !data) return fail(ZCRC_ERR_ARG, "null data");
+  int dev = -1;
+  ZCRC_HIP_TRY(hipGetDevice(&dev));
+  if (dev != s->dev) return fail(ZCRC_ERR_ARG, "stream used on another device");
+  return stream_update(s, static_cast<const uint8_t *>(data), n_bytes);
+}
+
+int zcrc32_stream_final(zcrc32_stream *s, uint32_t *crc) {
+  if (!s || !crc) return fail(ZCRC_ERR_ARG, "null argument");
+  uint32_t v = 0;
+  ZCRC_HIP_TRY(hipMemcpyAsync(&v, s->d_crc + (s->parts & 1u), 4, hipMemcpyDeviceToHost, s->stream));
+  ZCRC_HIP_TRY(hipStreamSynchronize(s->stream));
+  *crc = v;
+  return ZCRC_OK;
+}
+
+void zcrc32_stream_close(zcrc32_stream *s) { stream_free(s); }
 
 uint32_t zcrc32_combine(uint32_t crc_a, uint32_t crc_b, uint64_t len_b) {
   return gf2_crc_combine(host_xpow(), crc_a, crc_b, len_b);

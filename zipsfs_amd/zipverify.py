@@ -1,0 +1,135 @@
+"""Batched verification of ZIP archives on the GPU.
+
+ZIPsFS reads each entry's expected CRC from the central directory through
+libzip (``zip_stat`` -> ``st.crc``, src/ZIPsFS.c:998; shown to users as
+``<entry>@ARCHIVECRC32.TXT``, src/ZIPsFS_special_file.c:155-163) and checks
+it after a full preload (src/ZIPsFS_preloadfileram.c:237-250).  This module
+checks a whole archive at once: libzcrc parses the central directory
+(ZIP64 aware) and checksums every stored entry in one batched GPU launch.
+Deflated entries can optionally be inflated on the host (zlib inflate -- not a
+CRC) and then checksummed on the GPU in the same way.
+"""
+from __future__ import annotations
+
+import ctypes
+import zlib as _inflate_only  # used for raw-DEFLATE decompression only, never for CRCs
+from dataclasses import dataclass
+from typing import List, Optional
+
+import numpy as np
+
+from ._lib import ZcrcError, check, lib
+
+ZIP_OK, ZIP_MISMATCH, ZIP_UNVERIFIED, ZIP_BAD = 1, 0, -1, -2
+
+
+class _Entry(ctypes.Structure):
+    _fields_ = [("data_offset", ctypes.c_uint64), ("comp_size", ctypes.c_uint64),
+                ("uncomp_size", ctypes.c_uint64), ("name_offset", ctypes.c_uint64),
+                ("name_len", ctypes.c_uint32), ("crc_expected", ctypes.c_uint32),
+                ("crc_computed", ctypes.c_uint32), ("method", ctypes.c_uint16),
+                ("flags", ctypes.c_uint16), ("status", ctypes.c_int32), ("reserved", ctypes.c_uint32)]
+
+
+_SIGS = False
+
+
+def _setup():
+    global _SIGS
+    if _SIGS:
+        return lib()
+    l = lib()
+    l.zcrc_zip_scan.restype = ctypes.c_int
+    l.zcrc_zip_scan.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_size_t,
+                                ctypes.POINTER(ctypes.c_size_t)]
+    l.zcrc_zip_verify_host.restype = ctypes.c_int
+    l.zcrc_zip_verify_host.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_size_t]
+    l.zcrc_zip_verify_device.restype = ctypes.c_int
+    l.zcrc_zip_verify_device.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_size_t,
+                                         ctypes.c_void_p]
+    _SIGS = True
+    return l
+
+
+@dataclass
+class ZipEntryCheck:
+    name: str
+    method: int
+    comp_size: int
+    uncomp_size: int
+    data_offset: int
+    crc_expected: int
+    crc_computed: Optional[int]
+    status: int
+
+    @property
+    def ok(self) -> bool:
+        return self.status == ZIP_OK
+
+
+def _as_array(archive) -> np.ndarray:
+    import os
+    if isinstance(archive, (str, os.PathLike)):
+        return np.fromfile(archive, dtype=np.uint8)
+    if isinstance(archive, np.ndarray):
+        return np.ascontiguousarray(archive, dtype=np.uint8)
+    return np.frombuffer(bytes(archive) if not isinstance(archive, (bytes, bytearray, memoryview)) else archive,
+                         dtype=np.uint8)
+
+
+def scan(archive) -> List[ZipEntryCheck]:
+    """Central-directory listing (no CRCs computed)."""
+    a = _as_array(archive)
+    return [_to_check(a, e) for e in _scan_raw(a)]
+
+
+def _scan_raw(a: np.ndarray):
+    l = _setup()
+    n = ctypes.c_size_t(0)
+    check(l.zcrc_zip_scan(a.ctypes.data, a.size, None, 0, ctypes.byref(n)), "zcrc_zip_scan")
+    arr = (_Entry * max(n.value, 1))()
+    check(l.zcrc_zip_scan(a.ctypes.data, a.size, arr, n.value, ctypes.byref(n)), "zcrc_zip_scan")
+    return arr[: n.value]
+
+
+def _to_check(a: np.ndarray, e) -> ZipEntryCheck:
+    name = a[e.name_offset: e.name_offset + e.name_len].tobytes().decode("utf-8", "replace")
+    computed = e.crc_computed if e.status in (ZIP_OK, ZIP_MISMATCH) else None
+    return ZipEntryCheck(name, e.method, e.comp_size, e.uncomp_size, e.data_offset, e.crc_expected, computed,
+                         e.status)
+
+
+def verify(archive, device: bool = True, inflate: bool = False) -> List[ZipEntryCheck]:
+    """Verify every entry's CRC against the central directory on the GPU.
+
+    device=True stages the archive image into HBM once and checksums all
+    stored entries in one launch (zcrc_zip_verify_device); device=False uses
+    the host-resident path.  With inflate=True, deflated entries are inflated
+    on the host and their bytes checksummed on the GPU in one more batch.
+    """
+    a = _as_array(archive)
+    l = _setup()
+    entries = _scan_raw(a)
+    arr = (_Entry * max(len(entries), 1))(*entries)
+    if device:
+        import torch
+        from .crc32 import _stream_ptr
+        d = torch.from_numpy(a if a.flags.writeable else a.copy()).to("cuda")
+        check(l.zcrc_zip_verify_device(d.data_ptr(), a.size, arr, len(entries), _stream_ptr(None)),
+              "zcrc_zip_verify_device")
+    else:
+        check(l.zcrc_zip_verify_host(a.ctypes.data, a.size, arr, len(entries)), "zcrc_zip_verify_host")
+    out = [_to_check(a, e) for e in arr[: len(entries)]]
+    if inflate:
+        from .crc32 import crc32_batch
+        todo = [i for i, c in enumerate(out) if c.status == ZIP_UNVERIFIED and c.method == 8
+                and not (arr[i].flags & 1)]
+        if todo:
+            raw = [_inflate_only.decompressobj(-15).decompress(
+                a[out[i].data_offset: out[i].data_offset + out[i].comp_size].tobytes()) for i in todo]
+            crcs = crc32_batch(raw)
+            for i, data, c in zip(todo, raw, crcs):
+                ok = int(c) == out[i].crc_expected and len(data) == out[i].uncomp_size
+                out[i].crc_computed = int(c)
+                out[i].status = ZIP_OK if ok else ZIP_MISMATCH
+    return out
