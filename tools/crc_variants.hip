@@ -6,6 +6,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 
+#include <algorithm>
 #include <vector>
 
 #include "../zipsfs_amd/csrc/zcrc_batch_kernel.h"
@@ -28,10 +29,25 @@ static float time_it(kfn k, const BatchArgs &a, int cus, int reps) {
   hipEvent_t e0, e1;
   CHECK(hipEventCreate(&e0));
   CHECK(hipEventCreate(&e1));
+  const uint64_t nb = a.n;
+  CHECK(hipMemsetAsync(a.out, 0, nb * 4, 0));
   hipLaunchKernelGGL(k, dim3(cus), dim3(kThreads), 0, 0, a);
   CHECK(hipDeviceSynchronize());
+  float total = 0;
+  for (int r = 0; r < reps; r++) {
+    // per-launch reset of the work counter and of out[] (split pieces xor into
+    // it); the memsets are outside the timed interval
+      CHECK(hipMemsetAsync(a.out, 0, nb * 4, 0));
+    CHECK(hipEventRecord(e0, 0));
+    hipLaunchKernelGGL(k, dim3(cus), dim3(kThreads), 0, 0, a);
+    CHECK(hipEventRecord(e1, 0));
+    CHECK(hipEventSynchronize(e1));
+    float ms;
+    CHECK(hipEventElapsedTime(&ms, e0, e1));
+    total += ms;
+  }
+  return total / reps;
   CHECK(hipEventRecord(e0, 0));
-  for (int r = 0; r < reps; r++) hipLaunchKernelGGL(k, dim3(cus), dim3(kThreads), 0, 0, a);
   CHECK(hipEventRecord(e1, 0));
   CHECK(hipEventSynchronize(e1));
   float ms;
@@ -103,16 +119,55 @@ int main(int argc, char **argv) {
     kfn k;
     bool check;
   } vs[] = {
-      {"v2 (pipelined)", crc32_batch_kernel<false, 4, 0, true>, true},
-      {"v1 (0f98a60)", v1::crc32_batch_kernel<false, 4, 0, true>, true},
+      {"static", crc32_batch_kernel<false, 4, 0, true>, true},
   };
+  uint32_t *d_counter;
+  CHECK(hipMalloc(&d_counter, 32));
+  CHECK(hipMemset(d_counter, 0, 32));
+
   const uint64_t ranges[] = {65536};
-  a.out = ref;
-  hipLaunchKernelGGL((v1::crc32_batch_kernel<false, 4, 0, true>), dim3(cus), dim3(kThreads), 0, 0, a);
-  CHECK(hipDeviceSynchronize());
   uint32_t *h_ref = (uint32_t *)malloc(nbuf * 4), *h_out = (uint32_t *)malloc(nbuf * 4);
+  a.out = ref;
+  CHECK(hipMemset(ref, 0, nbuf * 4));
+  CHECK(hipMemset(d_counter, 0, 32));
+  hipLaunchKernelGGL((crc32_batch_kernel<false, 4, 0, true>), dim3(cus), dim3(kThreads), 0, 0, a);
+  CHECK(hipDeviceSynchronize());
   CHECK(hipMemcpy(h_ref, ref, nbuf * 4, hipMemcpyDeviceToHost));
   a.out = out;
+  // stamp runs: per-wave wall-clock begin/end (100 MHz)
+  auto stamp_run = [&](const char *name, kfn k) {
+    const uint64_t nw = (uint64_t)cus * kWaves;
+    uint64_t *dst;
+    CHECK(hipMalloc(&dst, nw * 32));
+    CHECK(hipMemset(dst, 0, nw * 32));
+    CHECK(hipMemset(d_counter, 0, 32));
+    a.stamps = dst;
+    hipLaunchKernelGGL(k, dim3(cus), dim3(kThreads), 0, 0, a);
+    CHECK(hipDeviceSynchronize());
+    std::vector<uint64_t> st(nw * 4);
+    CHECK(hipMemcpy(st.data(), dst, nw * 32, hipMemcpyDeviceToHost));
+    uint64_t t0 = ~0ull, t1 = 0;
+    for (uint64_t w = 0; w < nw; w++)
+      if (st[4 * w + 1]) t0 = std::min(t0, st[4 * w]), t1 = std::max(t1, st[4 * w + 1]);
+    std::vector<double> dur, endt;
+    double c2 = 0, c3 = 0;
+    for (uint64_t w = 0; w < nw; w++)
+      if (st[4 * w + 1]) {
+        dur.push_back((st[4 * w + 1] - st[4 * w]) * 1e-2);
+        endt.push_back((st[4 * w + 1] - t0) * 1e-2);
+        c2 += st[4 * w + 2];
+        c3 += st[4 * w + 3];
+      }
+    std::sort(dur.begin(), dur.end());
+    std::sort(endt.begin(), endt.end());
+    auto pct = [](const std::vector<double> &v, double p) { return v[(size_t)(p * (v.size() - 1))]; };
+    printf("stamps %-8s waves %zu span %.1f us | wave us p0 %.1f p10 %.1f p50 %.1f p90 %.1f p100 %.1f | end us p10 %.1f p50 %.1f p90 %.1f | w2 %.1f w3 %.1f\n",
+           name, dur.size(), (t1 - t0) * 1e-2, pct(dur, 0), pct(dur, .1), pct(dur, .5), pct(dur, .9), pct(dur, 1),
+           pct(endt, .1), pct(endt, .5), pct(endt, .9), c2 / dur.size(), c3 / dur.size());
+    a.stamps = nullptr;
+    CHECK(hipFree(dst));
+  };
+  stamp_run("static", crc32_batch_kernel<false, 4, 0, true, true>);
   for (int round = 0; round < 2; round++) {
     for (uint64_t mr : ranges)
     for (auto &v : vs) {

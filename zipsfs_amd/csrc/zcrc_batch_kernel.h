@@ -179,47 +179,13 @@ struct BatchView {
 
 // kD: 1 KiB blocks per register group (two groups in flight); kAblate != 0
 // replaces the table lookups with one VALU op (measurement builds only).
-template <bool kStrided, uint32_t kD = kDepth, int kAblate = 0, bool kRotate = true>
-__global__ __launch_bounds__(kThreads) void crc32_batch_kernel(BatchArgs args) {
-  __shared__ __attribute__((aligned(16))) uint32_t s_lds[kLdsBytes / 4];
-  const BatchView<kStrided> bv{args};
-  const TableBlob *tab = args.tab;
-
-  const uint64_t total = bv.total();
-  const uint64_t max_waves = (uint64_t)gridDim.x * kWaves;
-  const uint64_t min_range = args.min_range ? args.min_range : kMinRange;
-  uint64_t want = (total + min_range - 1) / min_range;
-  if (want < 1) want = 1;
-  const uint64_t W = want < max_waves ? want : max_waves;
-  if ((uint64_t)blockIdx.x * kWaves >= W) return;  // whole workgroup idle (uniform)
-
-  // ---- LDS fill: braided table x32 replicas + 8 combine tables ----------
-  {
-    const uint32_t tid = threadIdx.x;  // 0..1023 = (table j, byte v)
-    const uint32_t j = tid >> 8, v = tid & 255u;
-    const uint32_t val = tab->braid[tid];
-    const uint4 q = make_uint4(val, val, val, val);
-    char *dst = reinterpret_cast<char *>(s_lds) + (j >> 1) * 65536u + v * 256u + (j & 1u) * 128u;
-#pragma unroll
-    for (int r = 0; r < 8; r++) *reinterpret_cast<uint4 *>(dst + 16 * r) = q;
-    const uint4 *src = reinterpret_cast<const uint4 *>(tab->comb) + tid * 2;
-    uint4 *cdst = reinterpret_cast<uint4 *>(s_lds + kLdsCombDword) + tid * 2;
-    cdst[0] = src[0];
-    cdst[1] = src[1];
-  }
-  __syncthreads();
-
-  const uint32_t lane = threadIdx.x & 63u;
-  const uint64_t w = (uint64_t)blockIdx.x * kWaves + (threadIdx.x >> 6);
-  if (w >= W) return;  // no barrier after this point
-
-  // nominal boundary of wave k: floor(k * total / W), without 128-bit math
-  const uint64_t q_tot = total / W, r_tot = total % W;
-  const uint64_t S0 = uni64(bv.snap(q_tot * w + (r_tot * w) / W));
-  const uint64_t S1 = uni64((w + 1 == W) ? total : bv.snap(q_tot * (w + 1) + (r_tot * (w + 1)) / W));
-  const bool last_wave = (w + 1 == W);
-  if (S0 >= S1 && !last_wave) return;
-
+// Process every piece of the byte range [S0, S1) of the concatenated batch
+// (S0, S1 snapped; `last_range` also takes the trailing empty buffers).
+// Returns the number of pieces.  Wave-uniform; no barriers.
+template <bool kStrided, uint32_t kD, int kAblate, bool kRotate>
+__device__ __forceinline__ uint64_t process_range(const BatchArgs &args, const BatchView<kStrided> &bv,
+                                                  const uint32_t *s_lds, const TableBlob *tab, uint64_t S0,
+                                                  uint64_t S1, bool last_wave, uint32_t salt, uint32_t lane) {
   // lane constants for the braided lookups
   const uint32_t lo0 = (lane & 31u) * 4u;
   const uint32_t o0 = lo0, o1 = lo0 + 128u, o2 = lo0 + 65536u, o3 = lo0 + 65536u + 128u;
@@ -234,7 +200,7 @@ __global__ __launch_bounds__(kThreads) void crc32_batch_kernel(BatchArgs args) {
   // and the rotation de-phases waves whose ranges start on large power-of-two
   // boundaries (uniform batches), which otherwise walk the HBM channel
   // interleave in lockstep ("partition camping", tools/hbm_probe: up to -13%).
-  const uint64_t rot = (kRotate && npieces > 1) ? (uint64_t)(hash32((uint32_t)w) % (uint32_t)npieces) : 0;
+  const uint64_t rot = (kRotate && npieces > 1) ? (uint64_t)(hash32(salt) % (uint32_t)npieces) : 0;
 
   for (uint64_t k = 0; k < npieces; k++) {
     uint64_t i = i_first + k + rot;
@@ -366,6 +332,60 @@ __global__ __launch_bounds__(kThreads) void crc32_batch_kernel(BatchArgs args) {
       uint32_t contrib = d ? shift_bytes(tab, r, d) : (r ^ 0xFFFFFFFFu);
       if (lane == 0) atomicXor(args.out + i, contrib);
     }
+  }
+  return npieces;
+}
+
+template <bool kStrided, uint32_t kD = kDepth, int kAblate = 0, bool kRotate = true, bool kStamp = false>
+__global__ __launch_bounds__(kThreads) void crc32_batch_kernel(BatchArgs args) {
+  __shared__ __attribute__((aligned(16))) uint32_t s_lds[kLdsBytes / 4];
+  const BatchView<kStrided> bv{args};
+  const TableBlob *tab = args.tab;
+
+  const uint64_t total = bv.total();
+  const uint64_t max_waves = (uint64_t)gridDim.x * kWaves;
+  const uint64_t min_range = args.min_range ? args.min_range : kMinRange;
+  uint64_t want = (total + min_range - 1) / min_range;
+  if (want < 1) want = 1;
+  const uint64_t W = want < max_waves ? want : max_waves;
+  if ((uint64_t)blockIdx.x * kWaves >= W) return;  // whole workgroup idle (uniform)
+
+  // ---- LDS fill: braided table x32 replicas + 8 combine tables ----------
+  {
+    const uint32_t tid = threadIdx.x;  // 0..1023 = (table j, byte v)
+    const uint32_t j = tid >> 8, v = tid & 255u;
+    const uint32_t val = tab->braid[tid];
+    const uint4 q = make_uint4(val, val, val, val);
+    char *dst = reinterpret_cast<char *>(s_lds) + (j >> 1) * 65536u + v * 256u + (j & 1u) * 128u;
+#pragma unroll
+    for (int r = 0; r < 8; r++) *reinterpret_cast<uint4 *>(dst + 16 * r) = q;
+    const uint4 *src = reinterpret_cast<const uint4 *>(tab->comb) + tid * 2;
+    uint4 *cdst = reinterpret_cast<uint4 *>(s_lds + kLdsCombDword) + tid * 2;
+    cdst[0] = src[0];
+    cdst[1] = src[1];
+  }
+  __syncthreads();
+
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint64_t w = (uint64_t)blockIdx.x * kWaves + (threadIdx.x >> 6);
+  if (w >= W) return;  // no barrier after this point
+
+  // nominal boundary of wave k: floor(k * total / W), without 128-bit math
+  const uint64_t q_tot = total / W, r_tot = total % W;
+  const uint64_t S0 = uni64(bv.snap(q_tot * w + (r_tot * w) / W));
+  const uint64_t S1 = uni64((w + 1 == W) ? total : bv.snap(q_tot * (w + 1) + (r_tot * (w + 1)) / W));
+  const bool last_wave = (w + 1 == W);
+  if (S0 >= S1 && !last_wave) return;
+
+  // diagnostic build: wall-clock stamps (s_memrealtime, 100 MHz) per wave
+  const uint64_t t_begin = kStamp ? __builtin_amdgcn_s_memrealtime() : 0;
+  const uint64_t npieces =
+      process_range<kStrided, kD, kAblate, kRotate>(args, bv, s_lds, tab, S0, S1, last_wave, (uint32_t)w, lane);
+  if (kStamp && lane == 0) {
+    args.stamps[4 * w + 0] = t_begin;
+    args.stamps[4 * w + 1] = __builtin_amdgcn_s_memrealtime();
+    args.stamps[4 * w + 2] = npieces;
+    args.stamps[4 * w + 3] = S1 - S0;
   }
 }
 

@@ -41,6 +41,7 @@ struct BatchArgs {
   uint64_t n;
   const TableBlob *tab;
   uint64_t min_range;  // bytes per wave at least (0 = kMinRange)
+  uint64_t *stamps;    // diagnostic builds only (kStamp): 4 words per wave
 };
 
 hipError_t launch_batch(const BatchArgs &args, bool strided, int num_cus, hipStream_t stream);
