@@ -117,3 +117,17 @@ def test_dropin_shadows_reference(tmp_path):
     syms = subprocess.run(["nm", str(obj)], capture_output=True, text=True, check=True).stdout
     assert " U zcrc32" in syms
     assert "crc32_for_byte" not in syms and "cg_crc32_init_tables" not in syms
+
+
+def test_argument_errors_are_reported_not_computed():
+    """Invalid arguments return ZCRC_ERR_ARG (-2) before any device work."""
+    import ctypes
+    lib = _lib.lib()
+    assert lib.zcrc32_batch_device(None, None, None, None, 5, None) == -2
+    assert lib.zcrc32_batch(None, None, None, None, 3, 0) == -2
+    assert lib.zcrc32_batch_device(None, None, None, None, 0, None) == 0  # empty batch: nothing to do
+    out = ctypes.c_uint32()
+    assert lib.zcrc32_checked(None, 10, 0, ctypes.byref(out)) == -2
+    assert b"null" in lib.zcrc_last_error()
+    assert lib.zcrc32_batch_device_scratch_bytes(8192) == 8 * 8193 + 8  # one plan tile
+    assert lib.zcrc32_batch_device_scratch_bytes(8193) == 8 * 8194 + 16

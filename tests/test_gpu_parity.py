@@ -312,3 +312,20 @@ def test_zip_verify_batched(device):
     res = zv.verify(bytes(data), device=device)
     bad = [r for r in res if r.status == zv.ZIP_MISMATCH]
     assert [r.name for r in bad] == [victim.name]
+
+
+def test_concurrent_host_threads_dropin():
+    """ZIPsFS runs one preload thread per root (src/ZIPsFS_async.c:468); the
+    drop-in must be thread-safe: many threads, each with its own staging."""
+    from concurrent.futures import ThreadPoolExecutor
+    bufs = [o.payload(L, 300 + i) for i, L in enumerate([1, 4096, 65537, 1 << 20, 3 << 20, 17, 0, 999_999] * 4)]
+    exp = [zlib.crc32(b.tobytes()) for b in bufs]
+
+    def work(k):
+        return [z.cg_crc32(b) for b in bufs[k::4]] + list(z.crc32_batch(bufs[k::4]))
+
+    with ThreadPoolExecutor(8) as ex:
+        res = list(ex.map(work, range(4)))
+    for k in range(4):
+        e = exp[k::4]
+        assert res[k] == e + e

@@ -553,6 +553,7 @@ int zcrc32_batch_device_ws(const void *const *d_ptrs, const uint64_t *d_lens, co
 int zcrc32_batch_device(const void *const *d_ptrs, const uint64_t *d_lens, const uint32_t *d_seeds_or_null,
                         uint32_t *d_out, size_t n, void *stream) {
   if (n == 0) return ZCRC_OK;
+  if (!d_ptrs || !d_lens || !d_out) return fail(ZCRC_ERR_ARG, "null argument");
   hipStream_t st = static_cast<hipStream_t>(stream);
   const size_t bytes = zcrc32_batch_device_scratch_bytes(n);
   void *scratch = nullptr;
