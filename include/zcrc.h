@@ -59,20 +59,23 @@ int zcrc32_batch(const void *const *ptrs, const size_t *lens, const uint32_t *se
 /* Device-resident batch.  d_ptrs: device array of n device pointers;
  * d_lens: device array of n byte counts; d_seeds_or_null: device array or
  * NULL; d_out: device array of n results.  Asynchronous on `stream`; uses a
- * stream-ordered scratch allocation of 8*(n+1) + 8*ceil(n/8192) bytes. */
+ * stream-ordered scratch allocation of 256 + 8*(n+1) + 8*ceil(n/8192) bytes
+ * (work counter, length prefix, plan tile sums). */
 int zcrc32_batch_device(const void *const *d_ptrs, const uint64_t *d_lens,
                         const uint32_t *d_seeds_or_null, uint32_t *d_out, size_t n, void *stream);
 
 /* Same, with caller-owned scratch (graph-capturable: no allocation inside).
- * Needs zcrc32_batch_device_scratch_bytes(n) bytes of device memory. */
+ * Needs zcrc32_batch_device_scratch_bytes(n) bytes of device memory,
+ * 256-byte aligned for best performance.  One scratch per in-flight call. */
 size_t zcrc32_batch_device_scratch_bytes(size_t n);
 int zcrc32_batch_device_ws(const void *const *d_ptrs, const uint64_t *d_lens,
                            const uint32_t *d_seeds_or_null, uint32_t *d_out, size_t n,
                            void *d_scratch, size_t scratch_bytes, void *stream);
 
 /* Device-resident batch of equal-size chunks: buffer i = d_base + i*stride,
- * each `len` bytes (fixed-size cache chunks).  No scratch, one launch (plus a
- * memset of d_out when chunks may be split across waves). */
+ * each `len` bytes (fixed-size cache chunks).  One launch per 4 TiB, plus a
+ * memset of d_out when chunks may be split across waves and, for batches of
+ * >= 1 GiB, a 256-byte stream-ordered allocation for the work counter. */
 int zcrc32_batch_device_strided(const void *d_base, uint64_t stride, uint64_t len, size_t n,
                                 const uint32_t *d_seeds_or_null, uint32_t *d_out, void *stream);
 

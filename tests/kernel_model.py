@@ -18,10 +18,12 @@ ONE = 0x80000000
 
 # constants mirrored from zcrc_internal.h
 K_WAVES = 16
-K_MIN_RANGE = 256 << 10
+K_MIN_RANGE = 64 << 10
 K_SPLIT_GRAIN = 64 << 10
 K_SPLIT_MIN = 2 * K_SPLIT_GRAIN
 K_MIN_PIECE = 4096
+K_DYN_UNIT = 128 << 10
+K_DYN_SHIFT = 1
 
 
 def times_x(r: int) -> int:
@@ -141,16 +143,35 @@ class Batch:
         return b0 + q
 
 
-def wave_ranges(batch: Batch, num_cus: int):
+def wave_ranges(batch: Batch, num_cus: int, dyn_shift: int = K_DYN_SHIFT, unit: int = K_DYN_UNIT):
+    """Every (s0, s1, last) range the kernel processes: W static wave ranges
+    over the first Ts bytes, then the dynamic units of `unit` nominal bytes
+    over the last Td = total >> dyn_shift bytes (zcrc_batch_kernel.h,
+    crc32_batch_kernel).  Which wave claims a unit does not matter for the
+    result, so the model lists them in order."""
     total = batch.total
     want = max(1, (total + K_MIN_RANGE - 1) // K_MIN_RANGE)
     W = min(want, num_cus * K_WAVES)
-    q, r = divmod(total, W)
+    Td = (total >> dyn_shift) if dyn_shift else 0
+    if Td // W < unit:
+        Td = 0
+    Ts = total - Td
+    q, r = divmod(Ts, W)
     out = []
     for w in range(W):
         s0 = batch.snap(q * w + (r * w) // W)
-        s1 = total if w + 1 == W else batch.snap(q * (w + 1) + (r * (w + 1)) // W)
-        out.append((s0, s1, w + 1 == W))
+        if w + 1 == W:
+            s1 = batch.snap(Ts) if Td else total
+        else:
+            s1 = batch.snap(q * (w + 1) + (r * (w + 1)) // W)
+        out.append((s0, s1, w + 1 == W and not Td))
+    units = (Td + unit - 1) // unit if Td else 0
+    for u in range(units):
+        t0 = Ts + u * unit
+        last = u + 1 == units
+        s0 = batch.snap(min(t0, total))
+        s1 = total if last else batch.snap(min(t0 + unit, total))
+        out.append((s0, s1, last))
     return out
 
 
@@ -232,11 +253,11 @@ def crc_piece(mem: np.ndarray, pstart: int, pend: int, inj: int, T: Tables) -> i
     return r0
 
 
-def run_batch(batch: Batch, num_cus: int = 256) -> np.ndarray:
+def run_batch(batch: Batch, num_cus: int = 256, dyn_shift: int = K_DYN_SHIFT, unit: int = K_DYN_UNIT) -> np.ndarray:
     """CRCs of every buffer, computed the way the kernel computes them."""
     T = tables()
     out = np.zeros(batch.n, dtype=np.uint32)
-    for (s0, s1, last) in wave_ranges(batch, num_cus):
+    for (s0, s1, last) in wave_ranges(batch, num_cus, dyn_shift, unit):
         for (i, rel_lo, rel_hi) in wave_pieces(batch, s0, s1, last):
             n = batch.lens[i]
             seed = batch.seeds[i]

@@ -129,5 +129,5 @@ def test_argument_errors_are_reported_not_computed():
     out = ctypes.c_uint32()
     assert lib.zcrc32_checked(None, 10, 0, ctypes.byref(out)) == -2
     assert b"null" in lib.zcrc_last_error()
-    assert lib.zcrc32_batch_device_scratch_bytes(8192) == 8 * 8193 + 8  # one plan tile
-    assert lib.zcrc32_batch_device_scratch_bytes(8193) == 8 * 8194 + 16
+    assert lib.zcrc32_batch_device_scratch_bytes(8192) == 256 + 8 * 8193 + 8  # counter line | prefix | one plan tile
+    assert lib.zcrc32_batch_device_scratch_bytes(8193) == 256 + 8 * 8194 + 16

@@ -196,6 +196,44 @@ def test_random_mixed_batches_vs_oracle():
         np.testing.assert_array_equal(got, exp, err_msg=f"trial {trial}")
 
 
+def test_dynamic_half_large_mixed_batch():
+    """>= 1 GiB so the kernel's dynamic half engages (total >> 1 >= waves x
+    128 KiB units): claimed units cut buffers at arbitrary places, next to
+    empty, tiny and unaligned buffers with random seeds.  Every CRC vs the
+    oracle; the pointer-array form in shuffled address order and the strided
+    form."""
+    rnd = random.Random(2024)
+    kinds = [lambda: 0, lambda: rnd.randint(1, 3), lambda: rnd.randint(4, 5000), lambda: rnd.randint(60_000, 140_000),
+             lambda: rnd.randint(1 << 20, 3 << 20), lambda: rnd.randint(20 << 20, 70 << 20)]
+    lens = [rnd.choice(kinds)() for _ in range(2500)]
+    total = sum(lens) + 64 * len(lens)
+    assert sum(lens) >= 2 * z.device_info()["num_cus"] * 16 * (128 << 10)
+    mem = torch.randint(0, 256, (total,), dtype=torch.uint8, device=DEV)
+    offs, pos = [], 0
+    for L in lens:
+        pos += rnd.randint(0, 60)
+        offs.append(pos)
+        pos += L
+    order = list(range(len(lens)))
+    rnd.shuffle(order)  # batch order != address order
+    ptrs = torch.tensor([mem.data_ptr() + offs[i] for i in order], dtype=torch.int64, device=DEV)
+    lt = torch.tensor([lens[i] for i in order], dtype=torch.int64, device=DEV)
+    seeds_np = np.array([rnd.getrandbits(32) for _ in lens], dtype=np.uint32)
+    seeds = torch.tensor(seeds_np.view(np.int32), device=DEV)
+    got = u32(z.crc32_batch_device(ptrs, lt, seeds=seeds))
+    host = mem.cpu().numpy()
+    ap = np.array([host.ctypes.data + offs[i] for i in order], dtype=np.uint64)
+    exp = o.crc32_batch(ap, np.array([lens[i] for i in order], dtype=np.uint64), seeds_np, nthreads=16)
+    np.testing.assert_array_equal(got, exp)
+    # strided: 1100 x (1 MiB + 17) at stride +13, seeds chained from above
+    n, L, stride = 1100, (1 << 20) + 17, (1 << 20) + 30
+    got = u32(z.crc32_batch_strided(mem, stride, L, n, seeds=seeds[:n], base_offset=7))
+    ap = host.ctypes.data + 7 + np.arange(n, dtype=np.uint64) * stride
+    exp = o.crc32_batch(ap, np.full(n, L, dtype=np.uint64), seeds_np[:n], nthreads=16)
+    np.testing.assert_array_equal(got, exp)
+    del host
+
+
 def test_strided_api_seeds_and_stride():
     n, L, stride = 300, 200_000, 200_064
     mem, ptrs, lens = _strided_fill(n, L, stride=stride, index0=1000)

@@ -42,9 +42,9 @@ def test_model_all_empty_and_single():
     assert list(km.run_batch(b)) == [zlib.crc32(mem[3:12].tobytes())]
 
 
-def _check_partition(b, num_cus):
+def _check_partition(b, num_cus, dyn_shift=km.K_DYN_SHIFT):
     cover = {i: [] for i in range(b.n)}
-    for (s0, s1, last) in km.wave_ranges(b, num_cus):
+    for (s0, s1, last) in km.wave_ranges(b, num_cus, dyn_shift):
         for (i, lo, hi) in km.wave_pieces(b, s0, s1, last):
             cover[i].append((lo, hi))
     for i in range(b.n):
@@ -73,10 +73,44 @@ def test_partition_invariants(seed):
     mem = np.zeros(1, dtype=np.uint8)
     b = km.Batch(mem, [0] * n, lens)
     for num_cus in (1, 3, 256):
-        _check_partition(b, num_cus)
+        for dyn_shift in (0, 1, 2):
+            _check_partition(b, num_cus, dyn_shift)
 
 
 def test_partition_config4_shape():
     lens = [int(x) for x in o.zipf_lens(100000)]
     b = km.Batch(np.zeros(1, dtype=np.uint8), [0] * len(lens), lens)
     _check_partition(b, 256)
+    _check_partition(b, 256, 0)
+
+
+def test_dynamic_units_chain():
+    """Static ranges and dynamic units tile [0, total) exactly, including
+    totals that are not multiples of the unit; config 3 engages the dynamic
+    half with one claim counter of 262144 units."""
+    for total in (2**36, 2**36 + 12345, 13_123_505_587, 3 * 2**30 + 7):
+        b = km.Batch(np.zeros(1, dtype=np.uint8), [0], [total])
+        rs = km.wave_ranges(b, 256)
+        assert sum(1 for *_, last in rs if last) == 1
+        ends = sorted((s0, s1) for s0, s1, _ in rs if s1 > s0)
+        assert ends[0][0] == 0 and ends[-1][1] == total
+        for (a0, a1), (c0, c1) in zip(ends, ends[1:]):
+            assert a1 == c0
+    b = km.Batch(np.zeros(1, dtype=np.uint8), [0] * 65536, [1 << 20] * 65536)
+    assert len(km.wave_ranges(b, 256)) == 4096 + (2**35 >> 17)
+
+
+@pytest.mark.parametrize("dyn_shift,unit", [(1, 128 << 10), (2, 128 << 10), (1, 200_000)])
+def test_model_dynamic_tail_matches_oracle(dyn_shift, unit):
+    rnd = random.Random(7 + dyn_shift)
+    mem = np.random.default_rng(dyn_shift).integers(0, 256, size=21_000_000, dtype=np.uint8)
+    lens = [0, 3, 4000, 70000, 200_001, 1 << 20, 3_000_017, 3_000_017, 5_000_011, 65536, 2, 131072,
+            4_000_003] + [rnd.randint(0, 300_000) for _ in range(4)]
+    rnd.shuffle(lens)
+    addrs, seeds = _mk_batch(rnd, mem.size, lens)
+    b = km.Batch(mem, addrs, lens, seeds)
+    ranges = km.wave_ranges(b, 1, dyn_shift, unit)
+    assert len(ranges) > 16, "dynamic tail must be active in this case"
+    got = km.run_batch(b, num_cus=1, dyn_shift=dyn_shift, unit=unit)
+    exp = [o.cg_crc32(mem[a:a + L], s) for a, L, s in zip(addrs, lens, seeds)]
+    assert list(got) == exp

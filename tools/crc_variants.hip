@@ -31,13 +31,15 @@ static float time_it(kfn k, const BatchArgs &a, int cus, int reps) {
   CHECK(hipEventCreate(&e1));
   const uint64_t nb = a.n;
   CHECK(hipMemsetAsync(a.out, 0, nb * 4, 0));
+  if (a.ctr) CHECK(hipMemsetAsync(a.ctr, 0, 4, 0));
   hipLaunchKernelGGL(k, dim3(cus), dim3(kThreads), 0, 0, a);
   CHECK(hipDeviceSynchronize());
   float total = 0;
   for (int r = 0; r < reps; r++) {
     // per-launch reset of the work counter and of out[] (split pieces xor into
     // it); the memsets are outside the timed interval
-      CHECK(hipMemsetAsync(a.out, 0, nb * 4, 0));
+    CHECK(hipMemsetAsync(a.out, 0, nb * 4, 0));
+    if (a.ctr) CHECK(hipMemsetAsync(a.ctr, 0, 4, 0));
     CHECK(hipEventRecord(e0, 0));
     hipLaunchKernelGGL(k, dim3(cus), dim3(kThreads), 0, 0, a);
     CHECK(hipEventRecord(e1, 0));
@@ -118,24 +120,32 @@ int main(int argc, char **argv) {
     const char *name;
     kfn k;
     bool check;
+    uint32_t dyn;
+    uint64_t unit;
   } vs[] = {
-      {"static", crc32_batch_kernel<false, 4, 0, true>, true},
+      {"static", crc32_batch_kernel<false, 4, 0, true, false, 0>, true, 0, 0},
+      {"prio", crc32_batch_kernel<false, 4, 0, true, false, 1>, true, 0, 0},
+      {"product", crc32_batch_kernel<false, 4, 0, true, false, 1>, true, kDynShift, kDynUnit},
+      {"p+d2u128", crc32_batch_kernel<false, 4, 0, true, false, 1>, true, 2, 128 << 10},
   };
   uint32_t *d_counter;
   CHECK(hipMalloc(&d_counter, 32));
   CHECK(hipMemset(d_counter, 0, 32));
+  a.ctr = d_counter;
 
   const uint64_t ranges[] = {65536};
   uint32_t *h_ref = (uint32_t *)malloc(nbuf * 4), *h_out = (uint32_t *)malloc(nbuf * 4);
   a.out = ref;
   CHECK(hipMemset(ref, 0, nbuf * 4));
   CHECK(hipMemset(d_counter, 0, 32));
-  hipLaunchKernelGGL((crc32_batch_kernel<false, 4, 0, true>), dim3(cus), dim3(kThreads), 0, 0, a);
+  hipLaunchKernelGGL((crc32_batch_kernel<false, 4, 0, true, false, 0>), dim3(cus), dim3(kThreads), 0, 0, a);
   CHECK(hipDeviceSynchronize());
   CHECK(hipMemcpy(h_ref, ref, nbuf * 4, hipMemcpyDeviceToHost));
   a.out = out;
   // stamp runs: per-wave wall-clock begin/end (100 MHz)
-  auto stamp_run = [&](const char *name, kfn k) {
+  auto stamp_run = [&](const char *name, kfn k, uint32_t dyn, uint64_t unit) {
+    a.dyn_shift = dyn;
+    a.dyn_unit = unit;
     const uint64_t nw = (uint64_t)cus * kWaves;
     uint64_t *dst;
     CHECK(hipMalloc(&dst, nw * 32));
@@ -164,14 +174,46 @@ int main(int argc, char **argv) {
     printf("stamps %-8s waves %zu span %.1f us | wave us p0 %.1f p10 %.1f p50 %.1f p90 %.1f p100 %.1f | end us p10 %.1f p50 %.1f p90 %.1f | w2 %.1f w3 %.1f\n",
            name, dur.size(), (t1 - t0) * 1e-2, pct(dur, 0), pct(dur, .1), pct(dur, .5), pct(dur, .9), pct(dur, 1),
            pct(endt, .1), pct(endt, .5), pct(endt, .9), c2 / dur.size(), c3 / dur.size());
+    // where does the spread live?  by wave slot inside the WG, by XCD, and
+    // within-WG spread vs spread of WG means
+    {
+      double slot[kWaves] = {0}, xcd[8] = {0};
+      int nslot[kWaves] = {0}, nxcd[8] = {0};
+      std::vector<double> wg_mean, wg_spread;
+      for (uint64_t g = 0; g < (uint64_t)cus; g++) {
+        double s = 0, mn = 1e30, mx = 0;
+        int c = 0;
+        for (uint32_t w = 0; w < kWaves; w++) {
+          const uint64_t i = g * kWaves + w;
+          if (!st[4 * i + 1]) continue;
+          const double e = (st[4 * i + 1] - t0) * 1e-2;
+          slot[w] += e, nslot[w]++;
+          xcd[g % 8] += e, nxcd[g % 8]++;
+          s += e, c++, mn = std::min(mn, e), mx = std::max(mx, e);
+        }
+        if (c) wg_mean.push_back(s / c), wg_spread.push_back(mx - mn);
+      }
+      printf("  end us by wave slot:");
+      for (uint32_t w = 0; w < kWaves; w++) printf(" %.0f", nslot[w] ? slot[w] / nslot[w] : 0.0);
+      printf("\n  end us by xcd:");
+      for (int x = 0; x < 8; x++) printf(" %.0f", nxcd[x] ? xcd[x] / nxcd[x] : 0.0);
+      std::sort(wg_mean.begin(), wg_mean.end());
+      std::sort(wg_spread.begin(), wg_spread.end());
+      printf("\n  WG mean end us p0 %.0f p50 %.0f p100 %.0f | within-WG spread us p10 %.0f p50 %.0f p90 %.0f\n",
+             wg_mean.front(), pct(wg_mean, .5), wg_mean.back(), pct(wg_spread, .1), pct(wg_spread, .5),
+             pct(wg_spread, .9));
+    }
     a.stamps = nullptr;
     CHECK(hipFree(dst));
   };
-  stamp_run("static", crc32_batch_kernel<false, 4, 0, true, true>);
+  stamp_run("static", crc32_batch_kernel<false, 4, 0, true, true, 0>, 0, 0);
+  stamp_run("product", crc32_batch_kernel<false, 4, 0, true, true, 1>, kDynShift, kDynUnit);
   for (int round = 0; round < 2; round++) {
     for (uint64_t mr : ranges)
     for (auto &v : vs) {
       a.min_range = mr;
+      a.dyn_shift = v.dyn;
+      a.dyn_unit = v.unit;
       const float ms = time_it(v.k, a, cus, reps);
       int bad = 0;
       if (v.check) {

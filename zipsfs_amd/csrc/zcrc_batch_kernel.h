@@ -128,7 +128,9 @@ struct BatchView {
   __device__ uint64_t prefix(uint64_t i) const { return kStrided ? i * a.len : a.prefix[i]; }
   __device__ const uint8_t *ptr(uint64_t i) const { return kStrided ? a.base + i * a.stride : a.ptrs[i]; }
   __device__ uint32_t seed(uint64_t i) const { return a.seeds ? a.seeds[i] : 0u; }
-  __device__ uint64_t total() const { return kStrided ? a.n * a.len : a.prefix[a.n]; }
+  // read once per wave: prefix[n] would otherwise be re-read by every snap
+  const uint64_t tot_ = kStrided ? a.n * a.len : uni64(a.prefix[a.n]);
+  __device__ uint64_t total() const { return tot_; }
 
   // First i in [0, n] with prefix(i) >= t (prefix(n) = total >= t).  Wave-wide
   // 64-ary search; every lane returns the same value.
@@ -161,17 +163,84 @@ struct BatchView {
   // never split and split points sit at end-relative multiples of kSplitGrain.
   // Monotone non-decreasing in t, so snapped ranges stay ordered.
   __device__ uint64_t snap(uint64_t t) const {
+    uint64_t lb;
+    return snap_at(t, lower_bound(t), lb);
+  }
+
+  // snap() given i = lower_bound(t); also returns lb = lower_bound(result),
+  // which process_range needs, without a second search in the common cases.
+  __device__ uint64_t snap_at(uint64_t t, uint64_t i, uint64_t &lb) const {
     const uint64_t tot = total();
-    if (t == 0 || t >= tot) return t >= tot ? tot : 0;
-    const uint64_t i = lower_bound(t);
+    if (t == 0) return lb = 0, 0;
+    if (t >= tot) return lb = lower_bound(tot), tot;
     const uint64_t pi = prefix(i);
+    lb = i;
     if (pi == t) return t;
     const uint64_t b0 = prefix(i - 1);
     const uint64_t n = pi - b0, p = t - b0;
-    if (n < kSplitMin) return pi;
+    if (n < kSplitMin) return pi;  // prefix(i-1) < pi: lower_bound(pi) = i
     const uint64_t q = n - kSplitGrain * ((n - p) / kSplitGrain);
-    if (q < kMinPiece) return b0;
-    return b0 + q;
+    if (q < kMinPiece) return lb = lower_bound(b0), b0;  // empty buffers may precede i-1
+    return b0 + q;  // strictly inside buffer i-1
+  }
+
+  // lower_bound of two targets in one 64-ary pass (two independent loads per
+  // level instead of two dependent searches).
+  __device__ void lower_bound2(uint64_t t0, uint64_t t1, uint64_t &r0, uint64_t &r1) const {
+    if (kStrided) {
+      r0 = lower_bound(t0);
+      r1 = lower_bound(t1);
+      return;
+    }
+    const uint32_t lane = threadIdx.x & 63u;
+    uint64_t lo0 = 0, hi0 = a.n, lo1 = 0, hi1 = a.n;
+    while (hi0 - lo0 > 63 || hi1 - lo1 > 63) {
+      const uint64_t st0 = (hi0 - lo0 + 63) / 64, st1 = (hi1 - lo1 + 63) / 64;
+      uint64_t x0 = lo0 + (uint64_t)(lane + 1) * st0, x1 = lo1 + (uint64_t)(lane + 1) * st1;
+      if (x0 > hi0) x0 = hi0;
+      if (x1 > hi1) x1 = hi1;
+      const uint64_t v0 = a.prefix[x0], v1 = a.prefix[x1];
+      const uint64_t m0 = __ballot(v0 >= t0), m1 = __ballot(v1 >= t1);
+      if (hi0 - lo0 > 63) {
+        const uint32_t f = (uint32_t)__builtin_ctzll(m0);
+        const uint64_t nh = lo0 + (uint64_t)(f + 1) * st0;
+        const uint64_t nl = f == 0 ? lo0 : lo0 + (uint64_t)f * st0 + 1;
+        hi0 = uni64(nh < hi0 ? nh : hi0);
+        lo0 = uni64(nl);
+      }
+      if (hi1 - lo1 > 63) {
+        const uint32_t f = (uint32_t)__builtin_ctzll(m1);
+        const uint64_t nh = lo1 + (uint64_t)(f + 1) * st1;
+        const uint64_t nl = f == 0 ? lo1 : lo1 + (uint64_t)f * st1 + 1;
+        hi1 = uni64(nh < hi1 ? nh : hi1);
+        lo1 = uni64(nl);
+      }
+    }
+    const uint64_t x0 = lo0 + lane, x1 = lo1 + lane;
+    const uint64_t v0 = a.prefix[x0 <= hi0 ? x0 : hi0], v1 = a.prefix[x1 <= hi1 ? x1 : hi1];
+    const uint64_t m0 = __ballot(x0 <= hi0 && v0 >= t0), m1 = __ballot(x1 <= hi1 && v1 >= t1);
+    r0 = uni64(lo0 + (uint64_t)__builtin_ctzll(m0));
+    r1 = uni64(lo1 + (uint64_t)__builtin_ctzll(m1));
+  }
+
+  // Snapped range [S0, S1) for nominal [t0, t1) plus the lower bounds of the
+  // snapped ends (process_range's piece walk), with one dual search.
+  // `last`: S1 = total (the caller's final range).
+  __device__ void range(uint64_t t0, uint64_t t1, bool last, uint64_t &S0, uint64_t &S1, uint64_t &lb0,
+                        uint64_t &lb1) const {
+    const uint64_t tot = total();
+    const uint64_t c0 = t0 < tot ? t0 : tot, c1 = t1 < tot ? t1 : tot;
+    uint64_t i0, i1;
+    lower_bound2(c0, c1, i0, i1);
+    S0 = uni64(snap_at(c0, i0, lb0));
+    if (last) {
+      S1 = tot;
+      lb1 = a.n;
+    } else {
+      S1 = uni64(snap_at(c1, i1, lb1));
+    }
+    lb0 = uni64(lb0);
+    lb1 = uni64(lb1);
   }
 };
 
@@ -182,25 +251,34 @@ struct BatchView {
 // Process every piece of the byte range [S0, S1) of the concatenated batch
 // (S0, S1 snapped; `last_range` also takes the trailing empty buffers).
 // Returns the number of pieces.  Wave-uniform; no barriers.
-template <bool kStrided, uint32_t kD, int kAblate, bool kRotate>
+template <bool kStrided, uint32_t kD, int kAblate, bool kRotate, int kPrio = 0>
 __device__ __forceinline__ uint64_t process_range(const BatchArgs &args, const BatchView<kStrided> &bv,
                                                   const uint32_t *s_lds, const TableBlob *tab, uint64_t S0,
-                                                  uint64_t S1, bool last_wave, uint32_t salt, uint32_t lane) {
+                                                  uint64_t S1, bool last_wave, uint32_t salt, uint32_t lane,
+                                                  bool band, uint64_t lb0, uint64_t lb1) {
   // lane constants for the braided lookups
   const uint32_t lo0 = (lane & 31u) * 4u;
   const uint32_t o0 = lo0, o1 = lo0 + 128u, o2 = lo0 + 65536u, o3 = lo0 + 65536u + 128u;
 
   // Buffers [i_first, i_end) overlap this wave's range [S0, S1).
-  uint64_t i_first = bv.lower_bound(S0);
+  // lb0 = lower_bound(S0), lb1 = lower_bound(S1) (BatchView::range)
+  uint64_t i_first = lb0;
   if (i_first > 0 && i_first <= args.n && bv.prefix(i_first) > S0) i_first--;  // S0 inside buffer i-1
   i_first = uni64(i_first);
-  const uint64_t i_end = last_wave ? args.n : uni64(bv.lower_bound(S1));
+  const uint64_t i_end = last_wave ? args.n : lb1;
   const uint64_t npieces = i_end > i_first ? i_end - i_first : 0;
   // Visit the pieces in a per-wave rotated order.  Pieces are independent,
   // and the rotation de-phases waves whose ranges start on large power-of-two
   // boundaries (uniform batches), which otherwise walk the HBM channel
   // interleave in lockstep ("partition camping", tools/hbm_probe: up to -13%).
   const uint64_t rot = (kRotate && npieces > 1) ? (uint64_t)(hash32(salt) % (uint32_t)npieces) : 0;
+
+  // kPrio: least-progress-first issue priority.  Waves of a CU are otherwise
+  // served oldest-first, so with equal byte ranges slot 0-3 finish at ~50% of
+  // the kernel and slots 12-15 at 100% (tools/crc_variants stamps).
+  const uint64_t range_bytes = S1 > S0 ? S1 - S0 : 1;
+  uint64_t done = 0;
+  if (kPrio && band) __builtin_amdgcn_s_setprio(3);
 
   for (uint64_t k = 0; k < npieces; k++) {
     uint64_t i = i_first + k + rot;
@@ -211,6 +289,13 @@ __device__ __forceinline__ uint64_t process_range(const BatchArgs &args, const B
     const uint64_t rel_lo = (S0 > b0 ? S0 - b0 : 0);
     const uint64_t rel_hi = (b1 < S1 || last_wave) ? n : S1 - b0;
     const bool whole = (rel_lo == 0 && rel_hi == n);
+    if (kPrio && band) {
+      const uint32_t lvl = uni32((uint32_t)((4 * done) / range_bytes));
+      if (lvl == 1) __builtin_amdgcn_s_setprio(2);
+      else if (lvl == 2) __builtin_amdgcn_s_setprio(1);
+      else if (lvl >= 3) __builtin_amdgcn_s_setprio(0);
+      done += rel_hi - rel_lo;
+    }
     const uint32_t seed = uni32(bv.seed(i));
     const uint8_t *bptr = reinterpret_cast<const uint8_t *>(uni64(reinterpret_cast<uint64_t>(bv.ptr(i))));
 
@@ -336,7 +421,8 @@ __device__ __forceinline__ uint64_t process_range(const BatchArgs &args, const B
   return npieces;
 }
 
-template <bool kStrided, uint32_t kD = kDepth, int kAblate = 0, bool kRotate = true, bool kStamp = false>
+template <bool kStrided, uint32_t kD = kDepth, int kAblate = 0, bool kRotate = true, bool kStamp = false,
+          int kPrio = 1>
 __global__ __launch_bounds__(kThreads) void crc32_batch_kernel(BatchArgs args) {
   __shared__ __attribute__((aligned(16))) uint32_t s_lds[kLdsBytes / 4];
   const BatchView<kStrided> bv{args};
@@ -370,22 +456,63 @@ __global__ __launch_bounds__(kThreads) void crc32_batch_kernel(BatchArgs args) {
   const uint64_t w = (uint64_t)blockIdx.x * kWaves + (threadIdx.x >> 6);
   if (w >= W) return;  // no barrier after this point
 
-  // nominal boundary of wave k: floor(k * total / W), without 128-bit math
-  const uint64_t q_tot = total / W, r_tot = total % W;
-  const uint64_t S0 = uni64(bv.snap(q_tot * w + (r_tot * w) / W));
-  const uint64_t S1 = uni64((w + 1 == W) ? total : bv.snap(q_tot * (w + 1) + (r_tot * (w + 1)) / W));
-  const bool last_wave = (w + 1 == W);
-  if (S0 >= S1 && !last_wave) return;
+  // Static part: the first Ts = total - Td bytes in W equal snapped ranges,
+  // issue priority banded by progress (kPrio).  Dynamic half: the last
+  // Td = total >> dyn_shift bytes in fixed units claimed from one counter
+  // once a wave's static range is done, so the waves that the hardware
+  // serves faster (older wave slots, some XCDs: tools/crc_variants stamps)
+  // absorb the imbalance.  Units of 128 KiB measured best: larger ones leave
+  // stragglers, smaller ones pay per-piece latency.
+  const uint64_t unit = args.dyn_unit ? args.dyn_unit : kDynUnit;
+  uint64_t Td = (args.ctr && args.dyn_shift) ? (total >> args.dyn_shift) : 0;
+  if (Td / W < unit) Td = 0;  // fewer units than waves: static only
+  const uint64_t Ts = total - Td;
+  const uint64_t units = Td ? (Td + unit - 1) / unit : 0;
+
+  // nominal boundary of wave k: floor(k * Ts / W), without 128-bit math
+  const uint64_t q_tot = Ts / W, r_tot = Ts % W;
+  bool last = (w + 1 == W) && !Td;
+  uint64_t S0, S1, lb0, lb1;
+  bv.range(q_tot * w + (r_tot * w) / W, (w + 1 == W) ? Ts : q_tot * (w + 1) + (r_tot * (w + 1)) / W, last, S0,
+           S1, lb0, lb1);
+  bool band = true;
 
   // diagnostic build: wall-clock stamps (s_memrealtime, 100 MHz) per wave
   const uint64_t t_begin = kStamp ? __builtin_amdgcn_s_memrealtime() : 0;
-  const uint64_t npieces =
-      process_range<kStrided, kD, kAblate, kRotate>(args, bv, s_lds, tab, S0, S1, last_wave, (uint32_t)w, lane);
+  const uint64_t static_bytes = S1 - S0;
+  uint64_t npieces = 0;
+  uint32_t salt = (uint32_t)w;
+  // Claims: the first after the static range; later ones are prefetched
+  // (issued before the current unit is processed, so the atomic's latency
+  // hides behind the unit) while more than 2W units remain -- near the end a
+  // held-but-unstarted unit would become a straggler.
+  uint32_t u = 0, nx = 0;
+  bool have_next = false;
+  for (;;) {
+    if (!band && u + 2 * (uint32_t)W < units) {
+      if (lane == 0) nx = atomicAdd(args.ctr, 1u);
+      have_next = true;
+    }
+    if (S0 < S1 || last)
+      npieces += process_range<kStrided, kD, kAblate, kRotate, kPrio>(args, bv, s_lds, tab, S0, S1, last, salt, lane,
+                                                                       band, lb0, lb1);
+    if (!units) break;
+    if (!have_next && lane == 0) nx = atomicAdd(args.ctr, 1u);
+    have_next = false;
+    u = uni32(nx);
+    if (u >= units) break;
+    const uint64_t t0 = Ts + (uint64_t)u * unit;
+    last = (u + 1 == units);
+    bv.range(t0, t0 + unit, last, S0, S1, lb0, lb1);
+    salt = u ^ 0x9E3779B9u;
+    if (kPrio && band) __builtin_amdgcn_s_setprio(0);
+    band = false;
+  }
   if (kStamp && lane == 0) {
     args.stamps[4 * w + 0] = t_begin;
     args.stamps[4 * w + 1] = __builtin_amdgcn_s_memrealtime();
     args.stamps[4 * w + 2] = npieces;
-    args.stamps[4 * w + 3] = S1 - S0;
+    args.stamps[4 * w + 3] = static_bytes;
   }
 }
 

@@ -12,6 +12,9 @@ constexpr uint64_t kMinRange = 64ull << 10;    // default minimum bytes per wave
 constexpr uint64_t kSplitGrain = 64ull << 10;  // split points: end-relative multiples
 constexpr uint64_t kSplitMin = 2 * kSplitGrain;  // buffers below this are never split
 constexpr uint64_t kMinPiece = 4096;           // no split piece shorter than this
+constexpr uint64_t kDynUnit = 128ull << 10;    // dynamic-half unit (nominal bytes)
+constexpr uint32_t kDynShift = 1;              // dynamic part = total >> kDynShift
+constexpr size_t kCtrBytes = 256;              // work counter, own cache lines
 constexpr uint32_t kLdsBytes = 163840;         // all 160 KiB of the CU's LDS
 constexpr uint32_t kLdsCombDword = 32768;      // combine tables start at 128 KiB
 constexpr uint32_t kPlanPerThread = 8;
@@ -42,11 +45,18 @@ struct BatchArgs {
   const TableBlob *tab;
   uint64_t min_range;  // bytes per wave at least (0 = kMinRange)
   uint64_t *stamps;    // diagnostic builds only (kStamp): 4 words per wave
+  // dynamic part: the last total >> dyn_shift bytes are handed out in units
+  // of dyn_unit bytes (0 = kDynUnit) through *ctr, which must be zero at
+  // launch; ctr == nullptr or dyn_shift == 0 -> purely static partition
+  uint32_t *ctr;
+  uint32_t dyn_shift;
+  uint64_t dyn_unit;
 };
 
 hipError_t launch_batch(const BatchArgs &args, bool strided, int num_cus, hipStream_t stream);
+inline uint64_t plan_tiles(uint64_t n) { return n == 0 ? 1 : (n + kPlanTile - 1) / kPlanTile; }
 hipError_t launch_plan(const uint64_t *d_lens, uint64_t n, uint64_t *d_prefix, uint64_t *d_tile_sum,
-                       uint32_t *d_out, hipStream_t stream);
+                       uint32_t *d_out, uint32_t *d_ctr, hipStream_t stream);
 
 }  // namespace zcrc
 

@@ -56,9 +56,11 @@ __global__ __launch_bounds__(1024) void plan_tile_sums(const uint64_t *lens, uin
 }
 
 __global__ __launch_bounds__(1024) void plan_tile_scan(const uint64_t *lens, uint64_t n, const uint64_t *tile_sum,
-                                                       uint64_t *prefix, uint32_t *out, int zero_out) {
+                                                       uint64_t *prefix, uint32_t *out, int zero_out,
+                                                       uint32_t *ctr) {
   __shared__ uint64_t s_tmp[16];
   __shared__ uint64_t s_off;
+  if (ctr && blockIdx.x == 0 && threadIdx.x == 0) *ctr = 0u;  // the CRC kernel's work counter
   if (threadIdx.x < 64) {
     uint64_t acc = 0;
     for (uint32_t b = threadIdx.x; b < blockIdx.x; b += 64) acc += tile_sum[b];
@@ -101,15 +103,15 @@ hipError_t launch_batch(const BatchArgs &args, bool strided, int num_cus, hipStr
 }
 
 hipError_t launch_plan(const uint64_t *d_lens, uint64_t n, uint64_t *d_prefix, uint64_t *d_tile_sum,
-                       uint32_t *d_out, hipStream_t stream) {
+                       uint32_t *d_out, uint32_t *d_ctr, hipStream_t stream) {
   const uint64_t tiles = n == 0 ? 1 : (n + kPlanTile - 1) / kPlanTile;
   if (tiles > 1) {
     hipLaunchKernelGGL(plan_tile_sums, dim3((unsigned)tiles), dim3(1024), 0, stream, d_lens, n, d_tile_sum, d_out);
     hipLaunchKernelGGL(plan_tile_scan, dim3((unsigned)tiles), dim3(1024), 0, stream, d_lens, n,
-                       (const uint64_t *)d_tile_sum, d_prefix, d_out, 0);
+                       (const uint64_t *)d_tile_sum, d_prefix, d_out, 0, d_ctr);
   } else {
     hipLaunchKernelGGL(plan_tile_scan, dim3(1), dim3(1024), 0, stream, d_lens, n, (const uint64_t *)d_tile_sum,
-                       d_prefix, d_out, 1);
+                       d_prefix, d_out, 1, d_ctr);
   }
   return hipGetLastError();
 }

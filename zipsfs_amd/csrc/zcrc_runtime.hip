@@ -141,9 +141,13 @@ int batch_device_ws(const void *const *d_ptrs, const uint64_t *d_lens, const uin
   DeviceCtx *dc = nullptr;
   int rc = device_ctx(&dc);
   if (rc) return rc;
-  uint64_t *d_prefix = static_cast<uint64_t *>(scratch);
+  // scratch: work counter (own kCtrBytes line, zeroed by the plan) |
+  // prefix[n+1] | tile sums.  The counter must not share a cache line with
+  // the prefix, which every wave reads while claims hammer the counter.
+  uint32_t *d_ctr = static_cast<uint32_t *>(scratch);
+  uint64_t *d_prefix = reinterpret_cast<uint64_t *>(static_cast<uint8_t *>(scratch) + kCtrBytes);
   uint64_t *d_tiles = d_prefix + (n + 1);
-  ZCRC_HIP_TRY(launch_plan(d_lens, n, d_prefix, d_tiles, d_out, stream));
+  ZCRC_HIP_TRY(launch_plan(d_lens, n, d_prefix, d_tiles, d_out, d_ctr, stream));
   BatchArgs a{};
   a.ptrs = reinterpret_cast<const uint8_t *const *>(d_ptrs);
   a.prefix = d_prefix;
@@ -151,6 +155,8 @@ int batch_device_ws(const void *const *d_ptrs, const uint64_t *d_lens, const uin
   a.out = d_out;
   a.n = n;
   a.tab = dc->d_tab;
+  a.ctr = d_ctr;
+  a.dyn_shift = kDynShift;
   return launch_main(a, false, *dc, stream);
 }
 
@@ -539,10 +545,7 @@ int zcrc32_batch(const void *const *ptrs, const size_t *lens, const uint32_t *se
   return batch_host(ptrs, lens, seeds_or_null, out, n);
 }
 
-size_t zcrc32_batch_device_scratch_bytes(size_t n) {
-  const size_t tiles = n == 0 ? 1 : (n + kPlanTile - 1) / kPlanTile;
-  return 8 * (n + 1) + 8 * tiles;
-}
+size_t zcrc32_batch_device_scratch_bytes(size_t n) { return 8 * (n + 1) + 8 * zcrc::plan_tiles(n) + zcrc::kCtrBytes; }
 
 int zcrc32_batch_device_ws(const void *const *d_ptrs, const uint64_t *d_lens, const uint32_t *d_seeds_or_null,
                            uint32_t *d_out, size_t n, void *d_scratch, size_t scratch_bytes, void *stream) {
@@ -576,9 +579,20 @@ int zcrc32_batch_device_strided(const void *d_base, uint64_t stride, uint64_t le
   hipStream_t st = static_cast<hipStream_t>(stream);
   // keep every launch under kMaxLaunchBytes of payload
   const size_t per = len ? (size_t)std::max<uint64_t>(1, kMaxLaunchBytes / len) : n;
+  // work counter for the kernel's dynamic half, only when it can engage
+  // (at least one kDynUnit per wave): one stream-ordered 64-B allocation
+  uint32_t *d_ctr = nullptr;
+  const uint64_t waves = (uint64_t)dc->num_cus * kWaves;
+  if ((uint64_t)std::min(per, n) * len >> kDynShift >= waves * kDynUnit)
+    ZCRC_HIP_TRY(hipMallocAsync(reinterpret_cast<void **>(&d_ctr), kCtrBytes, st));
   for (size_t first = 0; first < n; first += per) {
     const size_t cnt = std::min(per, n - first);
     BatchArgs a{};
+    if (d_ctr) {
+      ZCRC_HIP_TRY(hipMemsetAsync(d_ctr, 0, 4, st));
+      a.ctr = d_ctr;
+      a.dyn_shift = kDynShift;
+    }
     a.base = static_cast<const uint8_t *>(d_base) + first * stride;
     a.stride = stride;
     a.len = len;
@@ -588,9 +602,13 @@ int zcrc32_batch_device_strided(const void *d_base, uint64_t stride, uint64_t le
     a.tab = dc->d_tab;
     if (len >= kSplitMin) ZCRC_HIP_TRY(hipMemsetAsync(a.out, 0, 4 * cnt, st));
     rc = launch_main(a, true, *dc, st);
-    if (rc) return rc;
+    if (rc) break;
   }
-  return ZCRC_OK;
+  if (d_ctr) {
+    const hipError_t e = hipFreeAsync(d_ctr, st);
+    if (!rc && e != hipSuccess) return fail(ZCRC_ERR_HIP, std::string("hipFreeAsync: ") + hipGetErrorString(e));
+  }
+  return rc;
 }
 
 zcrc32_stream *zcrc32_stream_open(uint32_t seed) {
