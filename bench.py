@@ -270,8 +270,10 @@ def main() -> None:
     traffic_src = "--pmc-traffic-bytes" if traffic is not None else None
     pmc_path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     if traffic is None and os.path.exists(pmc_path):
-        pm = json.load(open(pmc_path))
-        if pm.get("config") == args.config and pm.get("bytes_per_gpu_per_step") == wl.bytes_local:
+        # PMC traffic per config, collected by tools/collect_profiles.sh for
+        # the kernel this build launches (same workload bytes)
+        pm = json.load(open(pmc_path)).get(str(args.config))
+        if pm and pm.get("bytes_per_gpu_per_step") == wl.bytes_local:
             traffic = pm["traffic_bytes_per_launch"]
             traffic_src = pm["source"]
     cpu = None
@@ -312,7 +314,7 @@ def main() -> None:
                 "traffic_unit": "bytes per launch (HBM read+write, PMC)",
                 "traffic_source": traffic_src,
                 "algorithmic_bytes_per_launch": wl.bytes_local,
-                "kernel": "zcrc::crc32_batch_kernel<false, 4u, 0, true>",
+                "kernel": "zcrc::crc32_batch_kernel<false, 4u, 0, true, false, 1>",
                 "avg_kernel_ms": round(avg_kernel_ms, 4),
                 "launches_timed": prof.launches,
             },

@@ -23,7 +23,9 @@ K_SPLIT_GRAIN = 64 << 10
 K_SPLIT_MIN = 2 * K_SPLIT_GRAIN
 K_MIN_PIECE = 4096
 K_DYN_UNIT = 128 << 10
-K_DYN_SHIFT = 1
+K_DYN_AUTO = 0xFF
+K_DYN_SHIFT = K_DYN_AUTO
+K_DYN_SMALL_AVG = 512 << 10
 
 
 def times_x(r: int) -> int:
@@ -152,6 +154,8 @@ def wave_ranges(batch: Batch, num_cus: int, dyn_shift: int = K_DYN_SHIFT, unit: 
     total = batch.total
     want = max(1, (total + K_MIN_RANGE - 1) // K_MIN_RANGE)
     W = min(want, num_cus * K_WAVES)
+    if dyn_shift == K_DYN_AUTO:
+        dyn_shift = 1 if batch.n and total // batch.n < K_DYN_SMALL_AVG else 2
     Td = (total >> dyn_shift) if dyn_shift else 0
     if Td // W < unit:
         Td = 0

@@ -196,25 +196,37 @@ def test_random_mixed_batches_vs_oracle():
         np.testing.assert_array_equal(got, exp, err_msg=f"trial {trial}")
 
 
-def test_dynamic_half_large_mixed_batch():
-    """>= 1 GiB so the kernel's dynamic half engages (total >> 1 >= waves x
-    128 KiB units): claimed units cut buffers at arbitrary places, next to
-    empty, tiny and unaligned buffers with random seeds.  Every CRC vs the
-    oracle; the pointer-array form in shuffled address order and the strided
-    form."""
-    rnd = random.Random(2024)
-    kinds = [lambda: 0, lambda: rnd.randint(1, 3), lambda: rnd.randint(4, 5000), lambda: rnd.randint(60_000, 140_000),
-             lambda: rnd.randint(1 << 20, 3 << 20), lambda: rnd.randint(20 << 20, 70 << 20)]
-    lens = [rnd.choice(kinds)() for _ in range(2500)]
-    total = sum(lens) + 64 * len(lens)
-    assert sum(lens) >= 2 * z.device_info()["num_cus"] * 16 * (128 << 10)
+@pytest.mark.parametrize("shape", ["large_mean", "small_mean"])
+def test_dynamic_part_mixed_batches(shape):
+    """Batches big enough that the kernel's dynamic part engages: claimed
+    128 KiB units cut buffers at arbitrary places, next to empty, tiny and
+    unaligned buffers with random seeds, in shuffled address order.  Mean
+    buffer >= 512 KiB -> a quarter of the bytes dynamic, below -> half
+    (zcrc_internal.h kDynSmallAvg; tests/kernel_model.py mirrors the rule).
+    Every CRC vs the oracle."""
+    rnd = random.Random(2024 if shape == "large_mean" else 99)
+    if shape == "large_mean":
+        kinds = [lambda: 0, lambda: rnd.randint(1, 3), lambda: rnd.randint(4, 5000),
+                 lambda: rnd.randint(60_000, 140_000), lambda: rnd.randint(1 << 20, 3 << 20),
+                 lambda: rnd.randint(4 << 20, 12 << 20)]
+        n = 2500
+    else:
+        kinds = [lambda: 0, lambda: rnd.randint(1, 3), lambda: rnd.randint(4, 5000),
+                 lambda: rnd.randint(60_000, 140_000), lambda: rnd.randint(200_000, 400_000)]
+        n = 16000
+    lens = [rnd.choice(kinds)() for _ in range(n)]
+    cus = z.device_info()["num_cus"]
+    shift = 1 if sum(lens) // n < (512 << 10) else 2
+    assert shift == (2 if shape == "large_mean" else 1)
+    assert (sum(lens) >> shift) // (cus * 16) >= 128 << 10, "dynamic part must engage"
+    total = sum(lens) + 64 * n
     mem = torch.randint(0, 256, (total,), dtype=torch.uint8, device=DEV)
     offs, pos = [], 0
     for L in lens:
         pos += rnd.randint(0, 60)
         offs.append(pos)
         pos += L
-    order = list(range(len(lens)))
+    order = list(range(n))
     rnd.shuffle(order)  # batch order != address order
     ptrs = torch.tensor([mem.data_ptr() + offs[i] for i in order], dtype=torch.int64, device=DEV)
     lt = torch.tensor([lens[i] for i in order], dtype=torch.int64, device=DEV)
@@ -225,12 +237,14 @@ def test_dynamic_half_large_mixed_batch():
     ap = np.array([host.ctypes.data + offs[i] for i in order], dtype=np.uint64)
     exp = o.crc32_batch(ap, np.array([lens[i] for i in order], dtype=np.uint64), seeds_np, nthreads=16)
     np.testing.assert_array_equal(got, exp)
-    # strided: 1100 x (1 MiB + 17) at stride +13, seeds chained from above
-    n, L, stride = 1100, (1 << 20) + 17, (1 << 20) + 30
-    got = u32(z.crc32_batch_strided(mem, stride, L, n, seeds=seeds[:n], base_offset=7))
-    ap = host.ctypes.data + 7 + np.arange(n, dtype=np.uint64) * stride
-    exp = o.crc32_batch(ap, np.full(n, L, dtype=np.uint64), seeds_np[:n], nthreads=16)
-    np.testing.assert_array_equal(got, exp)
+    if shape == "large_mean":
+        # strided form: 2100 x (1 MiB + 17) at stride +13 (2.05 GiB, a quarter dynamic)
+        n, L, stride = 2100, (1 << 20) + 17, (1 << 20) + 30
+        assert n * stride + 7 <= total
+        got = u32(z.crc32_batch_strided(mem, stride, L, n, seeds=seeds[:n], base_offset=7))
+        ap = host.ctypes.data + 7 + np.arange(n, dtype=np.uint64) * stride
+        exp = o.crc32_batch(ap, np.full(n, L, dtype=np.uint64), seeds_np[:n], nthreads=16)
+        np.testing.assert_array_equal(got, exp)
     del host
 
 

@@ -73,7 +73,7 @@ def test_partition_invariants(seed):
     mem = np.zeros(1, dtype=np.uint8)
     b = km.Batch(mem, [0] * n, lens)
     for num_cus in (1, 3, 256):
-        for dyn_shift in (0, 1, 2):
+        for dyn_shift in (0, 1, 2, km.K_DYN_AUTO):
             _check_partition(b, num_cus, dyn_shift)
 
 
@@ -96,8 +96,12 @@ def test_dynamic_units_chain():
         assert ends[0][0] == 0 and ends[-1][1] == total
         for (a0, a1), (c0, c1) in zip(ends, ends[1:]):
             assert a1 == c0
+    # config 3 (1 MiB mean): a quarter dynamic; config 4 (128 KiB mean): half
     b = km.Batch(np.zeros(1, dtype=np.uint8), [0] * 65536, [1 << 20] * 65536)
-    assert len(km.wave_ranges(b, 256)) == 4096 + (2**35 >> 17)
+    assert len(km.wave_ranges(b, 256)) == 4096 + (2**34 >> 17)
+    lens = [int(x) for x in o.zipf_lens(100000)]
+    b = km.Batch(np.zeros(1, dtype=np.uint8), [0] * len(lens), lens)
+    assert len(km.wave_ranges(b, 256)) == 4096 + -(-(sum(lens) >> 1) // (128 << 10))
 
 
 @pytest.mark.parametrize("dyn_shift,unit", [(1, 128 << 10), (2, 128 << 10), (1, 200_000)])

@@ -126,7 +126,9 @@ int main(int argc, char **argv) {
       {"static", crc32_batch_kernel<false, 4, 0, true, false, 0>, true, 0, 0},
       {"prio", crc32_batch_kernel<false, 4, 0, true, false, 1>, true, 0, 0},
       {"product", crc32_batch_kernel<false, 4, 0, true, false, 1>, true, kDynShift, kDynUnit},
+      {"p+d1u128", crc32_batch_kernel<false, 4, 0, true, false, 1>, true, 1, 128 << 10},
       {"p+d2u128", crc32_batch_kernel<false, 4, 0, true, false, 1>, true, 2, 128 << 10},
+      {"p+d3u128", crc32_batch_kernel<false, 4, 0, true, false, 1>, true, 3, 128 << 10},
   };
   uint32_t *d_counter;
   CHECK(hipMalloc(&d_counter, 32));

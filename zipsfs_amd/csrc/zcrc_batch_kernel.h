@@ -457,14 +457,19 @@ __global__ __launch_bounds__(kThreads) void crc32_batch_kernel(BatchArgs args) {
   if (w >= W) return;  // no barrier after this point
 
   // Static part: the first Ts = total - Td bytes in W equal snapped ranges,
-  // issue priority banded by progress (kPrio).  Dynamic half: the last
-  // Td = total >> dyn_shift bytes in fixed units claimed from one counter
+  // issue priority banded by progress (kPrio).  Dynamic part: the last
+  // Td = total >> shift bytes in fixed units claimed from one counter
   // once a wave's static range is done, so the waves that the hardware
   // serves faster (older wave slots, some XCDs: tools/crc_variants stamps)
   // absorb the imbalance.  Units of 128 KiB measured best: larger ones leave
   // stragglers, smaller ones pay per-piece latency.
   const uint64_t unit = args.dyn_unit ? args.dyn_unit : kDynUnit;
-  uint64_t Td = (args.ctr && args.dyn_shift) ? (total >> args.dyn_shift) : 0;
+  // kDynAuto: half the bytes dynamic for batches of small ragged buffers
+  // (per-piece latency varies), a quarter for large buffers (every unit
+  // boundary inside a buffer costs a split piece).
+  const uint32_t shift = args.dyn_shift != kDynAuto ? args.dyn_shift
+                         : (args.n && total / args.n < kDynSmallAvg) ? 1u : 2u;
+  uint64_t Td = (args.ctr && shift) ? (total >> shift) : 0;
   if (Td / W < unit) Td = 0;  // fewer units than waves: static only
   const uint64_t Ts = total - Td;
   const uint64_t units = Td ? (Td + unit - 1) / unit : 0;

@@ -13,7 +13,9 @@ constexpr uint64_t kSplitGrain = 64ull << 10;  // split points: end-relative mul
 constexpr uint64_t kSplitMin = 2 * kSplitGrain;  // buffers below this are never split
 constexpr uint64_t kMinPiece = 4096;           // no split piece shorter than this
 constexpr uint64_t kDynUnit = 128ull << 10;    // dynamic-half unit (nominal bytes)
-constexpr uint32_t kDynShift = 1;              // dynamic part = total >> kDynShift
+constexpr uint32_t kDynAuto = 0xFF;            // dyn_shift: choose by mean buffer size
+constexpr uint32_t kDynShift = kDynAuto;       // dynamic part = total >> shift
+constexpr uint64_t kDynSmallAvg = 512ull << 10;  // mean below: half dynamic, else a quarter
 constexpr size_t kCtrBytes = 256;              // work counter, own cache lines
 constexpr uint32_t kLdsBytes = 163840;         // all 160 KiB of the CU's LDS
 constexpr uint32_t kLdsCombDword = 32768;      // combine tables start at 128 KiB

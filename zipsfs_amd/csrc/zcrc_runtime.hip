@@ -583,7 +583,7 @@ int zcrc32_batch_device_strided(const void *d_base, uint64_t stride, uint64_t le
   // (at least one kDynUnit per wave): one stream-ordered 64-B allocation
   uint32_t *d_ctr = nullptr;
   const uint64_t waves = (uint64_t)dc->num_cus * kWaves;
-  if ((uint64_t)std::min(per, n) * len >> kDynShift >= waves * kDynUnit)
+  if ((uint64_t)std::min(per, n) * len >> 2 >= waves * kDynUnit)  // len >= 512 KiB: a quarter
     ZCRC_HIP_TRY(hipMallocAsync(reinterpret_cast<void **>(&d_ctr), kCtrBytes, st));
   for (size_t first = 0; first < n; first += per) {
     const size_t cnt = std::min(per, n - first);
