@@ -1,7 +1,9 @@
 """oracle/oracle.py -- TEST INFRASTRUCTURE ONLY.
 
-ctypes front-end for the CPU restatement (oracle/crc32_port.c) and, when it
-has been built, the reference's own src/cg_crc32.c (oracle/_ref/).  Only
+ctypes front-end for the CPU restatements (oracle/crc32_port.c, the CRC;
+oracle/inflate_port.c, raw DEFLATE as zlib 1.2.11 accepts it), the system-zlib
+inflate baseline (oracle/zlib_baseline.c) and, when it has been built, the
+reference's own src/cg_crc32.c (oracle/_ref/).  Only
 tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may import
 this module; the product package zipsfs_amd never does.
 """
@@ -54,6 +56,12 @@ def _setup_port(lib: ctypes.CDLL) -> ctypes.CDLL:
     lib.oracle_crc32_batch.restype = ctypes.c_int
     lib.oracle_crc32_batch.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                        ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int]
+    lib.oracle_inflate.restype = ctypes.c_int
+    lib.oracle_inflate.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_size_t,
+                                   ctypes.POINTER(ctypes.c_size_t), ctypes.POINTER(ctypes.c_size_t)]
+    for fn in (lib.oracle_inflate_batch, lib.oracle_zlib_inflate_batch):
+        fn.restype = ctypes.c_int
+        fn.argtypes = [ctypes.c_void_p] * 6 + [ctypes.c_size_t, ctypes.c_int]
     lib.oracle_crc32_batch_fn.restype = ctypes.c_int
     lib.oracle_crc32_batch_fn.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                           ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int]
@@ -172,3 +180,44 @@ def ref_crc32_batch(ptrs: np.ndarray, lens: np.ndarray, seeds=None, nthreads: in
     if rc != 0:
         raise RuntimeError("reference batch failed")
     return out
+
+
+# ------------------------------------------------------------- inflate
+
+INFLATE_STATUS = {0: "ok", 1: "block type", 2: "stored length", 3: "code lengths", 4: "symbol",
+                  5: "distance too far", 6: "output overflow", 7: "input exhausted"}
+
+
+def inflate(src, cap: int) -> tuple:
+    """Raw DEFLATE -> (status, bytes, consumed).  status 0 = ok."""
+    arr, ptr = _buf(src)
+    dst = np.zeros(max(cap, 1), dtype=np.uint8)
+    ol, used = ctypes.c_size_t(0), ctypes.c_size_t(0)
+    rc = port().oracle_inflate(ptr, arr.size, dst.ctypes.data, cap, ctypes.byref(ol), ctypes.byref(used))
+    return rc, dst[:ol.value].tobytes() if rc == 0 else b"", used.value
+
+
+def _inflate_batch(fn, srcs, caps, nthreads):
+    n = len(srcs)
+    keep = [np.frombuffer(bytes(s), dtype=np.uint8) if not isinstance(s, np.ndarray) else s for s in srcs]
+    sp = np.array([k.ctypes.data for k in keep], dtype=np.uint64)
+    sl = np.array([k.size for k in keep], dtype=np.uint64)
+    caps = np.asarray(caps, dtype=np.uint64)
+    outs = [np.empty(max(int(c), 1), dtype=np.uint8) for c in caps]
+    dp = np.array([o.ctypes.data for o in outs], dtype=np.uint64)
+    ol = np.zeros(n, dtype=np.uint64)
+    st = np.zeros(n, dtype=np.int32)
+    if fn(sp.ctypes.data, sl.ctypes.data, dp.ctypes.data, caps.ctypes.data, ol.ctypes.data, st.ctypes.data,
+          n, nthreads) != 0:
+        raise RuntimeError("inflate batch failed to start")
+    return st, ol, outs
+
+
+def inflate_batch(srcs, caps, nthreads: int = 1):
+    """Restatement over many streams (pthread pool) -> (status[], out_len[], outs[])."""
+    return _inflate_batch(port().oracle_inflate_batch, srcs, caps, nthreads)
+
+
+def zlib_inflate_batch(srcs, caps, nthreads: int = 1):
+    """System zlib 1.2.11 raw inflate over many streams: the CPU baseline."""
+    return _inflate_batch(port().oracle_zlib_inflate_batch, srcs, caps, nthreads)
