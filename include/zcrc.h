@@ -79,6 +79,28 @@ int zcrc32_batch_device_ws(const void *const *d_ptrs, const uint64_t *d_lens,
 int zcrc32_batch_device_strided(const void *d_base, uint64_t stride, uint64_t len, size_t n,
                                 const uint32_t *d_seeds_or_null, uint32_t *d_out, void *stream);
 
+/* Batched raw-DEFLATE decode on the GPU.  ZIP method 8
+ * entries are what libzip/zlib inflate under zip_fread() in preloadram_now
+ * (src/ZIPsFS.c:2016-2019, src/ZIPsFS_preloadfileram.c:286-306); the format
+ * is RFC 1951 and streams are accepted exactly when zlib 1.2.11 accepts them.
+ * All pointers are device arrays of n entries: d_src/d_src_len the
+ * compressed streams (< 3.75 GiB each), d_dst/d_cap the output buffers,
+ * d_out_len the bytes produced (0 unless ok), d_status a ZCRC_INFLATE_* per
+ * stream.  One workgroup per stream; asynchronous on `stream`.  Returns
+ * ZCRC_OK when the launch was queued (per-stream results are in d_status). */
+#define ZCRC_INFLATE_OK 0
+#define ZCRC_INFLATE_ERR_BLOCK_TYPE 1  /* block type 3                             */
+#define ZCRC_INFLATE_ERR_STORED_LEN 2  /* stored block LEN != ~NLEN                 */
+#define ZCRC_INFLATE_ERR_CODES 3       /* invalid dynamic header / code lengths     */
+#define ZCRC_INFLATE_ERR_SYMBOL 4      /* invalid literal/length or distance code   */
+#define ZCRC_INFLATE_ERR_DIST 5        /* distance too far back                     */
+#define ZCRC_INFLATE_ERR_OUTPUT 6      /* output larger than d_cap                  */
+#define ZCRC_INFLATE_ERR_INPUT 7       /* input ends before the final block         */
+#define ZCRC_INFLATE_ERR_TOO_BIG 8     /* compressed stream of 3.75 GiB or more     */
+int zcrc_inflate_batch_device(const void *const *d_src, const uint64_t *d_src_len, void *const *d_dst,
+                              const uint64_t *d_cap, uint64_t *d_out_len, int32_t *d_status, size_t n,
+                              void *stream);
+
 /* Streaming / incremental CRC.  ZIPsFS fills a preload
  * buffer in <= 16 MiB zip_fread() chunks (src/ZIPsFS_preloadfileram.c:286-306)
  * and only then CRCs the whole entry under mutex_fhandle (:309-321).  A
@@ -99,12 +121,15 @@ void zcrc32_stream_close(zcrc32_stream *s);
  * src/ZIPsFS_special_file.c:155-163) and checks it after a full preload.
  * zcrc_zip_scan parses the central directory of an archive image (ZIP64
  * included) on the host; zcrc_zip_verify_* checksum the data of every
- * stored (method 0) entry in ONE batched GPU launch and compare.  Entries
- * that need inflating or decrypting are reported as UNVERIFIED. */
+ * stored (method 0) entry in ONE batched GPU launch, inflate every deflated
+ * (method 8) entry on the GPU (one launch per <= 16 GiB of output) and
+ * checksum the outputs in one more, and compare.  Encrypted entries and
+ * other methods are reported as UNVERIFIED. */
 #define ZCRC_ZIP_OK 1
-#define ZCRC_ZIP_MISMATCH 0
-#define ZCRC_ZIP_UNVERIFIED (-1)  /* compressed or encrypted: not checksummed here */
-#define ZCRC_ZIP_BAD (-2)         /* local header or data range outside the archive */
+#define ZCRC_ZIP_MISMATCH 0             /* CRC-32 or uncompressed size differs        */
+#define ZCRC_ZIP_UNVERIFIED (-1)        /* encrypted or other method: not checked     */
+#define ZCRC_ZIP_BAD (-2)               /* local header or data range outside archive */
+#define ZCRC_ZIP_INFLATE_ERROR (-3)     /* deflate stream invalid (see inflate_status) */
 typedef struct zcrc_zip_entry {
   uint64_t data_offset;  /* first byte of the entry's stored data in the archive */
   uint64_t comp_size;    /* bytes of entry data in the archive */
@@ -112,18 +137,18 @@ typedef struct zcrc_zip_entry {
   uint64_t name_offset;  /* file name (central directory copy) in the archive */
   uint32_t name_len;
   uint32_t crc_expected; /* central directory CRC-32 */
-  uint32_t crc_computed; /* set by zcrc_zip_verify_* for stored entries */
+  uint32_t crc_computed; /* set by zcrc_zip_verify_* (stored and deflated entries) */
   uint16_t method;       /* 0 stored, 8 deflate, ... */
   uint16_t flags;        /* general purpose bit flags */
   int32_t status;        /* ZCRC_ZIP_* */
-  uint32_t reserved;
+  int32_t inflate_status; /* ZCRC_INFLATE_* for deflated entries, else 0 */
 } zcrc_zip_entry;
 
 /* Parse the central directory.  entries may be NULL to count; *n_entries
  * receives the number of entries (even when it exceeds `capacity`). */
 int zcrc_zip_scan(const void *archive, size_t archive_len, zcrc_zip_entry *entries, size_t capacity,
                   size_t *n_entries);
-/* Verify with the archive image in host memory (staged to the GPU). */
+/* Verify with the archive image in host memory (staged to HBM once). */
 int zcrc_zip_verify_host(const void *archive, size_t archive_len, zcrc_zip_entry *entries, size_t n);
 /* Verify with the archive image resident in device memory (d_archive);
  * synchronous on `stream`. */

@@ -1,0 +1,97 @@
+"""GPU parity of libzcrc's batched inflate (zcrc_inflate.hip) with zlib
+1.2.11 and the inflate oracle (oracle/inflate_port.c): same corpus as
+tests/test_inflate.py, streams packed unaligned into one device buffer, one
+launch per batch.  Valid streams: bytes identical.  Corrupted streams: the
+GPU reports an error exactly when zlib does, and identical bytes otherwise."""
+import zlib
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+import inflate_streams as S  # noqa: E402
+import zipsfs_amd as z  # noqa: E402
+from oracle import oracle as o  # noqa: E402
+
+DEV = "cuda:0"
+
+
+def _run(streams, caps):
+    arena, dp, out_lens, status = z.inflate_to_device(streams, caps, device=DEV)
+    st = status.cpu().numpy()
+    ol = out_lens.cpu().numpy()
+    host = arena.cpu().numpy()
+    base = arena.data_ptr()
+    offs = (dp.cpu().numpy() - base).astype(np.int64)
+    outs = [host[offs[k]:offs[k] + ol[k]].tobytes() for k in range(len(streams))]
+    return st, ol, outs, arena, dp, out_lens
+
+
+def test_inflate_corpus_bitexact():
+    items = S.corpus()
+    streams = [s for _, s, _ in items]
+    st, ol, outs, *_ = _run(streams, [len(d) for _, _, d in items])
+    for k, (name, _, data) in enumerate(items):
+        assert st[k] == 0, (name, z.INFLATE_STATUS[int(st[k])])
+        assert ol[k] == len(data) and outs[k] == data, name
+
+
+def test_inflate_large_streams():
+    items = []
+    for k, (pname, gen) in enumerate(S.PAYLOADS.items()):
+        data = gen(3_000_000 + 12345 * k, 500 + k)
+        items.append((pname, S.deflate(data, 6), data))
+    items.append(("text-64MiB", S.deflate(S.text_payload(64 << 20, 3), 1), None))
+    caps = [len(d) if d is not None else 64 << 20 for _, _, d in items]
+    st, ol, outs, *_ = _run([s for _, s, _ in items], caps)
+    for k, (name, _, data) in enumerate(items):
+        assert st[k] == 0, name
+        exp = data if data is not None else S.text_payload(64 << 20, 3)
+        assert outs[k] == exp, name
+
+
+def test_inflate_errors_iff_zlib_errors():
+    items = S.corpus()
+    streams, caps, exp = [], [], []
+    for i, (name, stream, data) in enumerate(items):
+        if i % 2:
+            continue
+        for bad in S.corrupt_variants(stream, seed=i):
+            ok, ref = S.zlib_inflate(bad)
+            streams.append(bad)
+            caps.append(300 * len(bad) + 1024)
+            exp.append((name, ok, ref))
+    st, ol, outs, *_ = _run(streams, caps)
+    n_err = 0
+    for k, (name, ok, ref) in enumerate(exp):
+        assert (st[k] == 0) == ok, (name, z.INFLATE_STATUS[int(st[k])], ok)
+        if ok:
+            assert outs[k] == ref, name
+        else:
+            n_err += 1
+    assert n_err > 50
+
+
+def test_inflate_status_codes_match_oracle():
+    data = S.text_payload(5000, 1)
+    stream = S.deflate(data)
+    bits = [1, 1, 0] + [0, 0, 0, 0, 0, 0, 1] + [0, 0, 0, 0, 0]
+    far = sum(b << k for k, b in enumerate(bits)).to_bytes(3, "little")
+    cases = [(stream, len(data) - 1), (stream[:-3], len(data)), (bytes([0x07]), 10),
+             (bytes([0x01, 0x05, 0x00, 0x00, 0x00]), 10), (far, 100), (b"", 10)]
+    st, ol, outs, *_ = _run([c[0] for c in cases], [c[1] for c in cases])
+    want = [o.inflate(s, c)[0] if s else 7 for s, c in cases]
+    assert list(st) == want == [6, 7, 1, 2, 5, 7]
+
+
+def test_inflate_then_crc_on_device():
+    """The ZIP verification shape: inflate a batch in HBM, then CRC the
+    outputs with the batched CRC kernel -- no host round trip."""
+    items = [it for it in S.corpus() if len(it[2]) > 0][:200]
+    st, ol, outs, arena, dp, out_lens = _run([s for _, s, _ in items], [len(d) for _, _, d in items])
+    assert (st == 0).all()
+    crcs = z.crc32_batch_device(dp, out_lens).cpu().numpy().view(np.uint32)
+    assert list(crcs) == [zlib.crc32(d) for _, _, d in items]

@@ -340,30 +340,35 @@ def test_stream_incremental_like_preloadram():
 
 @pytest.mark.parametrize("device", [True, False])
 def test_zip_verify_batched(device):
-    """Whole-archive verification: stored entries in one GPU batch vs the
-    central-directory CRCs zipfile wrote; a flipped byte is caught; deflated
-    entries are verified after host inflate."""
+    """Whole-archive verification vs the central-directory CRCs zipfile
+    wrote: stored entries in one GPU CRC batch, deflated entries inflated on
+    the GPU and checksummed in one more.  A flipped byte in a stored entry is
+    a mismatch; one in a deflated entry is an inflate error or a mismatch."""
     import io
     import zipfile
     from zipsfs_amd import zipverify as zv
+    import inflate_streams as S
     rnd = random.Random(3)
     buf = io.BytesIO()
     with zipfile.ZipFile(buf, "w", allowZip64=True) as zf:
         for i in range(300):
-            data = o.payload(rnd.choice([0, 1, 5, 4095, 65536, 300_000, 2_000_001]), i).tobytes()
-            zf.writestr(f"e{i}", data, compress_type=zipfile.ZIP_STORED if i % 3 else zipfile.ZIP_DEFLATED)
+            n = rnd.choice([0, 1, 5, 4095, 65536, 300_000, 2_000_001])
+            data = o.payload(n, i).tobytes() if i % 2 else S.text_payload(n, i)
+            zf.writestr(f"e{i}", data, compress_type=zipfile.ZIP_STORED if i % 3 else zipfile.ZIP_DEFLATED,
+                        compresslevel=(i % 9) + 1 if i % 3 == 0 else None)
     data = bytearray(buf.getvalue())
     res = zv.verify(bytes(data), device=device)
-    stored = [r for r in res if r.method == 0]
-    assert stored and all(r.status == zv.ZIP_OK for r in stored)
-    assert all(r.status == zv.ZIP_UNVERIFIED for r in res if r.method == 8)
-    res = zv.verify(bytes(data), device=device, inflate=True)
-    assert all(r.status == zv.ZIP_OK for r in res)
-    victim = next(r for r in stored if r.comp_size > 1000)
-    data[victim.data_offset + 500] ^= 0x40
+    assert {r.method for r in res} == {0, 8}
+    assert all(r.status == zv.ZIP_OK for r in res), [(r.name, r.status, r.inflate_status) for r in res if not r.ok]
+    stored = [r for r in res if r.method == 0 and r.comp_size > 1000]
+    deflated = [r for r in res if r.method == 8 and r.comp_size > 1000]
+    data[stored[0].data_offset + 500] ^= 0x40
+    data[deflated[0].data_offset + deflated[0].comp_size // 2] ^= 0x10
     res = zv.verify(bytes(data), device=device)
-    bad = [r for r in res if r.status == zv.ZIP_MISMATCH]
-    assert [r.name for r in bad] == [victim.name]
+    bad = {r.name: r.status for r in res if not r.ok}
+    assert set(bad) == {stored[0].name, deflated[0].name}
+    assert bad[stored[0].name] == zv.ZIP_MISMATCH
+    assert bad[deflated[0].name] in (zv.ZIP_MISMATCH, zv.ZIP_INFLATE_ERROR)
 
 
 def test_concurrent_host_threads_dropin():

@@ -27,6 +27,7 @@ __all__ = [
     "ZcrcError", "Crc32Stream", "cg_crc32", "crc32_batch", "crc32_batch_device", "crc32_batch_device_ws",
     "crc32_batch_strided", "crc32_tensors", "crc32_combine", "fhandle_check_crc32",
     "verify_entries", "fill_synthetic", "profile", "device_info", "version",
+    "inflate_batch_device", "inflate_to_device", "INFLATE_STATUS",
 ]
 
 
@@ -241,6 +242,61 @@ def crc32_tensors(tensors: Sequence, seeds=None, stream=None):
     ptrs = torch.tensor([t.data_ptr() for t in tensors], dtype=torch.int64, device=dev)
     lens = torch.tensor([t.numel() * t.element_size() for t in tensors], dtype=torch.int64, device=dev)
     return crc32_batch_device(ptrs, lens, seeds=seeds, stream=stream)
+
+
+INFLATE_STATUS = {0: "ok", 1: "block type", 2: "stored length", 3: "code lengths", 4: "symbol",
+                  5: "distance too far", 6: "output overflow", 7: "input exhausted", 8: "stream too big"}
+
+
+def inflate_batch_device(src_ptrs, src_lens, dst_ptrs, caps, out_lens=None, status=None, stream=None):
+    """Batched raw-DEFLATE decode on the GPU (zcrc_inflate_batch_device).
+
+    All arguments are int64 device tensors of n entries (addresses / byte
+    counts).  Returns (out_lens int64, status int32) device tensors; status
+    0 = ok, otherwise ZCRC_INFLATE_* (INFLATE_STATUS)."""
+    torch = _torch()
+    for t, name in ((src_ptrs, "src_ptrs"), (src_lens, "src_lens"), (dst_ptrs, "dst_ptrs"), (caps, "caps")):
+        _check_dev(t, name, torch.int64)
+    n = src_ptrs.numel()
+    if not (src_lens.numel() == dst_ptrs.numel() == caps.numel() == n):
+        raise ValueError("length mismatch")
+    if out_lens is None:
+        out_lens = torch.empty(n, dtype=torch.int64, device=src_ptrs.device)
+    if status is None:
+        status = torch.empty(n, dtype=torch.int32, device=src_ptrs.device)
+    check(lib().zcrc_inflate_batch_device(src_ptrs.data_ptr(), src_lens.data_ptr(), dst_ptrs.data_ptr(),
+                                          caps.data_ptr(), out_lens.data_ptr(), status.data_ptr(), n,
+                                          _stream_ptr(stream)), "zcrc_inflate_batch_device")
+    return out_lens, status
+
+
+def inflate_to_device(streams: Sequence, caps: Sequence[int], device="cuda", stream=None):
+    """Upload host DEFLATE streams, inflate them on the GPU into one device
+    arena.  Returns (arena uint8 tensor, dst_ptrs, out_lens, status)."""
+    torch = _torch()
+    n = len(streams)
+    src_off, pos = [], 0
+    for st in streams:
+        src_off.append(pos)
+        pos += len(st)
+    host = np.zeros(max(pos, 1), dtype=np.uint8)
+    for off, st in zip(src_off, streams):
+        host[off:off + len(st)] = np.frombuffer(bytes(st), dtype=np.uint8)
+    src = torch.from_numpy(host).to(device)
+    caps_np = np.asarray(caps, dtype=np.int64)
+    dst_off = np.zeros(n, dtype=np.int64)
+    if n:
+        dst_off[1:] = np.cumsum(caps_np)[:-1]
+    arena = torch.empty(int(caps_np.sum()) + 1, dtype=torch.uint8, device=device)
+    sp = torch.tensor([src.data_ptr() + o for o in src_off], dtype=torch.int64, device=device)
+    sl = torch.tensor([len(st) for st in streams], dtype=torch.int64, device=device)
+    dp = arena.data_ptr() + torch.from_numpy(dst_off).to(device)
+    cp = torch.from_numpy(caps_np).to(device)
+    out_lens, status = inflate_batch_device(sp, sl, dp, cp, stream=stream)
+    # `src` must outlive the kernel: wait before it goes out of scope
+    (torch.cuda.current_stream() if stream is None else stream).synchronize()
+    del src
+    return arena, dp, out_lens, status
 
 
 def fill_synthetic(ptrs, lens, index0: int = 0, index_step: int = 1, seed: int = 0xC0FFEE, stream=None) -> None:

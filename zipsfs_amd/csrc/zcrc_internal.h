@@ -56,6 +56,19 @@ struct BatchArgs {
 };
 
 hipError_t launch_batch(const BatchArgs &args, bool strided, int num_cus, hipStream_t stream);
+// batched raw-DEFLATE decode (zcrc_inflate.hip): device arrays of n
+struct InflateArgs {
+  const uint8_t *const *src;
+  const uint64_t *src_len;
+  uint8_t *const *dst;
+  const uint64_t *cap;
+  uint64_t *out_len;
+  int32_t *status;
+  uint64_t n;
+};
+constexpr uint64_t kInflateMaxSrc = 0xF0000000ull;  // 32-bit buffer range and block arithmetic
+hipError_t launch_inflate(const InflateArgs &args, hipStream_t stream);
+
 inline uint64_t plan_tiles(uint64_t n) { return n == 0 ? 1 : (n + kPlanTile - 1) / kPlanTile; }
 hipError_t launch_plan(const uint64_t *d_lens, uint64_t n, uint64_t *d_prefix, uint64_t *d_tile_sum,
                        uint32_t *d_out, uint32_t *d_ctr, hipStream_t stream);

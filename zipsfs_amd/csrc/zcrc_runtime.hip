@@ -611,6 +611,27 @@ int zcrc32_batch_device_strided(const void *d_base, uint64_t stride, uint64_t le
   return rc;
 }
 
+int zcrc_inflate_batch_device(const void *const *d_src, const uint64_t *d_src_len, void *const *d_dst,
+                              const uint64_t *d_cap, uint64_t *d_out_len, int32_t *d_status, size_t n,
+                              void *stream) {
+  if (n == 0) return ZCRC_OK;
+  if (!d_src || !d_src_len || !d_dst || !d_cap || !d_out_len || !d_status) return fail(ZCRC_ERR_ARG, "null argument");
+  if (n > 0x7FFFFFFFu) return fail(ZCRC_ERR_ARG, "too many streams for one launch");
+  DeviceCtx *dc = nullptr;
+  int rc = device_ctx(&dc);
+  if (rc) return rc;
+  InflateArgs a{};
+  a.src = reinterpret_cast<const uint8_t *const *>(d_src);
+  a.src_len = d_src_len;
+  a.dst = reinterpret_cast<uint8_t *const *>(d_dst);
+  a.cap = d_cap;
+  a.out_len = d_out_len;
+  a.status = d_status;
+  a.n = n;
+  ZCRC_HIP_TRY(launch_inflate(a, static_cast<hipStream_t>(stream)));
+  return ZCRC_OK;
+}
+
 zcrc32_stream *zcrc32_stream_open(uint32_t seed) {
   zcrc32_stream *s = new (std::nothrow) zcrc32_stream();
   if (!s) {

@@ -5,7 +5,10 @@
 // (src/ZIPsFS_preloadfileram.c:237-250).  Here a whole archive is checked at
 // once: the host walks the central directory (APPNOTE 4.3.12/4.3.14/4.3.16,
 // ZIP64 4.5.3) and the data of every stored entry -- a plain byte range of the
-// archive -- is checksummed by one zcrc32_batch* launch.  The scan is bounds
+// archive -- is checksummed by one zcrc32_batch* launch.  Deflated entries
+// (method 8, the zip_fread()/zlib path of src/ZIPsFS.c:2016-2019) are
+// inflated on the GPU into an HBM arena (zcrc_inflate_batch_device) and the
+// outputs checksummed by the same batched CRC kernel.  The scan is bounds
 // checked against the image; it never reads outside [archive, archive+len).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -118,52 +121,98 @@ namespace {
 bool verifiable(const zcrc_zip_entry &E) {
   return E.status != ZCRC_ZIP_BAD && E.method == 0 && !(E.flags & 1u) && E.comp_size == E.uncomp_size;
 }
+// deflated, unencrypted, in range
+bool deflatable(const zcrc_zip_entry &E) { return E.status != ZCRC_ZIP_BAD && E.method == 8 && !(E.flags & 1u); }
 
-void finish(zcrc_zip_entry *entries, size_t n, const std::vector<size_t> &idx, const std::vector<uint32_t> &crc) {
+constexpr uint64_t kArenaBytes = 16ull << 30;  // inflate output per chunk
+
+void finish(zcrc_zip_entry *entries, const std::vector<size_t> &idx, const std::vector<uint32_t> &crc) {
   for (size_t j = 0; j < idx.size(); j++) {
     zcrc_zip_entry &E = entries[idx[j]];
     E.crc_computed = crc[j];
     E.status = crc[j] == E.crc_expected ? ZCRC_ZIP_OK : ZCRC_ZIP_MISMATCH;
   }
-  for (size_t i = 0; i < n; i++)
-    if (!verifiable(entries[i]) && entries[i].status != ZCRC_ZIP_BAD) entries[i].status = ZCRC_ZIP_UNVERIFIED;
+}
+
+// Deflated entries idx[a, b): one inflate launch into an arena, one CRC launch
+// over the outputs (lengths = the central directory's uncompressed sizes; an
+// entry whose inflate fails or yields another size is not a match anyway).
+int verify_deflated_chunk(const uint8_t *d_archive, zcrc_zip_entry *entries, const std::vector<size_t> &idx,
+                          size_t a, size_t b, hipStream_t st) {
+  const size_t m = b - a;
+  std::vector<uint64_t> h(4 * m);  // src | src_len | dst | cap
+  uint64_t arena_bytes = 0;
+  for (size_t j = 0; j < m; j++) {
+    const zcrc_zip_entry &E = entries[idx[a + j]];
+    h[j] = reinterpret_cast<uint64_t>(d_archive) + E.data_offset;
+    h[m + j] = E.comp_size;
+    h[2 * m + j] = arena_bytes;
+    h[3 * m + j] = E.uncomp_size;
+    arena_bytes += E.uncomp_size;
+  }
+  void *d_arena = nullptr, *d_desc = nullptr;
+  if (hipMallocAsync(&d_arena, arena_bytes + 16, st) != hipSuccess) return zfail("inflate arena allocation failed");
+  if (hipMallocAsync(&d_desc, 8 * 5 * m + 8 * m, st) != hipSuccess) {
+    (void)hipFreeAsync(d_arena, st);
+    return zfail("inflate descriptor allocation failed");
+  }
+  for (size_t j = 0; j < m; j++) h[2 * m + j] += reinterpret_cast<uint64_t>(d_arena);
+  uint64_t *dd = static_cast<uint64_t *>(d_desc);
+  uint64_t *d_src = dd, *d_srclen = dd + m, *d_dst = dd + 2 * m, *d_cap = dd + 3 * m, *d_olen = dd + 4 * m;
+  int32_t *d_status = reinterpret_cast<int32_t *>(dd + 5 * m);
+  uint32_t *d_crc = reinterpret_cast<uint32_t *>(d_status + m);
+  std::vector<uint64_t> olen(m);
+  std::vector<int32_t> status(m);
+  std::vector<uint32_t> crc(m);
+  int rc = ZCRC_OK;
+  if (hipMemcpyAsync(dd, h.data(), 8 * 4 * m, hipMemcpyHostToDevice, st) != hipSuccess)
+    rc = zfail("descriptor upload failed");
+  if (!rc)
+    rc = zcrc_inflate_batch_device(reinterpret_cast<const void *const *>(d_src), d_srclen,
+                                   reinterpret_cast<void *const *>(d_dst), d_cap, d_olen, d_status, m, st);
+  if (!rc) rc = zcrc32_batch_device(reinterpret_cast<const void *const *>(d_dst), d_cap, nullptr, d_crc, m, st);
+  if (!rc && (hipMemcpyAsync(olen.data(), d_olen, 8 * m, hipMemcpyDeviceToHost, st) != hipSuccess ||
+              hipMemcpyAsync(status.data(), d_status, 4 * m, hipMemcpyDeviceToHost, st) != hipSuccess ||
+              hipMemcpyAsync(crc.data(), d_crc, 4 * m, hipMemcpyDeviceToHost, st) != hipSuccess))
+    rc = zfail("result download failed");
+  (void)hipFreeAsync(d_desc, st);
+  (void)hipFreeAsync(d_arena, st);
+  if (!rc && hipStreamSynchronize(st) != hipSuccess) rc = zfail("stream synchronize failed");
+  if (rc) return rc;
+  for (size_t j = 0; j < m; j++) {
+    zcrc_zip_entry &E = entries[idx[a + j]];
+    E.inflate_status = status[j];
+    if (status[j] != ZCRC_INFLATE_OK) {
+      E.status = ZCRC_ZIP_INFLATE_ERROR;
+      continue;
+    }
+    E.crc_computed = crc[j];
+    E.status = (olen[j] == E.uncomp_size && crc[j] == E.crc_expected) ? ZCRC_ZIP_OK : ZCRC_ZIP_MISMATCH;
+  }
+  return ZCRC_OK;
 }
 
 }  // namespace
-
-extern "C" int zcrc_zip_verify_host(const void *archive, size_t archive_len, zcrc_zip_entry *entries, size_t n) {
-  if (!archive || (n && !entries)) return zfail("null argument");
-  const uint8_t *a = static_cast<const uint8_t *>(archive);
-  std::vector<size_t> idx;
-  std::vector<const void *> ptrs;
-  std::vector<size_t> lens;
-  for (size_t i = 0; i < n; i++)
-    if (verifiable(entries[i]) && entries[i].data_offset + entries[i].comp_size <= archive_len) {
-      idx.push_back(i);
-      ptrs.push_back(a + entries[i].data_offset);
-      lens.push_back(entries[i].comp_size);
-    }
-  std::vector<uint32_t> crc(idx.size());
-  if (!idx.empty()) {
-    const int rc = zcrc32_batch(ptrs.data(), lens.data(), nullptr, crc.data(), idx.size(), 0);
-    if (rc) return rc;
-  }
-  finish(entries, n, idx, crc);
-  return ZCRC_OK;
-}
 
 extern "C" int zcrc_zip_verify_device(const void *d_archive, size_t archive_len, zcrc_zip_entry *entries, size_t n,
                                       void *stream) {
   if (!d_archive || (n && !entries)) return zfail("null argument");
   hipStream_t st = static_cast<hipStream_t>(stream);
-  std::vector<size_t> idx;
+  std::vector<size_t> idx, didx;
   std::vector<uint64_t> hp, hl;
-  for (size_t i = 0; i < n; i++)
-    if (verifiable(entries[i]) && entries[i].data_offset + entries[i].comp_size <= archive_len) {
+  for (size_t i = 0; i < n; i++) {
+    zcrc_zip_entry &E = entries[i];
+    if (E.status == ZCRC_ZIP_BAD) continue;
+    E.status = ZCRC_ZIP_UNVERIFIED;  // until checked below
+    if (E.data_offset + E.comp_size > archive_len) continue;
+    if (verifiable(E)) {
       idx.push_back(i);
-      hp.push_back(reinterpret_cast<uint64_t>(d_archive) + entries[i].data_offset);
-      hl.push_back(entries[i].comp_size);
+      hp.push_back(reinterpret_cast<uint64_t>(d_archive) + E.data_offset);
+      hl.push_back(E.comp_size);
+    } else if (deflatable(E)) {
+      didx.push_back(i);
     }
+  }
   std::vector<uint32_t> crc(idx.size());
   if (!idx.empty()) {
     const size_t m = idx.size();
@@ -182,6 +231,33 @@ extern "C" int zcrc_zip_verify_device(const void *d_archive, size_t archive_len,
     if (!rc && hipStreamSynchronize(st) != hipSuccess) rc = zfail("stream synchronize failed");
     if (rc) return rc;
   }
-  finish(entries, n, idx, crc);
+  finish(entries, idx, crc);
+  // deflated entries in chunks of <= kArenaBytes of output
+  for (size_t a = 0; a < didx.size();) {
+    size_t b = a;
+    uint64_t bytes = 0;
+    while (b < didx.size() && (b == a || bytes + entries[didx[b]].uncomp_size <= kArenaBytes))
+      bytes += entries[didx[b++]].uncomp_size;
+    const int rc = verify_deflated_chunk(static_cast<const uint8_t *>(d_archive), entries, didx, a, b, st);
+    if (rc) return rc;
+    a = b;
+  }
   return ZCRC_OK;
+}
+
+extern "C" int zcrc_zip_verify_host(const void *archive, size_t archive_len, zcrc_zip_entry *entries, size_t n) {
+  if (!archive || (n && !entries)) return zfail("null argument");
+  // stage the image once and verify it where the GPU reads it
+  hipStream_t st = nullptr;
+  if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess) return zfail("stream create failed");
+  void *d = nullptr;
+  int rc = ZCRC_OK;
+  if (hipMallocAsync(&d, archive_len ? archive_len : 1, st) != hipSuccess) rc = zfail("archive allocation failed");
+  if (!rc && archive_len && hipMemcpyAsync(d, archive, archive_len, hipMemcpyHostToDevice, st) != hipSuccess)
+    rc = zfail("archive upload failed");
+  if (!rc) rc = zcrc_zip_verify_device(d, archive_len, entries, n, st);
+  if (d) (void)hipFreeAsync(d, st);
+  (void)hipStreamSynchronize(st);
+  (void)hipStreamDestroy(st);
+  return rc;
 }

@@ -5,14 +5,14 @@ libzip (``zip_stat`` -> ``st.crc``, src/ZIPsFS.c:998; shown to users as
 ``<entry>@ARCHIVECRC32.TXT``, src/ZIPsFS_special_file.c:155-163) and checks
 it after a full preload (src/ZIPsFS_preloadfileram.c:237-250).  This module
 checks a whole archive at once: libzcrc parses the central directory
-(ZIP64 aware) and checksums every stored entry in one batched GPU launch.
-Deflated entries can optionally be inflated on the host (zlib inflate -- not a
-CRC) and then checksummed on the GPU in the same way.
+(ZIP64 aware), checksums every stored entry in one batched GPU launch, and
+inflates every deflated entry on the GPU (zcrc_inflate.hip, SURVEY 8(f) rank
+4) into HBM, where the same batched CRC kernel checks the outputs.  Nothing is
+decompressed or checksummed on the host.
 """
 from __future__ import annotations
 
 import ctypes
-import zlib as _inflate_only  # used for raw-DEFLATE decompression only, never for CRCs
 from dataclasses import dataclass
 from typing import List, Optional
 
@@ -20,7 +20,7 @@ import numpy as np
 
 from ._lib import ZcrcError, check, lib
 
-ZIP_OK, ZIP_MISMATCH, ZIP_UNVERIFIED, ZIP_BAD = 1, 0, -1, -2
+ZIP_OK, ZIP_MISMATCH, ZIP_UNVERIFIED, ZIP_BAD, ZIP_INFLATE_ERROR = 1, 0, -1, -2, -3
 
 
 class _Entry(ctypes.Structure):
@@ -28,7 +28,7 @@ class _Entry(ctypes.Structure):
                 ("uncomp_size", ctypes.c_uint64), ("name_offset", ctypes.c_uint64),
                 ("name_len", ctypes.c_uint32), ("crc_expected", ctypes.c_uint32),
                 ("crc_computed", ctypes.c_uint32), ("method", ctypes.c_uint16),
-                ("flags", ctypes.c_uint16), ("status", ctypes.c_int32), ("reserved", ctypes.c_uint32)]
+                ("flags", ctypes.c_uint16), ("status", ctypes.c_int32), ("inflate_status", ctypes.c_int32)]
 
 
 _SIGS = False
@@ -61,6 +61,7 @@ class ZipEntryCheck:
     crc_expected: int
     crc_computed: Optional[int]
     status: int
+    inflate_status: int = 0
 
     @property
     def ok(self) -> bool:
@@ -96,16 +97,19 @@ def _to_check(a: np.ndarray, e) -> ZipEntryCheck:
     name = a[e.name_offset: e.name_offset + e.name_len].tobytes().decode("utf-8", "replace")
     computed = e.crc_computed if e.status in (ZIP_OK, ZIP_MISMATCH) else None
     return ZipEntryCheck(name, e.method, e.comp_size, e.uncomp_size, e.data_offset, e.crc_expected, computed,
-                         e.status)
+                         e.status, e.inflate_status)
 
 
-def verify(archive, device: bool = True, inflate: bool = False) -> List[ZipEntryCheck]:
-    """Verify every entry's CRC against the central directory on the GPU.
+def verify(archive, device: bool = True) -> List[ZipEntryCheck]:
+    """Verify every entry's CRC-32 (and size) against the central directory.
 
-    device=True stages the archive image into HBM once and checksums all
-    stored entries in one launch (zcrc_zip_verify_device); device=False uses
-    the host-resident path.  With inflate=True, deflated entries are inflated
-    on the host and their bytes checksummed on the GPU in one more batch.
+    device=True stages the archive image into HBM through torch and calls
+    zcrc_zip_verify_device; device=False hands the host image to
+    zcrc_zip_verify_host, which stages it itself.  Either way stored entries
+    are checksummed in one batch, deflated entries are inflated on the GPU
+    and their outputs checksummed in one more; encrypted entries and other
+    methods come back ZIP_UNVERIFIED, broken deflate streams
+    ZIP_INFLATE_ERROR (inflate_status says why).
     """
     a = _as_array(archive)
     l = _setup()
@@ -119,17 +123,4 @@ def verify(archive, device: bool = True, inflate: bool = False) -> List[ZipEntry
               "zcrc_zip_verify_device")
     else:
         check(l.zcrc_zip_verify_host(a.ctypes.data, a.size, arr, len(entries)), "zcrc_zip_verify_host")
-    out = [_to_check(a, e) for e in arr[: len(entries)]]
-    if inflate:
-        from .crc32 import crc32_batch
-        todo = [i for i, c in enumerate(out) if c.status == ZIP_UNVERIFIED and c.method == 8
-                and not (arr[i].flags & 1)]
-        if todo:
-            raw = [_inflate_only.decompressobj(-15).decompress(
-                a[out[i].data_offset: out[i].data_offset + out[i].comp_size].tobytes()) for i in todo]
-            crcs = crc32_batch(raw)
-            for i, data, c in zip(todo, raw, crcs):
-                ok = int(c) == out[i].crc_expected and len(data) == out[i].uncomp_size
-                out[i].crc_computed = int(c)
-                out[i].status = ZIP_OK if ok else ZIP_MISMATCH
-    return out
+    return [_to_check(a, e) for e in arr[: len(entries)]]
