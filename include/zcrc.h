@@ -100,6 +100,13 @@ int zcrc32_batch_device_strided(const void *d_base, uint64_t stride, uint64_t le
 int zcrc_inflate_batch_device(const void *const *d_src, const uint64_t *d_src_len, void *const *d_dst,
                               const uint64_t *d_cap, uint64_t *d_out_len, int32_t *d_status, size_t n,
                               void *stream);
+/* Same for host memory, plus the CRC-32 of every output: the preload of a
+ * deflated entry (raw stream via libzip ZIP_FL_COMPRESSED) inflated and
+ * checksummed in one call.  Streams are packed into pinned staging, inflated
+ * and checksummed on the GPU and copied back; synchronous.  out_len[i] = 0 and
+ * crc_or_null[i] = 0 unless status[i] == ZCRC_INFLATE_OK.  flags: pass 0. */
+int zcrc_inflate_batch(const void *const *src, const size_t *src_len, void *const *dst, const size_t *cap,
+                       size_t *out_len, int32_t *status, uint32_t *crc_or_null, size_t n, unsigned flags);
 
 /* Streaming / incremental CRC.  ZIPsFS fills a preload
  * buffer in <= 16 MiB zip_fread() chunks (src/ZIPsFS_preloadfileram.c:286-306)

@@ -95,3 +95,15 @@ def test_inflate_then_crc_on_device():
     assert (st == 0).all()
     crcs = z.crc32_batch_device(dp, out_lens).cpu().numpy().view(np.uint32)
     assert list(crcs) == [zlib.crc32(d) for _, _, d in items]
+
+
+def test_inflate_host_batch_with_crc():
+    """zcrc_inflate_batch: host streams in, host bytes + CRC-32 out (the
+    deflated-entry preload shape), including an error entry and grouping."""
+    items = [it for it in S.corpus() if it[0].startswith(("text", "spectrum"))][:150]
+    streams = [s for _, s, _ in items] + [b"\x07", b""]
+    caps = [len(d) for _, _, d in items] + [10, 0]
+    res = z.inflate_batch(streams, caps)
+    for (name, _, data), (st, out, crc) in zip(items, res):
+        assert st == 0 and out == data and crc == zlib.crc32(data), name
+    assert res[-2][0] == 1 and res[-1][0] == 7

@@ -27,7 +27,7 @@ __all__ = [
     "ZcrcError", "Crc32Stream", "cg_crc32", "crc32_batch", "crc32_batch_device", "crc32_batch_device_ws",
     "crc32_batch_strided", "crc32_tensors", "crc32_combine", "fhandle_check_crc32",
     "verify_entries", "fill_synthetic", "profile", "device_info", "version",
-    "inflate_batch_device", "inflate_to_device", "INFLATE_STATUS",
+    "inflate_batch_device", "inflate_to_device", "inflate_batch", "INFLATE_STATUS",
 ]
 
 
@@ -268,6 +268,28 @@ def inflate_batch_device(src_ptrs, src_lens, dst_ptrs, caps, out_lens=None, stat
                                           caps.data_ptr(), out_lens.data_ptr(), status.data_ptr(), n,
                                           _stream_ptr(stream)), "zcrc_inflate_batch_device")
     return out_lens, status
+
+
+def inflate_batch(streams: Sequence, caps: Sequence[int]):
+    """Host streams -> [(status, bytes, crc32)] (zcrc_inflate_batch): raw
+    DEFLATE inflated and CRC-checked on the GPU, outputs copied back."""
+    views = [_host_view(x) for x in streams]
+    n = len(views)
+    caps = [int(c) for c in caps]
+    if len(caps) != n:
+        raise ValueError("caps length mismatch")
+    outs = [bytearray(max(c, 1)) for c in caps]
+    obufs = [(ctypes.c_char * len(b)).from_buffer(b) for b in outs]
+    sp = (ctypes.c_void_p * max(n, 1))(*[v[1] for v in views])
+    sl = (ctypes.c_size_t * max(n, 1))(*[v[2] for v in views])
+    dp = (ctypes.c_void_p * max(n, 1))(*[ctypes.addressof(b) for b in obufs])
+    cp = (ctypes.c_size_t * max(n, 1))(*caps)
+    ol = (ctypes.c_size_t * max(n, 1))()
+    st = (ctypes.c_int32 * max(n, 1))()
+    cr = (ctypes.c_uint32 * max(n, 1))()
+    check(lib().zcrc_inflate_batch(sp, sl, dp, cp, ol, st, cr, n, 0), "zcrc_inflate_batch")
+    del views, obufs
+    return [(int(st[i]), bytes(outs[i][:ol[i]]), int(cr[i])) for i in range(n)]
 
 
 def inflate_to_device(streams: Sequence, caps: Sequence[int], device="cuda", stream=None):

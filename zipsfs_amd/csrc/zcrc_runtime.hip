@@ -632,6 +632,131 @@ int zcrc_inflate_batch_device(const void *const *d_src, const uint64_t *d_src_le
   return ZCRC_OK;
 }
 
+namespace zcrc {
+namespace {
+
+// Host-memory inflate: per-thread pinned staging, grown on demand.
+struct InflateStage {
+  uint8_t *h_in = nullptr, *h_out = nullptr;
+  size_t cap_in = 0, cap_out = 0;
+  ~InflateStage() {
+    if (h_in) (void)hipHostFree(h_in);
+    if (h_out) (void)hipHostFree(h_out);
+  }
+  int reserve(size_t in, size_t out) {
+    if (in > cap_in) {
+      if (h_in) (void)hipHostFree(h_in);
+      h_in = nullptr;
+      cap_in = 0;
+      ZCRC_HIP_TRY(hipHostMalloc(reinterpret_cast<void **>(&h_in), in, hipHostMallocDefault));
+      cap_in = in;
+    }
+    if (out > cap_out) {
+      if (h_out) (void)hipHostFree(h_out);
+      h_out = nullptr;
+      cap_out = 0;
+      ZCRC_HIP_TRY(hipHostMalloc(reinterpret_cast<void **>(&h_out), out, hipHostMallocDefault));
+      cap_out = out;
+    }
+    return ZCRC_OK;
+  }
+};
+thread_local InflateStage t_inflate;
+constexpr size_t kInflateGroupBytes = 1ull << 30;  // in + out bytes staged per group
+
+// streams [a, b): pack, one H2D, inflate, CRC, one D2H, unpack
+int inflate_host_group(const void *const *src, const size_t *src_len, void *const *dst, const size_t *cap,
+                       size_t *out_len, int32_t *status, uint32_t *crc, size_t a, size_t b, hipStream_t st) {
+  const size_t m = b - a;
+  size_t in = 0, out = 0;
+  for (size_t i = a; i < b; i++) in += src_len[i], out += cap[i];
+  int rc = t_inflate.reserve(in + 16, out + 16);
+  if (rc) return rc;
+  std::vector<uint64_t> h(4 * m);
+  size_t pi = 0, po = 0;
+  for (size_t j = 0; j < m; j++) {
+    const size_t i = a + j;
+    if (src_len[i]) memcpy(t_inflate.h_in + pi, src[i], src_len[i]);
+    h[j] = pi;
+    h[m + j] = src_len[i];
+    h[2 * m + j] = po;
+    h[3 * m + j] = cap[i];
+    pi += src_len[i];
+    po += cap[i];
+  }
+  void *d_in = nullptr, *d_out = nullptr, *d_desc = nullptr;
+  ZCRC_HIP_TRY(hipMallocAsync(&d_in, in + 16, st));
+  ZCRC_HIP_TRY(hipMallocAsync(&d_out, out + 16, st));
+  ZCRC_HIP_TRY(hipMallocAsync(&d_desc, 8 * 5 * m + 8 * m, st));
+  for (size_t j = 0; j < m; j++) {
+    h[j] += reinterpret_cast<uint64_t>(d_in);
+    h[2 * m + j] += reinterpret_cast<uint64_t>(d_out);
+  }
+  uint64_t *dd = static_cast<uint64_t *>(d_desc);
+  int32_t *d_status = reinterpret_cast<int32_t *>(dd + 5 * m);
+  uint32_t *d_crc = reinterpret_cast<uint32_t *>(d_status + m);
+  std::vector<uint64_t> olen(m);
+  std::vector<int32_t> stv(m);
+  std::vector<uint32_t> crcv(m);
+  ZCRC_HIP_TRY(hipMemcpyAsync(d_in, t_inflate.h_in, in, hipMemcpyHostToDevice, st));
+  ZCRC_HIP_TRY(hipMemcpyAsync(dd, h.data(), 8 * 4 * m, hipMemcpyHostToDevice, st));
+  rc = zcrc_inflate_batch_device(reinterpret_cast<const void *const *>(dd), dd + m,
+                                 reinterpret_cast<void *const *>(dd + 2 * m), dd + 3 * m, dd + 4 * m, d_status, m, st);
+  if (!rc)
+    rc = zcrc32_batch_device(reinterpret_cast<const void *const *>(dd + 2 * m), dd + 4 * m, nullptr, d_crc, m, st);
+  if (!rc) {
+    ZCRC_HIP_TRY(hipMemcpyAsync(t_inflate.h_out, d_out, out, hipMemcpyDeviceToHost, st));
+    ZCRC_HIP_TRY(hipMemcpyAsync(olen.data(), dd + 4 * m, 8 * m, hipMemcpyDeviceToHost, st));
+    ZCRC_HIP_TRY(hipMemcpyAsync(stv.data(), d_status, 4 * m, hipMemcpyDeviceToHost, st));
+    ZCRC_HIP_TRY(hipMemcpyAsync(crcv.data(), d_crc, 4 * m, hipMemcpyDeviceToHost, st));
+  }
+  (void)hipFreeAsync(d_desc, st);
+  (void)hipFreeAsync(d_out, st);
+  (void)hipFreeAsync(d_in, st);
+  ZCRC_HIP_TRY(hipStreamSynchronize(st));
+  if (rc) return rc;
+  po = 0;
+  for (size_t j = 0; j < m; j++) {
+    const size_t i = a + j;
+    const bool ok = stv[j] == ZCRC_INFLATE_OK;
+    if (ok && olen[j]) memcpy(dst[i], t_inflate.h_out + po, olen[j]);
+    po += cap[i];
+    status[i] = stv[j];
+    out_len[i] = ok ? olen[j] : 0;
+    if (crc) crc[i] = ok ? crcv[j] : 0u;
+  }
+  return ZCRC_OK;
+}
+
+}  // namespace
+}  // namespace zcrc
+
+int zcrc_inflate_batch(const void *const *src, const size_t *src_len, void *const *dst, const size_t *cap,
+                       size_t *out_len, int32_t *status, uint32_t *crc_or_null, size_t n, unsigned flags) {
+  (void)flags;
+  if (n == 0) return ZCRC_OK;
+  if (!src || !src_len || !dst || !cap || !out_len || !status) return fail(ZCRC_ERR_ARG, "null argument");
+  for (size_t i = 0; i < n; i++) {
+    if ((src_len[i] && !src[i]) || (cap[i] && !dst[i])) return fail(ZCRC_ERR_ARG, "null buffer pointer");
+    if (src_len[i] >= kInflateMaxSrc) return fail(ZCRC_ERR_TOO_BIG, "compressed stream of 3.75 GiB or more");
+  }
+  DeviceCtx *dc = nullptr;
+  int rc = device_ctx(&dc);
+  if (rc) return rc;
+  rc = host_ctx_init();
+  if (rc) return rc;
+  StageSlot &slot = t_host.slot[0];
+  ZCRC_HIP_TRY(hipStreamSynchronize(slot.stream));
+  for (size_t a = 0; a < n;) {
+    size_t b = a, bytes = 0;
+    while (b < n && (b == a || bytes + src_len[b] + cap[b] <= kInflateGroupBytes)) bytes += src_len[b] + cap[b], b++;
+    rc = inflate_host_group(src, src_len, dst, cap, out_len, status, crc_or_null, a, b, slot.stream);
+    if (rc) return rc;
+    a = b;
+  }
+  return ZCRC_OK;
+}
+
 zcrc32_stream *zcrc32_stream_open(uint32_t seed) {
   zcrc32_stream *s = new (std::nothrow) zcrc32_stream();
   if (!s) {
