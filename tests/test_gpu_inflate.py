@@ -65,9 +65,13 @@ def test_inflate_errors_iff_zlib_errors():
             caps.append(300 * len(bad) + 1024)
             exp.append((name, ok, ref))
     st, ol, outs, *_ = _run(streams, caps)
+    want = [o.inflate(b, c)[0] for b, c in zip(streams, caps)]
     n_err = 0
     for k, (name, ok, ref) in enumerate(exp):
         assert (st[k] == 0) == ok, (name, z.INFLATE_STATUS[int(st[k])], ok)
+        # not just "an error": the oracle's status code (input exhaustion
+        # wins over what zero bits past the end would have decoded to)
+        assert st[k] == want[k], (name, z.INFLATE_STATUS[int(st[k])], z.INFLATE_STATUS[want[k]])
         if ok:
             assert outs[k] == ref, name
         else:

@@ -30,6 +30,12 @@
 #include "../../include/zcrc.h"
 #include "zcrc_internal.h"
 
+#ifdef ZCRC_INFLATE_TRACE
+#define ITRACE(...) do { if (threadIdx.x == 0 && blockIdx.x < 4) printf(__VA_ARGS__); } while (0)
+#else
+#define ITRACE(...) do { } while (0)
+#endif
+
 namespace zcrc {
 namespace {
 
@@ -166,6 +172,7 @@ __device__ bool build_code(Lds &s, const uint8_t *lens, uint32_t n, uint32_t roo
 struct Reader {
   __amdgpu_buffer_rsrc_t rsrc;
   uint32_t lead;     // src - (src & ~15)
+  uint32_t end;      // lead + src_len: bytes at or past it read as zero
   uint64_t src_len;
   uint4 A, B;        // blocks kA, kA+1 (1 KiB each; lane holds 16 B)
   uint32_t kA;
@@ -203,7 +210,8 @@ struct Reader {
     }
     const uint32_t g = P >> 2;
     const uint32_t lo = dword_at(g), hi = dword_at(g + 1);
-    const uint32_t w = __builtin_amdgcn_alignbyte(hi, lo, P & 3u);
+    uint32_t w = __builtin_amdgcn_alignbyte(hi, lo, P & 3u);
+    if (P + 4u > end) w &= P >= end ? 0u : (1u << (8u * (end - P))) - 1u;
     bb |= (uint64_t)w << nb;
     nb += 32;
     P += 4;
@@ -239,6 +247,15 @@ __device__ uint32_t decode_slow(Reader &r, const uint16_t *cnt, const uint16_t *
   return mk(0, K_BAD, 0, 0);
 }
 
+// A symbol the code cannot accept.  The canonical decoder (the oracle)
+// reads the whole code first -- its length, or all 15 bits when no code
+// matches -- so those bits count as consumed: past the end of the input the
+// kernel's epilogue then reports ZCRC_INFLATE_ERR_INPUT, as the oracle does.
+__device__ __forceinline__ int32_t bad_symbol(Reader &r, uint32_t e, int32_t err) {
+  r.drop(e_len(e) ? e_len(e) : 15u);
+  return err;
+}
+
 struct Out {
   uint8_t *dst;
   uint64_t cap;
@@ -266,6 +283,8 @@ __device__ int32_t codes(Lds &s, Reader &r, Out &o) {
     if (r.overrun()) return ZCRC_INFLATE_ERR_INPUT;
     r.refill();
     uint32_t e = u32u(s.ll[r.peek(kLLRoot)]);
+    ITRACE("[%u] sym P=%u nb=%u bb=%llx e=%x kind=%u len=%u val=%u pos=%llu\n", blockIdx.x, r.P, r.nb,
+           (unsigned long long)r.bb, e, e_kind(e), e_len(e), e_val(e), (unsigned long long)o.pos);
     if (e_kind(e) == K_LONG) e = u32u(decode_slow(r, s.llcnt, s.llsym, A_LITLEN));
     const uint32_t kind = e_kind(e);
     if (kind == K_LIT) {
@@ -280,14 +299,14 @@ __device__ int32_t codes(Lds &s, Reader &r, Out &o) {
       r.drop(e_len(e));
       return ZCRC_INFLATE_OK;
     }
-    if (kind != K_BASE || e_len(e) == 0) return ZCRC_INFLATE_ERR_SYMBOL;
+    if (kind != K_BASE || e_len(e) == 0) return bad_symbol(r, e, ZCRC_INFLATE_ERR_SYMBOL);
     r.drop(e_len(e));
     const uint32_t len = e_val(e) + r.peek(e_extra(e));
     r.drop(e_extra(e));
     r.refill();
     uint32_t d = u32u(s.dd[r.peek(kDRoot)]);
     if (e_kind(d) == K_LONG) d = u32u(decode_slow(r, s.ddcnt, s.ddsym, A_DIST));
-    if (e_kind(d) != K_BASE || e_len(d) == 0) return ZCRC_INFLATE_ERR_SYMBOL;
+    if (e_kind(d) != K_BASE || e_len(d) == 0) return bad_symbol(r, d, ZCRC_INFLATE_ERR_SYMBOL);
     r.drop(e_len(d));
     const uint32_t dist = e_val(d) + r.peek(e_extra(d));
     r.drop(e_extra(d));
@@ -359,7 +378,7 @@ __device__ int32_t dynamic_tables(Lds &s, Reader &r) {
     if (r.overrun()) return ZCRC_INFLATE_ERR_INPUT;
     r.refill();
     const uint32_t e = u32u(s.dd[r.peek(kCLRoot)]);
-    if (e_kind(e) != K_LIT || e_len(e) == 0) return ZCRC_INFLATE_ERR_CODES;
+    if (e_kind(e) != K_LIT || e_len(e) == 0) return bad_symbol(r, e, ZCRC_INFLATE_ERR_CODES);
     r.drop(e_len(e));
     const uint32_t sym = e_val(e);
     uint32_t val, rep;
@@ -427,17 +446,26 @@ __global__ __launch_bounds__(64) void inflate_kernel(InflateArgs a) {
     const uint64_t base = reinterpret_cast<uint64_t>(src) & ~(uint64_t)15;
     r.lead = (uint32_t)(reinterpret_cast<uint64_t>(src) - base);
     r.src_len = src_len;
+    r.end = r.lead + (uint32_t)src_len;
+    // The buffer unit range-checks whole dwords (a dword that straddles
+    // num_records reads as 0), so the range is rounded up to the 16-byte
+    // granule holding the last byte -- same page, never a fault -- and the
+    // bytes past `end` are masked in refill().
     r.rsrc = __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void *>(base), (short)0,
-                                               (int)(uint32_t)(r.lead + src_len), 0x00020000);
+                                               (int)((r.end + 15u) & ~15u), 0x00020000);
     r.seek(r.lead);
+    ITRACE("[%u] seek lead=%u A0=%x d0=%x d1=%x\n", blockIdx.x, r.lead, r.A.x, r.dword_at(0), r.dword_at(1));
     uint32_t last = 0;
     do {
       if (r.overrun()) {
         st = ZCRC_INFLATE_ERR_INPUT;
         break;
       }
+      ITRACE("[%u] hdr P=%u nb=%u bb=%llx lead=%u srclen=%llu\n", blockIdx.x, r.P, r.nb,
+             (unsigned long long)r.bb, r.lead, (unsigned long long)r.src_len);
       last = r.bits(1);
       const uint32_t type = r.bits(2);
+      ITRACE("[%u]   last=%u type=%u\n", blockIdx.x, last, type);
       if (type == 0) {
         st = stored(s, r, o);
       } else if (type == 1) {
@@ -450,7 +478,10 @@ __global__ __launch_bounds__(64) void inflate_kernel(InflateArgs a) {
         st = ZCRC_INFLATE_ERR_BLOCK_TYPE;
       }
     } while (!last && st == ZCRC_INFLATE_OK);
-    if (st == ZCRC_INFLATE_OK && r.consumed() > src_len) st = ZCRC_INFLATE_ERR_INPUT;
+    // Bits past the end read as zero.  Whenever the decode used any of them
+    // -- whether it then ended cleanly or failed on what they said -- the
+    // canonical decoder would have stopped at the first one: input error.
+    if (r.consumed() > src_len) st = ZCRC_INFLATE_ERR_INPUT;
   }
   if (st == ZCRC_INFLATE_OK) flush(s, o, o.pos);
   if (threadIdx.x == 0) {
