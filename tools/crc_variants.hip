@@ -123,12 +123,12 @@ int main(int argc, char **argv) {
     uint32_t dyn;
     uint64_t unit;
   } vs[] = {
+      {"static-dflt", crc32_batch_kernel<false, 4, 0, true, false, 0, 0>, true, 0, 0},
+      {"product-dflt", crc32_batch_kernel<false, 4, 0, true, false, 1, 0>, true, kDynShift, kDynUnit},
       {"static", crc32_batch_kernel<false, 4, 0, true, false, 0>, true, 0, 0},
       {"prio", crc32_batch_kernel<false, 4, 0, true, false, 1>, true, 0, 0},
       {"product", crc32_batch_kernel<false, 4, 0, true, false, 1>, true, kDynShift, kDynUnit},
-      {"p+d1u128", crc32_batch_kernel<false, 4, 0, true, false, 1>, true, 1, 128 << 10},
-      {"p+d2u128", crc32_batch_kernel<false, 4, 0, true, false, 1>, true, 2, 128 << 10},
-      {"p+d3u128", crc32_batch_kernel<false, 4, 0, true, false, 1>, true, 3, 128 << 10},
+      {"product+sc1nt", crc32_batch_kernel<false, 4, 0, true, false, 1, 18>, true, kDynShift, kDynUnit},
   };
   uint32_t *d_counter;
   CHECK(hipMalloc(&d_counter, 32));
@@ -208,8 +208,10 @@ int main(int argc, char **argv) {
     a.stamps = nullptr;
     CHECK(hipFree(dst));
   };
-  stamp_run("static", crc32_batch_kernel<false, 4, 0, true, true, 0>, 0, 0);
-  stamp_run("product", crc32_batch_kernel<false, 4, 0, true, true, 1>, kDynShift, kDynUnit);
+  if (getenv("CRC_VARIANTS_STAMPS")) {
+    stamp_run("static", crc32_batch_kernel<false, 4, 0, true, true, 0>, 0, 0);
+    stamp_run("product", crc32_batch_kernel<false, 4, 0, true, true, 1>, kDynShift, kDynUnit);
+  }
   for (int round = 0; round < 2; round++) {
     for (uint64_t mr : ranges)
     for (auto &v : vs) {

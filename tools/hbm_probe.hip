@@ -187,6 +187,44 @@ __global__ void read_chunk_sweep(const uint4 *p, uint64_t n16, uint32_t *out) {
   out[(uint64_t)blockIdx.x * blockDim.x + threadIdx.x] = acc.x ^ acc.y ^ acc.z ^ acc.w;
 }
 
+// the same two shapes with non-temporal (nt) loads
+typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ uint4 ntload(const uint4 *a) {
+  const v4u v = __builtin_nontemporal_load(reinterpret_cast<const v4u *>(a));
+  return make_uint4(v[0], v[1], v[2], v[3]);
+}
+
+template <int D>
+__global__ void read_grid_nt(const uint4 *p, uint64_t n16, uint32_t *out) {
+  uint4 acc = make_uint4(0, 0, 0, 0);
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x * D;
+  for (uint64_t base = (uint64_t)blockIdx.x * blockDim.x * D; base + (uint64_t)blockDim.x * D <= n16;
+       base += stride) {
+    uint4 v[D];
+#pragma unroll
+    for (int u = 0; u < D; u++) v[u] = ntload(&p[base + (uint64_t)u * blockDim.x + threadIdx.x]);
+    consume<D>(v, acc);
+  }
+  out[(uint64_t)blockIdx.x * blockDim.x + threadIdx.x] = acc.x ^ acc.y ^ acc.z ^ acc.w;
+}
+
+template <int D>
+__global__ void read_wave_nt(const uint4 *p, uint64_t n16, uint32_t *out) {
+  uint4 acc = make_uint4(0, 0, 0, 0);
+  const uint64_t waves = (uint64_t)gridDim.x * (blockDim.x / 64);
+  const uint64_t w = (uint64_t)blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64;
+  const uint64_t per = n16 / waves;
+  const uint32_t lane = threadIdx.x & 63;
+  const uint4 *q = p + w * per;
+  for (uint64_t base = 0; base + 64 * D <= per; base += 64 * D) {
+    uint4 v[D];
+#pragma unroll
+    for (int u = 0; u < D; u++) v[u] = ntload(&q[base + u * 64 + lane]);
+    consume<D>(v, acc);
+  }
+  out[(uint64_t)blockIdx.x * blockDim.x + threadIdx.x] = acc.x ^ acc.y ^ acc.z ^ acc.w;
+}
+
 typedef void (*kfn)(const uint4 *, uint64_t, uint32_t *);
 
 static double run(const char *name, kfn k, int grid, int block, const uint4 *p, uint64_t n16, uint32_t *out, int reps,
@@ -231,6 +269,11 @@ int main(int argc, char **argv) {
   for (int round = 0; round < 2; round++) {
     printf("-- round %d\n", round);
     run("grid-stride D=4 (1024 thr, 1/CU)", read_grid<4>, cus, 1024, p, n16, out, reps, bytes);
+    run("grid-stride D=4 nt", read_grid_nt<4>, cus, 1024, p, n16, out, reps, bytes);
+    run("grid-stride D=8 nt", read_grid_nt<8>, cus, 1024, p, n16, out, reps, bytes);
+    run("wave-contig D=4", read_wave<4>, cus, 1024, p, n16, out, reps, bytes);
+    run("wave-contig D=4 nt", read_wave_nt<4>, cus, 1024, p, n16, out, reps, bytes);
+    if (getenv("PROBE_ALL") == nullptr) continue;
     run("wg-rot 64K D=4", read_wg_rot<4, 64>, cus, 1024, p, n16, out, reps, bytes);
     run("wg-rot 1M D=4", read_wg_rot<4, 1024>, cus, 1024, p, n16, out, reps, bytes);
     run("wg-rot 4M D=4", read_wg_rot<4, 4096>, cus, 1024, p, n16, out, reps, bytes);
