@@ -35,7 +35,13 @@ def main():
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--cpu-budget-s", type=float, default=10.0)
+    ap.add_argument("--kind", default="mixed", choices=["mixed", "text", "spectrum"])
+    ap.add_argument("--lib", default=None, help="alternate libzcrc build (measurement variants)")
+    ap.add_argument("--no-cpu", action="store_true")
     args = ap.parse_args()
+    if args.lib:
+        import zipsfs_amd._lib as L
+        L.LIB_PATH = os.path.abspath(args.lib)
 
     import torch
     import zlib
@@ -46,7 +52,10 @@ def main():
     dev = "cuda:0"
     raw, comp = [], []
     for u in range(args.unique):
-        gen = S.text_payload if u % 2 == 0 else S.spectrum_payload
+        if args.kind == "mixed":
+            gen = S.text_payload if u % 2 == 0 else S.spectrum_payload
+        else:
+            gen = S.text_payload if args.kind == "text" else S.spectrum_payload
         data = gen(args.size, 7000 + u)
         raw.append(data)
         comp.append(S.deflate(data, args.level))
@@ -81,13 +90,14 @@ def main():
     run(True)
     torch.cuda.synchronize()
     assert int((st != 0).sum()) == 0, "inflate failed"
+    check = args.lib is None  # ablation builds produce wrong bytes by design
     crcs = run(True).cpu().numpy().view(np.uint32)
     want = [zlib.crc32(raw[p]) for p in pick[: args.unique]]
-    assert list(crcs[: args.unique]) == want, "parity"
+    assert not check or list(crcs[: args.unique]) == want, "parity"
     host_out = arena[: min(out_bytes, 64 << 20)].cpu().numpy()
     for k in range(min(args.unique, 8)):
         a = int(dst_off[k])
-        if a + caps[k] <= host_out.size:
+        if check and a + caps[k] <= host_out.size:
             assert host_out[a:a + caps[k]].tobytes() == raw[pick[k]]
 
     res = {}
@@ -104,6 +114,9 @@ def main():
         res[key] = {"ms": round(ms, 3), "out_GBs": round(out_bytes / ms / 1e6, 2),
                     "in_GBs": round(in_bytes / ms / 1e6, 2)}
 
+    if args.no_cpu:
+        print(json.dumps({"kind": args.kind, "lib": args.lib, "gpu": res}), flush=True)
+        return
     # CPU baseline: system zlib (libzip's inflate), bounded sample
     nsamp = max(args.cpu_threads, min(args.entries, 64))
     streams = [comp[pick[k]] for k in range(nsamp)]

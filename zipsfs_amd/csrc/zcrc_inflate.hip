@@ -9,21 +9,26 @@
 // and go straight into the batched CRC kernel without leaving HBM.
 //
 // Design:
-//   * one 64-lane workgroup per stream; DEFLATE is serial within a stream,
-//     so the batch is the parallelism.  ~38 KiB LDS per workgroup -> four
-//     streams resident per CU, more waiting in the dispatcher, which also
-//     balances ragged stream sizes for free;
-//   * LDS holds the 32 KiB window as a ring (every back-reference is an LDS
-//     read), a 2^10-entry literal/length LUT and a 2^8-entry distance LUT,
-//     plus canonical count/symbol arrays for codes longer than the LUT root;
-//   * input: 2 KiB staged in VGPRs (16 B per lane, coalesced 1 KiB loads one
-//     block ahead); the wave-uniform bit reader gathers dwords with
-//     v_readlane, so decode state lives in SGPRs;
-//   * table builds are wave-parallel (ballot counts, ballot-ranked canonical
-//     symbol order, every LUT index decoded canonically by its own lane);
-//   * matches copy lane-parallel through the ring (i mod dist for
-//     overlapping short distances); output leaves the ring in 512-byte
-//     lane-parallel flushes.
+//   * one 64-lane workgroup per stream: DEFLATE is serial within a stream,
+//     so the batch is the parallelism.  All decode state is wave-uniform and
+//     lives in SGPRs; a single wave per SIMD issues one instruction every
+//     ~4 cycles, so the figure of merit is instructions per symbol;
+//   * Huffman lookup tables live in VGPRs, not LDS: entry idx of a 2^R table
+//     sits in lane idx & 63 of register idx >> 6, so a lookup is
+//     s_set_gpr_idx (dynamic register) + v_readlane -- no LDS round trip on
+//     the symbol chain.  Literal/length root 10 (16 VGPRs), distance root 8
+//     (4 VGPRs), code-length root 7 (2 VGPRs); longer codes take a canonical
+//     slow path with per-length (first, count, offset) kept in LDS;
+//   * LDS (~34 KiB, four streams per CU) holds the 32 KiB window as a ring
+//     (back-references are lane-parallel LDS copies) and the canonical symbol
+//     order the table builds need;
+//   * input: three 1 KiB blocks staged in VGPRs (16 B per lane, coalesced
+//     buffer loads issued one block ahead of use); the bit reader gathers
+//     dwords with v_readlane;
+//   * output leaves the ring in 8 KiB batches of 16-B stores, lagging the
+//     decode (a byte is overwritten only 32 KiB later);
+//   * table builds are wave-parallel: ballot counts, ballot-ranked
+//     canonical order, every lane decodes its own LUT indices.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -41,7 +46,23 @@ namespace {
 
 constexpr uint32_t kWin = 32768, kWinMask = kWin - 1;
 constexpr uint32_t kLLRoot = 10, kDRoot = 8, kCLRoot = 7;
-constexpr uint32_t kFlush = 512;
+constexpr uint32_t kLLRegs = (1u << kLLRoot) / 64, kDRegs = (1u << kDRoot) / 64, kCLRegs = (1u << kCLRoot) / 64;
+constexpr uint32_t kFlushLag = 8192;  // bytes decoded ahead of the last flush
+
+// Register-resident tables are LLVM vectors: a dynamic subscript lowers to
+// s_set_gpr_idx + v_mov (no scratch), where a local array would be demoted
+// to memory.
+typedef uint32_t v2u __attribute__((ext_vector_type(2)));
+typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+typedef uint32_t v8u __attribute__((ext_vector_type(8)));
+typedef uint32_t v16u __attribute__((ext_vector_type(16)));
+template <uint32_t N> struct VecOf;
+template <> struct VecOf<2> { typedef v2u T; };
+template <> struct VecOf<4> { typedef v4u T; };
+template <> struct VecOf<16> { typedef v16u T; };
+typedef VecOf<kLLRegs>::T LLTab;
+typedef VecOf<kDRegs>::T DTab;
+typedef VecOf<kCLRegs>::T CLTab;
 
 // LUT entry: [0:4) code length, [4:7) kind, [7:11) extra bits, [11:27) value
 enum : uint32_t { K_BAD = 0, K_LIT = 1, K_BASE = 2, K_EOB = 3, K_LONG = 4 };
@@ -55,166 +76,227 @@ __device__ __forceinline__ uint32_t e_kind(uint32_t e) { return (e >> 4) & 7u; }
 __device__ __forceinline__ uint32_t e_extra(uint32_t e) { return (e >> 7) & 15u; }
 __device__ __forceinline__ uint32_t e_val(uint32_t e) { return e >> 11; }
 
-__device__ __forceinline__ uint32_t u32u(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane(v); }
+__device__ __forceinline__ uint32_t uni(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); }
+__device__ __forceinline__ uint32_t lane_get(uint32_t v, uint32_t lane) {
+  return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)lane);
+}
 
-// RFC 1951 3.2.5 base/extra tables
-__constant__ uint16_t c_len_base[29] = {3,  4,  5,  6,  7,  8,  9,  10, 11,  13,  15,  17,  19,  23, 27,
-                                        31, 35, 43, 51, 59, 67, 83, 99, 115, 131, 163, 195, 227, 258};
-__constant__ uint8_t c_len_extra[29] = {0, 0, 0, 0, 0, 0, 0, 0, 1, 1, 1, 1, 2, 2, 2,
-                                        2, 3, 3, 3, 3, 4, 4, 4, 4, 5, 5, 5, 5, 0};
-__constant__ uint16_t c_dist_base[30] = {1,    2,    3,    4,    5,    7,    9,    13,    17,    25,
-                                         33,   49,   65,   97,   129,  193,  257,  385,   513,   769,
-                                         1025, 1537, 2049, 3073, 4097, 6145, 8193, 12289, 16385, 24577};
-__constant__ uint8_t c_dist_extra[30] = {0, 0, 0, 0, 1, 1, 2, 2, 3, 3, 4, 4, 5, 5, 6,
-                                         6, 7, 7, 8, 8, 9, 9, 10, 10, 11, 11, 12, 12, 13, 13};
-__constant__ uint8_t c_clen_order[19] = {16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 12, 3, 13, 2, 14, 1, 15};
-
-struct Lds {
-  uint8_t ring[kWin];
-  uint32_t ll[1u << kLLRoot];
-  uint32_t dd[1u << kDRoot];  // distance LUT; the code-length LUT while reading a header
-  uint16_t llcnt[16], ddcnt[16];
-  uint16_t llsym[288], ddsym[32];
-  uint16_t offs[16];
-  uint8_t lens[336];  // clen code lengths [0,19) | litlen+dist lengths [19, 19+316)
-};
-
+// RFC 1951 3.2.5 in closed form: length code k = sym - 257 (k < 28) has
+// base 3 + k and no extra bits below 8, else e = (k - 4) / 4 extra bits and
+// base ((4 + k % 4) << e) + 3; code 285 is 258.  Distance code d has base
+// d + 1 below 4, else e = d / 2 - 1 extra bits and base ((2 + d % 2) << e) + 1.
 __device__ __forceinline__ uint32_t symbol_entry(uint32_t alphabet, uint32_t sym, uint32_t len) {
   if (alphabet == A_LITLEN) {
     if (sym < 256) return mk(len, K_LIT, 0, sym);
     if (sym == 256) return mk(len, K_EOB, 0, 0);
-    if (sym < 286) return mk(len, K_BASE, c_len_extra[sym - 257], c_len_base[sym - 257]);
-    return mk(len, K_BAD, 0, 0);
+    if (sym < 285) {
+      const uint32_t k = sym - 257;
+      if (k < 8) return mk(len, K_BASE, 0, 3 + k);
+      const uint32_t e = (k - 4) >> 2;
+      return mk(len, K_BASE, e, ((4u + (k & 3u)) << e) + 3u);
+    }
+    if (sym == 285) return mk(len, K_BASE, 0, 258);
+    return mk(len, K_BAD, 0, 0);  // 286, 287
   }
-  if (alphabet == A_DIST) return sym < 30 ? mk(len, K_BASE, c_dist_extra[sym], c_dist_base[sym]) : mk(len, K_BAD, 0, 0);
+  if (alphabet == A_DIST) {
+    if (sym < 4) return mk(len, K_BASE, 0, sym + 1);
+    if (sym < 30) {
+      const uint32_t e = (sym >> 1) - 1;
+      return mk(len, K_BASE, e, ((2u + (sym & 1u)) << e) + 1u);
+    }
+    return mk(len, K_BAD, 0, 0);  // 30, 31
+  }
   return mk(len, K_LIT, 0, sym);
 }
 
-// Build the canonical code for lens[0..n) (RFC 1951 3.2.2) into cnt/sym
-// and a 2^root LUT.  Returns false where zlib's inflate_table() rejects the
-// set: over-subscribed, or incomplete unless (not CLEN and a single
-// length-1 code); an all-zero set is accepted (decoding from it fails).
-__device__ bool build_code(Lds &s, const uint8_t *lens, uint32_t n, uint32_t root, uint32_t *lut, uint16_t *cnt,
-                           uint16_t *sym, uint32_t alphabet) {
+__constant__ uint8_t kClenOrder[19] = {16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 12, 3, 13, 2, 14, 1, 15};
+
+// per-length canonical parameters, for codes longer than the LUT root
+struct CodeMeta {
+  uint16_t first[16], cnt[16], offs[16];
+};
+
+// Lanes that have nothing to write store into `ring[kWin + 4 * lane]` (the
+// dummy tail) instead of branching around the store: the hot loop then has
+// no divergent branch, so the compiler keeps it unstructurized -- plain
+// s_cbranch_scc on SGPR state (with a divergent `if` anywhere inside, the
+// whole loop is rewritten into predicate-flag flow: ~90 instructions per
+// literal instead of ~30).
+constexpr uint32_t kDummy = kWin;
+struct Lds {
+  uint8_t ring[kWin + 256];
+  uint16_t llsym[288], ddsym[32], clsym[20];
+  CodeMeta llm, ddm;
+  uint8_t lens[320];  // litlen lengths [0, nlen), distance lengths [nlen, nlen + ndist)
+  uint8_t cllens[20];
+};
+
+// Build the canonical code for lens[0..n) (RFC 1951 3.2.2): the VGPR LUT
+// (entry idx in lane idx & 63 of lut[idx >> 6]), the canonical symbol order
+// sym[], and, when some code is longer than ROOT, the per-length meta in
+// LDS.  Returns false where zlib's inflate_table() rejects the set:
+// over-subscribed, or incomplete unless (not CLEN and a single length-1
+// code); an all-zero set is accepted (decoding from it fails).
+//
+// Per-length quantities live in lane L (count, offset, first code), so the
+// build needs few SGPRs: one uniform pass per length ranks the symbols of
+// that length by ballot, lane scans give offsets and first codes, and the
+// LUT pass walks the lengths with v_readlane.
+template <uint32_t ROOT, uint32_t NREG>
+__device__ bool build_code(const uint8_t *lens, uint32_t n, uint16_t *sym, CodeMeta *meta, uint32_t alphabet,
+                           typename VecOf<NREG>::T &lut) {
   const uint32_t lane = threadIdx.x;
-  // counts per length: ballots over 64-symbol chunks
-  uint32_t count[16];
+  const uint32_t nch = (n + 63) >> 6;  // <= 5
+  const uint64_t lt = (1ull << lane) - 1ull;
+  uint32_t lv[5], rk[5];
 #pragma unroll
-  for (int L = 0; L < 16; L++) count[L] = 0;
-  for (uint32_t c = 0; c < n; c += 64) {
-    const uint32_t sidx = c + lane;
-    const uint32_t l = sidx < n ? lens[sidx] : 0u;
-#pragma unroll
-    for (int L = 1; L < 16; L++) count[L] += (uint32_t)__builtin_popcountll(__ballot(l == (uint32_t)L));
+  for (uint32_t c = 0; c < 5; c++) {
+    const uint32_t s = c * 64 + lane;
+    lv[c] = (c < nch && s < n) ? lens[s] : 0u;
+    rk[c] = 0;
   }
-  int left = 1;
-  uint32_t max_len = 0;
+  // count and rank (by symbol) the codes of each length
+  uint32_t cntv = 0;
+  for (uint32_t L = 1; L < 16; L++) {
+    uint32_t run = 0;
 #pragma unroll
-  for (int L = 1; L < 16; L++) {
-    left = (left << 1) - (int)count[L];
-    if (count[L]) max_len = L;
-    if (left < 0) break;
-  }
-  if (left < 0) return false;
-  if (max_len && left > 0 && (alphabet == A_CLEN || max_len != 1)) return false;
-  if (lane == 0) {
-    uint32_t o = 0;
-    cnt[0] = 0;
-#pragma unroll
-    for (int L = 1; L < 16; L++) {
-      cnt[L] = (uint16_t)count[L];
-      s.offs[L] = (uint16_t)o;
-      o += count[L];
-    }
-  }
-  __syncthreads();
-  // canonical symbol order: by (length, symbol); ranks from ballots
-  for (uint32_t c = 0; c < n; c += 64) {
-    const uint32_t sidx = c + lane;
-    const uint32_t l = sidx < n ? lens[sidx] : 0u;
-    const uint64_t lt = (1ull << lane) - 1ull;
-#pragma unroll
-    for (int L = 1; L < 16; L++) {
-      if (!count[L]) continue;
-      const uint64_t m = __ballot(l == (uint32_t)L);
-      if (!m) continue;
-      const uint32_t base = s.offs[L];
-      if (l == (uint32_t)L) sym[base + (uint32_t)__builtin_popcountll(m & lt)] = (uint16_t)sidx;
-      __syncthreads();
-      if (lane == 0) s.offs[L] = (uint16_t)(base + (uint32_t)__builtin_popcountll(m));
-      __syncthreads();
-    }
-  }
-  __syncthreads();
-  // LUT: lane decodes its own indices canonically (bits LSB-first)
-  const uint32_t size = 1u << root;
-  for (uint32_t idx = lane; idx < size; idx += 64) {
-    int code = 0, first = 0, index = 0;
-    uint32_t e = (max_len > root) ? mk(0, K_LONG, 0, 0) : mk(0, K_BAD, 0, 0);
-    for (uint32_t L = 1; L <= root; L++) {
-      code |= (int)((idx >> (L - 1)) & 1u);
-      const int ct = (int)cnt[L];
-      if (code - ct < first) {
-        e = symbol_entry(alphabet, sym[index + (code - first)], L);
-        break;
+    for (uint32_t c = 0; c < 5; c++) {
+      if (c < nch) {
+        const uint64_t m = __ballot(lv[c] == L);
+        if (lv[c] == L) rk[c] = run + (uint32_t)__builtin_popcountll(m & lt);
+        run += (uint32_t)__builtin_popcountll(m);
       }
-      index += ct;
-      first += ct;
-      first <<= 1;
-      code <<= 1;
     }
-    lut[idx] = e;
+    if (lane == L) cntv = run;
   }
+  // lane scans over lengths 1..15: offs = sum of counts below, and the
+  // Kraft partial sums in units of 2^-15 give the first codes
+  const uint32_t kr = (lane >= 1 && lane < 16) ? cntv << (15 - lane) : 0u;
+  uint32_t offs_inc = cntv, kr_inc = kr;
+#pragma unroll
+  for (uint32_t k = 1; k < 16; k <<= 1) {
+    const uint32_t a = __shfl_up(offs_inc, k, 64), b = __shfl_up(kr_inc, k, 64);
+    if (lane >= k) {
+      offs_inc += a;
+      kr_inc += b;
+    }
+  }
+  const uint32_t offsv = offs_inc - cntv;
+  const uint32_t firstv = (lane < 16) ? (kr_inc - kr) >> (15 - lane) : 0u;
+  const uint32_t kraft = lane_get(kr_inc, 15);  // 2^15 = complete
+  const uint64_t used = __ballot(cntv != 0 && lane < 16);
+  const uint32_t max_len = used ? 63u - (uint32_t)__builtin_clzll(used) : 0u;
+  if (kraft > 32768u) return false;  // over-subscribed
+  if (max_len && kraft < 32768u && (alphabet == A_CLEN || max_len != 1)) return false;
+  if (max_len > ROOT && lane < 16) {
+    meta->first[lane] = (uint16_t)firstv;
+    meta->cnt[lane] = (uint16_t)cntv;
+    meta->offs[lane] = (uint16_t)offsv;
+  }
+#pragma unroll
+  for (uint32_t c = 0; c < 5; c++) {
+    if (c < nch) {
+      const uint32_t o = (uint32_t)__shfl(offsv, lv[c] & 15u, 64);
+      if (lv[c]) sym[o + rk[c]] = (uint16_t)(c * 64 + lane);
+    }
+  }
+  __syncthreads();
+  // LUT: lane decodes its own indices canonically
+  uint32_t hitL[NREG], hidx[NREG];
+#pragma unroll
+  for (uint32_t r = 0; r < NREG; r++) hitL[r] = hidx[r] = 0;
+  const uint32_t top = max_len < ROOT ? max_len : ROOT;
+  for (uint32_t L = 1; L <= top; L++) {
+    const uint32_t cL = lane_get(cntv, L);
+    if (!cL) continue;
+    const uint32_t fL = lane_get(firstv, L), oL = lane_get(offsv, L);
+#pragma unroll
+    for (uint32_t r = 0; r < NREG; r++) {
+      const uint32_t d = (__builtin_bitreverse32(lane + 64u * r) >> (32 - L)) - fL;
+      if (d < cL) {
+        hitL[r] = L;
+        hidx[r] = oL + d;
+      }
+    }
+  }
+  const uint32_t miss = (max_len > ROOT) ? mk(0, K_LONG, 0, 0) : mk(0, K_BAD, 0, 0);
+#pragma unroll
+  for (uint32_t r = 0; r < NREG; r++) lut[r] = hitL[r] ? symbol_entry(alphabet, sym[hidx[r]], hitL[r]) : miss;
   __syncthreads();
   return true;
 }
 
+// code longer than the LUT root (rare): canonical decode of the low 15 bits
+__device__ __noinline__ uint32_t decode_slow(uint32_t bits15, const CodeMeta *m, const uint16_t *sym, uint32_t root,
+                                             uint32_t alphabet) {
+  const uint32_t rev = __builtin_bitreverse32(bits15) >> 17;
+  for (uint32_t L = root + 1; L <= 15; L++) {
+    const uint32_t d = (rev >> (15 - L)) - uni(m->first[L]);
+    if (d < uni(m->cnt[L])) return uni(symbol_entry(alphabet, uni(sym[uni(m->offs[L]) + d]), L));
+  }
+  return mk(0, K_BAD, 0, 0);
+}
+
+// Wave-uniform bit reader.  Input is staged in VGPRs as a 4-slot ring of
+// 1 KiB blocks (block b in registers 4(b & 3) .. 4(b & 3) + 3; lane l holds
+// the 16 B at b * 1024 + 16 l), so dword g is register ((g >> 6) & 12) |
+// (g & 3) of lane (g >> 2) & 63: one s_set_gpr_idx move and a v_readlane.
+// Blocks kA and kA + 1 are resident, kA + 2 is in flight in `pend` and lands
+// in its slot at the next slide, by which time its load has returned.
 struct Reader {
   __amdgpu_buffer_rsrc_t rsrc;
-  uint32_t lead;     // src - (src & ~15)
-  uint32_t end;      // lead + src_len: bytes at or past it read as zero
-  uint64_t src_len;
-  uint4 A, B;        // blocks kA, kA+1 (1 KiB each; lane holds 16 B)
+  uint32_t lead;   // src - (src & ~15)
+  uint32_t end;    // lead + src_len: bytes at or past it read as zero
+  uint32_t limit;  // overrun guard
+  v16u st;
+  uint4 pend;
   uint32_t kA;
-  uint32_t P;        // next byte (relative to the aligned base) to enter bb
-  uint64_t bb;       // bit buffer, LSB first
-  uint32_t nb;       // valid bits in bb
+  uint32_t P;   // next byte (relative to the aligned base) to enter bb
+  uint64_t bb;  // bit buffer, LSB first
+  uint32_t nb;  // valid bits in bb
 
   __device__ uint4 load_block(uint32_t k) const {
-    const uint32_t off = k * 1024u + 16u * threadIdx.x;
-    auto v = __builtin_amdgcn_raw_buffer_load_b128(rsrc, off, 0, 0);
+    auto v = __builtin_amdgcn_raw_buffer_load_b128(rsrc, k * 1024u + 16u * threadIdx.x, 0, 0);
     return make_uint4(v[0], v[1], v[2], v[3]);
+  }
+  __device__ void put_slot(uint32_t slot, uint4 v) {
+    switch (slot & 3u) {
+      case 0: st.s0 = v.x; st.s1 = v.y; st.s2 = v.z; st.s3 = v.w; break;
+      case 1: st.s4 = v.x; st.s5 = v.y; st.s6 = v.z; st.s7 = v.w; break;
+      case 2: st.s8 = v.x; st.s9 = v.y; st.sa = v.z; st.sb = v.w; break;
+      default: st.sc = v.x; st.sd = v.y; st.se = v.z; st.sf = v.w; break;
+    }
   }
   __device__ void seek(uint32_t p) {
     P = p;
     bb = 0;
     nb = 0;
     kA = p >> 10;
-    A = load_block(kA);
-    B = load_block(kA + 1);
+    put_slot(kA, load_block(kA));
+    put_slot(kA + 1, load_block(kA + 1));
+    pend = load_block(kA + 2);
   }
-  __device__ uint32_t dword_at(uint32_t g) const {
-    const bool inA = (g >> 8) == kA;
-    const uint32_t c = g & 3u;
-    const uint32_t x = inA ? A.x : B.x, y = inA ? A.y : B.y, z = inA ? A.z : B.z, w = inA ? A.w : B.w;
-    const uint32_t v = c == 0 ? x : c == 1 ? y : c == 2 ? z : w;
-    return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)((g >> 2) & 63u));
-  }
-  // top up to >= 32 valid bits
-  __device__ void refill() {
-    if (nb > 32) return;
-    while (P >= (kA + 1) * 1024u) {  // slide the staging window
-      A = B;
+  __device__ uint32_t dword_at(uint32_t g) const { return lane_get(st[((g >> 6) & 12u) | (g & 3u)], (g >> 2) & 63u); }
+  // Top up to 56..63 valid bits (enough for a whole length/distance pair,
+  // at most 48 bits, so the symbol loop refills once per symbol at most):
+  // the 8 bytes at P are or-ed in above the valid bits and P advances by the
+  // whole bytes that fit.  Bytes at or past `end` read as zero.  False once
+  // the input is overrun.
+  __device__ bool refill() {
+    if (P >= (kA + 1) * 1024u) {  // slide: land kA + 2, prefetch kA + 3
+      put_slot(kA + 2, pend);
       kA++;
-      B = load_block(kA + 1);
+      pend = load_block(kA + 2);
     }
-    const uint32_t g = P >> 2;
-    const uint32_t lo = dword_at(g), hi = dword_at(g + 1);
-    uint32_t w = __builtin_amdgcn_alignbyte(hi, lo, P & 3u);
-    if (P + 4u > end) w &= P >= end ? 0u : (1u << (8u * (end - P))) - 1u;
-    bb |= (uint64_t)w << nb;
-    nb += 32;
-    P += 4;
+    const uint32_t g = P >> 2, sh = P & 3u;
+    const uint32_t d0 = dword_at(g), d1 = dword_at(g + 1), d2 = dword_at(g + 2);
+    uint64_t w = ((uint64_t)__builtin_amdgcn_alignbyte(d2, d1, sh) << 32) | __builtin_amdgcn_alignbyte(d1, d0, sh);
+    if (P + 8u > end) w &= P >= end ? 0ull : ~0ull >> (64u - 8u * (end - P));
+    bb |= w << nb;
+    const uint32_t take = (63u - nb) >> 3;
+    P += take;
+    nb += 8u * take;
+    return P <= limit;
   }
   __device__ uint32_t peek(uint32_t k) const { return (uint32_t)bb & ((1u << k) - 1u); }
   __device__ void drop(uint32_t k) {
@@ -229,23 +311,7 @@ struct Reader {
   }
   // input bytes consumed (through the last bit used)
   __device__ uint64_t consumed() const { return (uint64_t)P - lead - nb / 8u; }
-  __device__ bool overrun() const { return (uint64_t)P > (uint64_t)lead + src_len + 16u; }
 };
-
-// canonical decode of a code longer than the LUT root (rare)
-__device__ uint32_t decode_slow(Reader &r, const uint16_t *cnt, const uint16_t *sym, uint32_t alphabet) {
-  int code = 0, first = 0, index = 0;
-  for (uint32_t L = 1; L <= 15; L++) {
-    code |= (int)((r.bb >> (L - 1)) & 1u);
-    const int ct = cnt[L];
-    if (code - ct < first) return symbol_entry(alphabet, sym[index + (code - first)], L);
-    index += ct;
-    first += ct;
-    first <<= 1;
-    code <<= 1;
-  }
-  return mk(0, K_BAD, 0, 0);
-}
 
 // A symbol the code cannot accept.  The canonical decoder (the oracle)
 // reads the whole code first -- its length, or all 15 bits when no code
@@ -256,128 +322,295 @@ __device__ __forceinline__ int32_t bad_symbol(Reader &r, uint32_t e, int32_t err
   return err;
 }
 
+// Output: bytes [fl, pos) are decoded but still only in the ring.  `room`
+// counts the literals/match bytes that may be added before something must
+// happen: min(cap - pos, kFlushLag - (pos - fl)).
 struct Out {
   uint8_t *dst;
   uint64_t cap;
   uint64_t pos;  // bytes produced
-  uint64_t fl;   // bytes flushed to dst
+  uint64_t fl;   // bytes flushed to dst (a multiple of 1024 until the end)
+  uint32_t room;
+  bool al16;     // dst 16-byte aligned
+  __device__ void set_room() {
+    const uint64_t c = cap - pos;
+    const uint32_t f = kFlushLag - (uint32_t)(pos - fl);
+    room = c < f ? (uint32_t)c : f;
+  }
 };
 
-__device__ void flush(Lds &s, Out &o, uint64_t upto) {
+// ring [fl, upto) -> dst, 1 KiB per step: one 16-B LDS read and one 16-B
+// store per lane when dst is 16-B aligned, else 16 coalesced byte steps.
+// Stores go through a buffer resource sized to the bytes due, so the
+// hardware drops the lanes past `upto` (no divergent branch).
+__device__ __forceinline__ void flush_to(Lds &s, Out &o, uint64_t upto) {
   const uint32_t lane = threadIdx.x;
   while (o.fl < upto) {
-    const uint64_t i = o.fl + lane;
-    if (i < upto) o.dst[i] = s.ring[i & kWinMask];
-    o.fl = (o.fl + 64 < upto) ? o.fl + 64 : upto;
+    const uint32_t roff = (uint32_t)(o.fl & kWinMask);
+    const uint32_t m = (upto - o.fl < 1024u) ? (uint32_t)(upto - o.fl) : 1024u;
+    const __amdgpu_buffer_rsrc_t d = __builtin_amdgcn_make_buffer_rsrc(o.dst + o.fl, (short)0, (int)m, 0x00020000);
+    if (o.al16 && m == 1024u) {
+      const uint4 v = *reinterpret_cast<const uint4 *>(&s.ring[roff + 16u * lane]);
+      typedef uint32_t v4w __attribute__((ext_vector_type(4)));
+      v4w w;
+      w.x = v.x;
+      w.y = v.y;
+      w.z = v.z;
+      w.w = v.w;
+      __builtin_amdgcn_raw_buffer_store_b128(w, d, 16u * lane, 0, 0);
+    } else {
+#pragma unroll
+      for (uint32_t k = 0; k < 16; k++)
+        __builtin_amdgcn_raw_buffer_store_b8(s.ring[roff + 64u * k + lane], d, 64u * k + lane, 0, 0);
+    }
+    o.fl += m;
   }
 }
 
-__device__ __forceinline__ void maybe_flush(Lds &s, Out &o) {
-  if (o.pos - o.fl >= kFlush) flush(s, o, o.fl + kFlush);
+// flush one kFlushLag batch when due (pending < kFlushLag + 1024 here, so
+// one suffices), then recompute the room.  An `if`, not a `while`: a second
+// loop level around flush_to's makes the structurizer treat the whole
+// decode state as divergent (VGPRs and select chains instead of SGPRs).
+__device__ __forceinline__ void settle(Lds &s, Out &o) {
+  if ((uint32_t)(o.pos - o.fl) >= kFlushLag) flush_to(s, o, o.fl + kFlushLag);
+  o.set_room();
 }
 
-// one Huffman-coded block (fixed or dynamic tables already built)
-__device__ int32_t codes(Lds &s, Reader &r, Out &o) {
+// lane-parallel copy of `len` bytes from `dist` back (dist <= pos checked);
+// lanes past `len` write to the dummy tail
+__device__ __forceinline__ void copy_match(Lds &s, uint32_t p0, uint32_t len, uint32_t dist) {
   const uint32_t lane = threadIdx.x;
+  const uint32_t src = p0 - dist;
+  if (dist >= 64u || len <= dist) {
+    // every source byte precedes the 64-byte step that writes it
+    for (uint32_t i0 = 0; i0 < len; i0 += 64) {
+      const uint32_t i = i0 + lane;
+      const uint8_t v = s.ring[(src + i) & kWinMask];
+      s.ring[i < len ? (p0 + i) & kWinMask : kDummy + 4u * lane] = v;
+    }
+  } else {
+    // short period: byte i repeats byte i mod dist
+    const float rcp = 1.0f / (float)dist;
+    for (uint32_t i0 = 0; i0 < len; i0 += 64) {
+      const uint32_t i = i0 + lane;
+      uint32_t m = i - (uint32_t)((float)i * rcp) * dist;
+      m = (int32_t)m < 0 ? m + dist : m;
+      m = m >= dist ? m - dist : m;
+      const uint8_t v = s.ring[(src + m) & kWinMask];
+      s.ring[i < len ? (p0 + i) & kWinMask : kDummy + 4u * lane] = v;
+    }
+  }
+}
+
+// Literal runs, the hot path of poorly compressible data (~93% of the
+// symbols of the spectrum payloads), as one hand-scheduled loop: ~22
+// instructions per literal (compiled C++ spends ~90 on predicate flow).
+// Decodes literals while >= 15 bits are buffered and room remains; lane 0
+// writes each byte into the ring, the other lanes into the dummy tail
+// (address = pos * sel + dummy, sel = 1 on lane 0 only).  Returns 0 when
+// the caller must refill first (fewer than 15 bits, or a non-literal / full
+// room with fewer than 48 bits), 1 when the next symbol needs the general
+// path.  Fixed registers: bb in s[60:61] (its low word is the LUT index and
+// the v_readlane lane select), the literal/length LUT in v[40:55] (read
+// with s_set_gpr_idx, as the compiler does for a dynamic vector subscript).
+// No hazard needs a wait state here: SALU results feed SALU, VALU and the
+// readlane lane select; the only VALU->SALU edge is v_readlane itself.
+__device__ __forceinline__ uint32_t literal_run(uint64_t &bb, uint32_t &nb, uint32_t &p, uint32_t &room,
+                                                const LLTab &ll, uint32_t vsel, uint32_t vdum) {
+  uint32_t why, t0, t1;
+  // VGPR temporaries are fixed clobbers (v56..v58), not outputs: an asm with
+  // a VGPR output counts as a source of divergence and would demote the
+  // whole decode state to VGPRs.
+  asm volatile(
+      "L_top_%=:\n\t"
+      "s_mov_b32 %[why], 0\n\t"
+      "s_cmp_lt_u32 %[nb], 15\n\t"
+      "s_cbranch_scc1 L_out_%=\n\t"
+      "s_bfe_u32 %[t0], s60, 0x40006\n\t"
+      "s_set_gpr_idx_on %[t0], gpr_idx(SRC0)\n\t"
+      "v_mov_b32 v56, v40\n\t"
+      "s_set_gpr_idx_off\n\t"
+      "v_readlane_b32 %[t1], v56, s60\n\t"
+      "s_bfe_u32 %[t0], %[t1], 0x30004\n\t"
+      "s_cmp_lg_u32 %[t0], 1\n\t"
+      "s_cbranch_scc1 L_chk_%=\n\t"
+      "s_cmp_eq_u32 %[room], 0\n\t"
+      "s_cbranch_scc1 L_chk_%=\n\t"
+      "s_and_b32 %[t0], %[t1], 15\n\t"
+      "s_lshr_b64 s[60:61], s[60:61], %[t0]\n\t"
+      "s_sub_u32 %[nb], %[nb], %[t0]\n\t"
+      "s_lshr_b32 %[t1], %[t1], 11\n\t"
+      "s_and_b32 %[t0], %[p], 0x7fff\n\t"
+      "v_mov_b32 v57, %[t1]\n\t"
+      "v_mad_u32_u24 v58, %[t0], %[vsel], %[vdum]\n\t"
+      "ds_write_b8 v58, v57\n\t"
+      "s_add_u32 %[p], %[p], 1\n\t"
+      "s_sub_u32 %[room], %[room], 1\n\t"
+      "s_branch L_top_%=\n\t"
+      "L_chk_%=:\n\t"
+      "s_cmp_lt_u32 %[nb], 48\n\t"
+      "s_cselect_b32 %[why], 0, 1\n\t"
+      "L_out_%=:"
+      : [nb] "+s"(nb), [room] "+s"(room), [p] "+s"(p), [why] "=&s"(why), [t0] "=&s"(t0), [t1] "=&s"(t1),
+        "+{s[60:61]}"(bb)
+      : [vdum] "v"(vdum), [vsel] "v"(vsel), "{v[40:55]}"(ll)
+      : "memory", "scc", "v56", "v57", "v58");
+  return why;
+}
+
+// One Huffman-coded block with the tables in ll / dd.  A single loop with
+// one exit: literal runs go through literal_run(), everything else through
+// the general path below.
+__device__ int32_t codes(Lds &s, Reader &r, Out &o, const LLTab &ll, const DTab &dd) {
+  const uint32_t lane = threadIdx.x;
+  const uint32_t ring_lds = (uint32_t)reinterpret_cast<uintptr_t>(
+      (__attribute__((address_space(3))) uint8_t *)(&s.ring[0]));
+  const uint32_t vsel = lane == 0 ? 1u : 0u;
+  const uint32_t vdum = ring_lds + (lane == 0 ? 0u : kDummy + 4u * lane);
+  int32_t st = ZCRC_INFLATE_OK;
   for (;;) {
-    if (r.overrun()) return ZCRC_INFLATE_ERR_INPUT;
-    r.refill();
-    uint32_t e = u32u(s.ll[r.peek(kLLRoot)]);
-    ITRACE("[%u] sym P=%u nb=%u bb=%llx e=%x kind=%u len=%u val=%u pos=%llu\n", blockIdx.x, r.P, r.nb,
-           (unsigned long long)r.bb, e, e_kind(e), e_len(e), e_val(e), (unsigned long long)o.pos);
-    if (e_kind(e) == K_LONG) e = u32u(decode_slow(r, s.llcnt, s.llsym, A_LITLEN));
+    if (r.nb < 48 && !r.refill()) {
+      st = ZCRC_INFLATE_ERR_INPUT;
+      break;
+    }
+#ifndef ZI_NO_ASM
+    {
+      // (readfirstlane: the compiler cannot always prove this state
+      // uniform, and the asm needs it in SGPRs)
+      uint32_t p = uni((uint32_t)o.pos);
+      const uint32_t p0 = p;
+      uint64_t bb = ((uint64_t)uni((uint32_t)(r.bb >> 32)) << 32) | uni((uint32_t)r.bb);
+      uint32_t nb = uni(r.nb), room = uni(o.room);
+      const uint32_t why = literal_run(bb, nb, p, room, ll, vsel, vdum);
+      r.bb = bb;
+      r.nb = nb;
+      o.room = room;
+      o.pos += p - p0;
+      if (!why) continue;
+    }
+#endif
+    const uint32_t ix = (uint32_t)r.bb & ((1u << kLLRoot) - 1u);
+    uint32_t e = lane_get(ll[ix >> 6], ix);
+    ITRACE("[%u] sym P=%u nb=%u e=%x kind=%u len=%u val=%u pos=%llu\n", blockIdx.x, r.P, r.nb, e, e_kind(e),
+           e_len(e), e_val(e), (unsigned long long)o.pos);
+    if (__builtin_expect(e_kind(e) == K_LONG, 0)) e = uni(decode_slow(r.peek(15), &s.llm, s.llsym, kLLRoot, A_LITLEN));
     const uint32_t kind = e_kind(e);
     if (kind == K_LIT) {
       r.drop(e_len(e));
-      if (o.pos >= o.cap) return ZCRC_INFLATE_ERR_OUTPUT;
-      if (lane == 0) s.ring[o.pos & kWinMask] = (uint8_t)e_val(e);
+      if (__builtin_expect(o.room == 0, 0)) {
+        if (o.pos >= o.cap) {
+          st = ZCRC_INFLATE_ERR_OUTPUT;
+          break;
+        }
+        settle(s, o);
+      }
+#ifndef ZI_ABL_NOLIT
+      s.ring[lane == 0 ? (uint32_t)o.pos & kWinMask : kDummy + 4u * lane] = (uint8_t)e_val(e);
+#endif
       o.pos++;
-      maybe_flush(s, o);
+      o.room--;
       continue;
     }
     if (kind == K_EOB) {
       r.drop(e_len(e));
-      return ZCRC_INFLATE_OK;
+      break;
     }
-    if (kind != K_BASE || e_len(e) == 0) return bad_symbol(r, e, ZCRC_INFLATE_ERR_SYMBOL);
+    if (kind != K_BASE || e_len(e) == 0) {
+      st = bad_symbol(r, e, ZCRC_INFLATE_ERR_SYMBOL);
+      break;
+    }
     r.drop(e_len(e));
     const uint32_t len = e_val(e) + r.peek(e_extra(e));
     r.drop(e_extra(e));
-    r.refill();
-    uint32_t d = u32u(s.dd[r.peek(kDRoot)]);
-    if (e_kind(d) == K_LONG) d = u32u(decode_slow(r, s.ddcnt, s.ddsym, A_DIST));
-    if (e_kind(d) != K_BASE || e_len(d) == 0) return bad_symbol(r, d, ZCRC_INFLATE_ERR_SYMBOL);
+    const uint32_t jx = (uint32_t)r.bb & ((1u << kDRoot) - 1u);
+    uint32_t d = lane_get(dd[jx >> 6], jx);
+    if (__builtin_expect(e_kind(d) == K_LONG, 0)) d = uni(decode_slow(r.peek(15), &s.ddm, s.ddsym, kDRoot, A_DIST));
+    if (e_kind(d) != K_BASE || e_len(d) == 0) {
+      st = bad_symbol(r, d, ZCRC_INFLATE_ERR_SYMBOL);
+      break;
+    }
     r.drop(e_len(d));
     const uint32_t dist = e_val(d) + r.peek(e_extra(d));
     r.drop(e_extra(d));
-    if (dist > o.pos) return ZCRC_INFLATE_ERR_DIST;
-    if (len > o.cap - o.pos) return ZCRC_INFLATE_ERR_OUTPUT;
-    // lane-parallel copy through the ring; every source byte precedes pos
-    // (short distances replicate with i mod dist; long ones go 64 at a time)
-    const uint32_t p0 = (uint32_t)o.pos;
-    for (uint32_t i0 = 0; i0 < len; i0 += 64) {
-      const uint32_t i = i0 + lane;
-      uint8_t v = 0;
-      if (i < len) {
-        const uint32_t off = dist < 64 ? i % dist : i;
-        v = s.ring[(p0 - dist + off) & kWinMask];
-      }
-      __builtin_amdgcn_wave_barrier();
-      if (i < len) s.ring[(p0 + i) & kWinMask] = v;
-      __builtin_amdgcn_wave_barrier();
+    if (dist > o.pos) {
+      st = ZCRC_INFLATE_ERR_DIST;
+      break;
     }
+    if (__builtin_expect(len > o.room, 0) && len > o.cap - o.pos) {
+      st = ZCRC_INFLATE_ERR_OUTPUT;
+      break;
+    }
+#ifndef ZI_ABL_NOCOPY
+    copy_match(s, (uint32_t)o.pos, len, dist);
+#endif
     o.pos += len;
-    maybe_flush(s, o);
+    if (__builtin_expect(len >= o.room, 0)) settle(s, o);  // may overshoot the lag by < 258
+    else o.room -= len;
   }
+  return st;
 }
 
 __device__ int32_t stored(Lds &s, Reader &r, Out &o) {
   const uint32_t lane = threadIdx.x;
   r.drop(r.nb & 7u);  // byte boundary
-  r.refill();
-  const uint32_t len = r.peek(16);
-  r.drop(16);
-  r.refill();
-  const uint32_t nlen = r.peek(16);
-  r.drop(16);
+  const uint32_t len = r.bits(16);
+  const uint32_t nlen = r.bits(16);
   if (len != (~nlen & 0xFFFFu)) return ZCRC_INFLATE_ERR_STORED_LEN;
   const uint32_t q = r.P - r.nb / 8u;  // next unconsumed byte (aligned-base relative)
-  if ((uint64_t)q - r.lead + len > r.src_len) return ZCRC_INFLATE_ERR_INPUT;
+  if ((uint64_t)q - r.lead + len > (uint64_t)(r.end - r.lead)) return ZCRC_INFLATE_ERR_INPUT;
   if (len > o.cap - o.pos) return ZCRC_INFLATE_ERR_OUTPUT;
-  const uint32_t p0 = (uint32_t)o.pos;
-  for (uint32_t i0 = 0; i0 < len; i0 += 64) {
-    const uint32_t i = i0 + lane;
-    if (i < len) {
-      const uint8_t v = __builtin_amdgcn_raw_buffer_load_b8(r.rsrc, q + i, 0, 0);
-      s.ring[(p0 + i) & kWinMask] = v;
+  // 1 KiB per step: 16 coalesced byte loads per lane, then 16 ring writes
+  for (uint32_t i0 = 0; i0 < len; i0 += 1024) {
+    uint32_t v[16];
+#pragma unroll
+    for (int k = 0; k < 16; k++) {
+      const uint32_t j = i0 + 64u * k + lane;
+      v[k] = __builtin_amdgcn_raw_buffer_load_b8(r.rsrc, q + j, 0, 0);  // lanes past len: discarded below
     }
-    __builtin_amdgcn_wave_barrier();
-    o.pos = p0 + ((i0 + 64 < len) ? i0 + 64 : len);
-    maybe_flush(s, o);
+    const uint32_t p0 = (uint32_t)o.pos;
+#pragma unroll
+    for (int k = 0; k < 16; k++) {
+      const uint32_t j = 64u * k + lane;
+      s.ring[i0 + j < len ? (p0 + j) & kWinMask : kDummy + 4u * lane] = (uint8_t)v[k];
+    }
+    o.pos += (len - i0 < 1024u) ? len - i0 : 1024u;
+    settle(s, o);
   }
   r.seek(q + len);
   return ZCRC_INFLATE_OK;
 }
 
-__device__ int32_t dynamic_tables(Lds &s, Reader &r) {
+__device__ int32_t dynamic_tables(Lds &s, Reader &r, LLTab &ll, DTab &dd) {
   const uint32_t lane = threadIdx.x;
   const uint32_t nlen = r.bits(5) + 257, ndist = r.bits(5) + 1, ncode = r.bits(4) + 4;
   if (nlen > 286 || ndist > 30) return ZCRC_INFLATE_ERR_CODES;
-  if (lane < 19) s.lens[lane] = 0;
-  __syncthreads();
-  for (uint32_t k = 0; k < ncode; k++) {
-    const uint32_t v = r.bits(3);
-    if (lane == 0) s.lens[c_clen_order[k]] = (uint8_t)v;
+  // code-length code lengths: 3 bits each, in kClenOrder order; lane k takes
+  // field k from a 30-bit then a 27-bit window
+  {
+    const uint32_t n1 = ncode < 10 ? ncode : 10;
+    r.refill();
+    const uint32_t w1 = r.peek(30);
+    r.drop(3 * n1);
+    uint32_t w2 = 0;
+    if (ncode > 10) {
+      r.refill();
+      w2 = r.peek(27);
+      r.drop(3 * (ncode - 10));
+    }
+    if (lane < 19) {
+      const uint32_t v = lane < 10 ? (w1 >> (3 * lane)) & 7u : (w2 >> (3 * (lane - 10))) & 7u;
+      s.cllens[kClenOrder[lane]] = (uint8_t)(lane < ncode ? v : 0u);
+    }
+    __syncthreads();
   }
-  __syncthreads();
-  // code-length code in the distance slots (max code length 7 = its root)
-  if (!build_code(s, s.lens, 19, kCLRoot, s.dd, s.ddcnt, s.ddsym, A_CLEN)) return ZCRC_INFLATE_ERR_CODES;
+  CLTab cl;
+  if (!build_code<kCLRoot, kCLRegs>(s.cllens, 19, s.clsym, nullptr, A_CLEN, cl)) return ZCRC_INFLATE_ERR_CODES;
   uint32_t idx = 0, prev = 0;
   const uint32_t total = nlen + ndist;
   while (idx < total) {
-    if (r.overrun()) return ZCRC_INFLATE_ERR_INPUT;
-    r.refill();
-    const uint32_t e = u32u(s.dd[r.peek(kCLRoot)]);
+    if (r.nb < 32 && !r.refill()) return ZCRC_INFLATE_ERR_INPUT;
+    const uint32_t ix = r.peek(kCLRoot);
+    const uint32_t e = lane_get(cl[ix >> 6], ix & 63u);
     if (e_kind(e) != K_LIT || e_len(e) == 0) return bad_symbol(r, e, ZCRC_INFLATE_ERR_CODES);
     r.drop(e_len(e));
     const uint32_t sym = e_val(e);
@@ -389,29 +622,31 @@ __device__ int32_t dynamic_tables(Lds &s, Reader &r) {
     } else if (sym == 16) {
       if (idx == 0) return ZCRC_INFLATE_ERR_CODES;
       val = prev;
-      rep = 3 + r.bits(2);
+      rep = 3 + r.peek(2);
+      r.drop(2);
     } else if (sym == 17) {
       val = 0;
-      rep = 3 + r.bits(3);
+      rep = 3 + r.peek(3);
+      r.drop(3);
       prev = 0;
     } else {
       val = 0;
-      rep = 11 + r.bits(7);
+      rep = 11 + r.peek(7);
+      r.drop(7);
       prev = 0;
     }
     if (idx + rep > total) return ZCRC_INFLATE_ERR_CODES;
-    for (uint32_t k = lane; k < rep; k += 64) s.lens[19 + idx + k] = (uint8_t)val;
+    for (uint32_t k = lane; k < rep; k += 64) s.lens[idx + k] = (uint8_t)val;
     idx += rep;
   }
   __syncthreads();
-  const uint8_t *ll = s.lens + 19, *dl = s.lens + 19 + nlen;
-  if (ll[256] == 0) return ZCRC_INFLATE_ERR_CODES;
-  if (!build_code(s, ll, nlen, kLLRoot, s.ll, s.llcnt, s.llsym, A_LITLEN)) return ZCRC_INFLATE_ERR_CODES;
-  if (!build_code(s, dl, ndist, kDRoot, s.dd, s.ddcnt, s.ddsym, A_DIST)) return ZCRC_INFLATE_ERR_CODES;
+  if (s.lens[256] == 0) return ZCRC_INFLATE_ERR_CODES;
+  if (!build_code<kLLRoot, kLLRegs>(s.lens, nlen, s.llsym, &s.llm, A_LITLEN, ll)) return ZCRC_INFLATE_ERR_CODES;
+  if (!build_code<kDRoot, kDRegs>(s.lens + nlen, ndist, s.ddsym, &s.ddm, A_DIST, dd)) return ZCRC_INFLATE_ERR_CODES;
   return ZCRC_INFLATE_OK;
 }
 
-__device__ void fixed_tables(Lds &s) {
+__device__ void fixed_tables(Lds &s, LLTab &ll, DTab &dd) {
   const uint32_t lane = threadIdx.x;
   for (uint32_t k = lane; k < 320; k += 64) {
     uint8_t l;
@@ -423,12 +658,12 @@ __device__ void fixed_tables(Lds &s) {
     s.lens[k] = l;
   }
   __syncthreads();
-  build_code(s, s.lens, 288, kLLRoot, s.ll, s.llcnt, s.llsym, A_LITLEN);
-  build_code(s, s.lens + 288, 32, kDRoot, s.dd, s.ddcnt, s.ddsym, A_DIST);
+  build_code<kLLRoot, kLLRegs>(s.lens, 288, s.llsym, &s.llm, A_LITLEN, ll);
+  build_code<kDRoot, kDRegs>(s.lens + 288, 32, s.ddsym, &s.ddm, A_DIST, dd);
 }
 
 __global__ __launch_bounds__(64) void inflate_kernel(InflateArgs a) {
-  __shared__ Lds s;
+  __shared__ __attribute__((aligned(16))) Lds s;
   const uint64_t i = blockIdx.x;
   if (i >= a.n) return;
   const uint8_t *src = a.src[i];
@@ -438,6 +673,8 @@ __global__ __launch_bounds__(64) void inflate_kernel(InflateArgs a) {
   o.cap = a.cap[i];
   o.pos = 0;
   o.fl = 0;
+  o.al16 = (reinterpret_cast<uint64_t>(o.dst) & 15u) == 0;
+  o.set_room();
   int32_t st = ZCRC_INFLATE_OK;
   Reader r;
   if (src_len == 0 || src_len > kInflateMaxSrc) {
@@ -445,45 +682,47 @@ __global__ __launch_bounds__(64) void inflate_kernel(InflateArgs a) {
   } else {
     const uint64_t base = reinterpret_cast<uint64_t>(src) & ~(uint64_t)15;
     r.lead = (uint32_t)(reinterpret_cast<uint64_t>(src) - base);
-    r.src_len = src_len;
     r.end = r.lead + (uint32_t)src_len;
+    r.limit = r.end + 16u;
     // The buffer unit range-checks whole dwords (a dword that straddles
     // num_records reads as 0), so the range is rounded up to the 16-byte
     // granule holding the last byte -- same page, never a fault -- and the
     // bytes past `end` are masked in refill().
-    r.rsrc = __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void *>(base), (short)0,
-                                               (int)((r.end + 15u) & ~15u), 0x00020000);
+    r.rsrc = __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void *>(base), (short)0, (int)((r.end + 15u) & ~15u),
+                                               0x00020000);
     r.seek(r.lead);
-    ITRACE("[%u] seek lead=%u A0=%x d0=%x d1=%x\n", blockIdx.x, r.lead, r.A.x, r.dword_at(0), r.dword_at(1));
+    LLTab ll;
+    DTab dd;
     uint32_t last = 0;
     do {
-      if (r.overrun()) {
+      if (!r.refill()) {
         st = ZCRC_INFLATE_ERR_INPUT;
         break;
       }
-      ITRACE("[%u] hdr P=%u nb=%u bb=%llx lead=%u srclen=%llu\n", blockIdx.x, r.P, r.nb,
-             (unsigned long long)r.bb, r.lead, (unsigned long long)r.src_len);
-      last = r.bits(1);
-      const uint32_t type = r.bits(2);
-      ITRACE("[%u]   last=%u type=%u\n", blockIdx.x, last, type);
+      last = r.peek(1);
+      const uint32_t type = (uint32_t)(r.bb >> 1) & 3u;
+      r.drop(3);
+      ITRACE("[%u] block last=%u type=%u P=%u nb=%u pos=%llu\n", blockIdx.x, last, type, r.P, r.nb,
+             (unsigned long long)o.pos);
       if (type == 0) {
         st = stored(s, r, o);
       } else if (type == 1) {
-        fixed_tables(s);
-        st = codes(s, r, o);
+        fixed_tables(s, ll, dd);
+        st = codes(s, r, o, ll, dd);
       } else if (type == 2) {
-        st = dynamic_tables(s, r);
-        if (st == ZCRC_INFLATE_OK) st = codes(s, r, o);
+        st = dynamic_tables(s, r, ll, dd);
+        if (st == ZCRC_INFLATE_OK) st = codes(s, r, o, ll, dd);
       } else {
         st = ZCRC_INFLATE_ERR_BLOCK_TYPE;
       }
+      st = (int32_t)uni((uint32_t)st);
     } while (!last && st == ZCRC_INFLATE_OK);
     // Bits past the end read as zero.  Whenever the decode used any of them
     // -- whether it then ended cleanly or failed on what they said -- the
     // canonical decoder would have stopped at the first one: input error.
     if (r.consumed() > src_len) st = ZCRC_INFLATE_ERR_INPUT;
   }
-  if (st == ZCRC_INFLATE_OK) flush(s, o, o.pos);
+  if (st == ZCRC_INFLATE_OK) flush_to(s, o, o.pos);
   if (threadIdx.x == 0) {
     a.out_len[i] = st == ZCRC_INFLATE_OK ? o.pos : 0;
     a.status[i] = st;
