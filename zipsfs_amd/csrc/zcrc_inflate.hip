@@ -243,6 +243,12 @@ __device__ __noinline__ uint32_t decode_slow(uint32_t bits15, const CodeMeta *m,
 // (g & 3) of lane (g >> 2) & 63: one s_set_gpr_idx move and a v_readlane.
 // Blocks kA and kA + 1 are resident, kA + 2 is in flight in `pend` and lands
 // in its slot at the next slide, by which time its load has returned.
+//
+// Refills add 32 bits at a time while at most 32 are buffered.  P advances
+// in steps of 4, so P & 3 is fixed between seeks: the dword holding byte P
+// is cached in q, and a refill fetches one new dword (g + 1) and funnels
+// the pair.  Refills never slide: callers slide first (slide_if_needed),
+// which keeps a single site that rewrites the staging registers.
 struct Reader {
   __amdgpu_buffer_rsrc_t rsrc;
   uint32_t lead;   // src - (src & ~15)
@@ -251,9 +257,11 @@ struct Reader {
   v16u st;
   uint4 pend;
   uint32_t kA;
-  uint32_t P;   // next byte (relative to the aligned base) to enter bb
-  uint64_t bb;  // bit buffer, LSB first
-  uint32_t nb;  // valid bits in bb
+  uint32_t P;    // next byte (relative to the aligned base) to enter bb
+  uint32_t q;    // dword P >> 2
+  uint32_t sh8;  // 8 * (P & 3)
+  uint64_t bb;   // bit buffer, LSB first
+  uint32_t nb;   // valid bits in bb
 
   __device__ uint4 load_block(uint32_t k) const {
     auto v = __builtin_amdgcn_raw_buffer_load_b128(rsrc, k * 1024u + 16u * threadIdx.x, 0, 0);
@@ -267,6 +275,7 @@ struct Reader {
       default: st.sc = v.x; st.sd = v.y; st.se = v.z; st.sf = v.w; break;
     }
   }
+  __device__ uint32_t dword_at(uint32_t g) const { return lane_get(st[((g >> 6) & 12u) | (g & 3u)], (g >> 2) & 63u); }
   __device__ void seek(uint32_t p) {
     P = p;
     bb = 0;
@@ -275,28 +284,33 @@ struct Reader {
     put_slot(kA, load_block(kA));
     put_slot(kA + 1, load_block(kA + 1));
     pend = load_block(kA + 2);
+    q = dword_at(p >> 2);
+    sh8 = 8u * (p & 3u);
   }
-  __device__ uint32_t dword_at(uint32_t g) const { return lane_get(st[((g >> 6) & 12u) | (g & 3u)], (g >> 2) & 63u); }
-  // Top up to 56..63 valid bits (enough for a whole length/distance pair,
-  // at most 48 bits, so the symbol loop refills once per symbol at most):
-  // the 8 bytes at P are or-ed in above the valid bits and P advances by the
-  // whole bytes that fit.  Bytes at or past `end` read as zero.  False once
-  // the input is overrun.
-  __device__ bool refill() {
-    if (P >= (kA + 1) * 1024u) {  // slide: land kA + 2, prefetch kA + 3
+  // once P has entered block kA + 1: land kA + 2, prefetch kA + 3
+  __device__ void slide_if_needed() {
+    if ((P >> 10) != kA) {
       put_slot(kA + 2, pend);
       kA++;
       pend = load_block(kA + 2);
     }
-    const uint32_t g = P >> 2, sh = P & 3u;
-    const uint32_t d0 = dword_at(g), d1 = dword_at(g + 1), d2 = dword_at(g + 2);
-    uint64_t w = ((uint64_t)__builtin_amdgcn_alignbyte(d2, d1, sh) << 32) | __builtin_amdgcn_alignbyte(d1, d0, sh);
-    if (P + 8u > end) w &= P >= end ? 0ull : ~0ull >> (64u - 8u * (end - P));
-    bb |= w << nb;
-    const uint32_t take = (63u - nb) >> 3;
-    P += take;
-    nb += 8u * take;
+  }
+  // +32 bits (caller: nb <= 32, slid within the last ~1 KiB); bytes at or
+  // past `end` read as zero; false once the input is overrun
+  __device__ bool refill() {
+    const uint32_t r = dword_at((P >> 2) + 1);
+    uint32_t w = (uint32_t)((((uint64_t)r << 32) | q) >> sh8);
+    if (P + 4u > end) w &= P >= end ? 0u : (1u << (8u * (end - P))) - 1u;
+    bb |= (uint64_t)w << nb;
+    nb += 32;
+    P += 4;
+    q = r;
     return P <= limit;
+  }
+  // slow paths: slide if due, refill if at most 32 bits are buffered
+  __device__ bool ensure() {
+    slide_if_needed();
+    return nb > 32 || refill();
   }
   __device__ uint32_t peek(uint32_t k) const { return (uint32_t)bb & ((1u << k) - 1u); }
   __device__ void drop(uint32_t k) {
@@ -304,7 +318,7 @@ struct Reader {
     nb -= k;
   }
   __device__ uint32_t bits(uint32_t k) {  // k <= 16
-    refill();
+    ensure();
     const uint32_t v = peek(k);
     drop(k);
     return v;
@@ -404,38 +418,71 @@ __device__ __forceinline__ void copy_match(Lds &s, uint32_t p0, uint32_t len, ui
 
 // Literal runs, the hot path of poorly compressible data (~93% of the
 // symbols of the spectrum payloads), as one hand-scheduled loop: ~22
-// instructions per literal (compiled C++ spends ~90 on predicate flow).
-// Decodes literals while >= 15 bits are buffered and room remains; lane 0
-// writes each byte into the ring, the other lanes into the dummy tail
-// (address = pos * sel + dummy, sel = 1 on lane 0 only).  Returns 0 when
-// the caller must refill first (fewer than 15 bits, or a non-literal / full
-// room with fewer than 48 bits), 1 when the next symbol needs the general
-// path.  Fixed registers: bb in s[60:61] (its low word is the LUT index and
-// the v_readlane lane select), the literal/length LUT in v[40:55] (read
-// with s_set_gpr_idx, as the compiler does for a dynamic vector subscript).
-// No hazard needs a wait state here: SALU results feed SALU, VALU and the
-// readlane lane select; the only VALU->SALU edge is v_readlane itself.
-__device__ __forceinline__ uint32_t literal_run(uint64_t &bb, uint32_t &nb, uint32_t &p, uint32_t &room,
-                                                const LLTab &ll, uint32_t vsel, uint32_t vdum) {
-  uint32_t why, t0, t1;
-  // VGPR temporaries are fixed clobbers (v56..v58), not outputs: an asm with
-  // a VGPR output counts as a source of divergence and would demote the
-  // whole decode state to VGPRs.
+// instructions per literal plus a ~24-instruction 32-bit refill every ~3.5
+// literals (compiled C++ spent ~90 per literal on predicate flow).
+// Keeps >= 33 bits buffered, refilling inline; decodes literals while room
+// remains; lane 0 writes each byte into the ring, the other lanes into the
+// dummy tail (address = pos * sel + dummy, sel = 1 on lane 0 only).
+// Returns 0 when the caller must slide or refill first (P entered the next
+// block, or the refill would read past `end`), 1 when the next symbol needs
+// the general path (non-literal, or no room) -- then >= 33 bits are buffered.
+// Fixed registers: bb in s[60:61] (its low word is the LUT index and the
+// v_readlane lane select), {q, r} in s[62:63] (funnel-shifted by s_lshr_b64),
+// the literal/length LUT in v[40:55] and the input ring in v[60:75], both
+// read with s_set_gpr_idx (as the compiler does for a dynamic subscript).
+// VGPR temporaries are fixed clobbers (v56..v58), not outputs: an asm with a
+// VGPR output counts as a source of divergence and would demote the whole
+// decode state to VGPRs.  No hazard needs a wait state: SALU results feed
+// SALU, VALU and readlane lane selects; the only VALU->SALU edges are
+// v_readlane results.
+__device__ __forceinline__ uint32_t literal_run(Reader &r, uint32_t &p, uint32_t &room, const LLTab &ll,
+                                                uint32_t vsel, uint32_t vdum) {
+  uint32_t why, t0, t1, t2;
+  uint64_t bb = r.bb;
+  uint64_t qr = r.q;
+  uint32_t nb = r.nb, P = r.P;
   asm volatile(
       "L_top_%=:\n\t"
+      "s_cmp_gt_u32 %[nb], 32\n\t"
+      "s_cbranch_scc1 L_have_%=\n\t"
+      // refill 32 bits: exit if past the end or into the next block
       "s_mov_b32 %[why], 0\n\t"
-      "s_cmp_lt_u32 %[nb], 15\n\t"
+      "s_add_u32 %[t2], %[P], 4\n\t"
+      "s_cmp_gt_u32 %[t2], %[end]\n\t"
       "s_cbranch_scc1 L_out_%=\n\t"
+      "s_lshr_b32 %[t0], %[P], 10\n\t"
+      "s_cmp_lg_u32 %[t0], %[ka]\n\t"
+      "s_cbranch_scc1 L_out_%=\n\t"
+      "s_lshr_b32 %[t1], %[P], 2\n\t"
+      "s_add_u32 %[t1], %[t1], 1\n\t"
+      "s_lshr_b32 %[t0], %[t1], 6\n\t"
+      "s_and_b32 %[t0], %[t0], 12\n\t"
+      "s_and_b32 %[t2], %[t1], 3\n\t"
+      "s_or_b32 %[t0], %[t0], %[t2]\n\t"
+      "s_lshr_b32 %[t1], %[t1], 2\n\t"
+      "s_set_gpr_idx_on %[t0], gpr_idx(SRC0)\n\t"
+      "v_mov_b32 v56, v60\n\t"
+      "s_set_gpr_idx_off\n\t"
+      "v_readlane_b32 s63, v56, %[t1]\n\t"
+      "s_lshr_b64 s[64:65], s[62:63], %[sh8]\n\t"
+      "s_mov_b32 s65, 0\n\t"
+      "s_lshl_b64 s[64:65], s[64:65], %[nb]\n\t"
+      "s_or_b64 s[60:61], s[60:61], s[64:65]\n\t"
+      "s_mov_b32 s62, s63\n\t"
+      "s_add_u32 %[nb], %[nb], 32\n\t"
+      "s_add_u32 %[P], %[P], 4\n\t"
+      "L_have_%=:\n\t"
       "s_bfe_u32 %[t0], s60, 0x40006\n\t"
       "s_set_gpr_idx_on %[t0], gpr_idx(SRC0)\n\t"
       "v_mov_b32 v56, v40\n\t"
       "s_set_gpr_idx_off\n\t"
       "v_readlane_b32 %[t1], v56, s60\n\t"
+      "s_mov_b32 %[why], 1\n\t"
       "s_bfe_u32 %[t0], %[t1], 0x30004\n\t"
       "s_cmp_lg_u32 %[t0], 1\n\t"
-      "s_cbranch_scc1 L_chk_%=\n\t"
+      "s_cbranch_scc1 L_out_%=\n\t"
       "s_cmp_eq_u32 %[room], 0\n\t"
-      "s_cbranch_scc1 L_chk_%=\n\t"
+      "s_cbranch_scc1 L_out_%=\n\t"
       "s_and_b32 %[t0], %[t1], 15\n\t"
       "s_lshr_b64 s[60:61], s[60:61], %[t0]\n\t"
       "s_sub_u32 %[nb], %[nb], %[t0]\n\t"
@@ -447,14 +494,16 @@ __device__ __forceinline__ uint32_t literal_run(uint64_t &bb, uint32_t &nb, uint
       "s_add_u32 %[p], %[p], 1\n\t"
       "s_sub_u32 %[room], %[room], 1\n\t"
       "s_branch L_top_%=\n\t"
-      "L_chk_%=:\n\t"
-      "s_cmp_lt_u32 %[nb], 48\n\t"
-      "s_cselect_b32 %[why], 0, 1\n\t"
       "L_out_%=:"
-      : [nb] "+s"(nb), [room] "+s"(room), [p] "+s"(p), [why] "=&s"(why), [t0] "=&s"(t0), [t1] "=&s"(t1),
-        "+{s[60:61]}"(bb)
-      : [vdum] "v"(vdum), [vsel] "v"(vsel), "{v[40:55]}"(ll)
-      : "memory", "scc", "v56", "v57", "v58");
+      : [nb] "+s"(nb), [room] "+s"(room), [p] "+s"(p), [P] "+s"(P), [why] "=&s"(why), [t0] "=&s"(t0),
+        [t1] "=&s"(t1), [t2] "=&s"(t2), "+{s[60:61]}"(bb), "+{s[62:63]}"(qr)
+      : [vdum] "v"(vdum), [vsel] "v"(vsel), [end] "s"(r.end), [ka] "s"(r.kA), [sh8] "s"(r.sh8),
+        "{v[40:55]}"(ll), "{v[60:75]}"(r.st)
+      : "memory", "scc", "v56", "v57", "v58", "s64", "s65");
+  r.bb = bb;
+  r.q = (uint32_t)qr;
+  r.nb = nb;
+  r.P = P;
   return why;
 }
 
@@ -469,7 +518,8 @@ __device__ int32_t codes(Lds &s, Reader &r, Out &o, const LLTab &ll, const DTab 
   const uint32_t vdum = ring_lds + (lane == 0 ? 0u : kDummy + 4u * lane);
   int32_t st = ZCRC_INFLATE_OK;
   for (;;) {
-    if (r.nb < 48 && !r.refill()) {
+    r.slide_if_needed();  // the only slide site of the symbol loop
+    if (r.nb <= 32 && !r.refill()) {
       st = ZCRC_INFLATE_ERR_INPUT;
       break;
     }
@@ -479,11 +529,12 @@ __device__ int32_t codes(Lds &s, Reader &r, Out &o, const LLTab &ll, const DTab 
       // uniform, and the asm needs it in SGPRs)
       uint32_t p = uni((uint32_t)o.pos);
       const uint32_t p0 = p;
-      uint64_t bb = ((uint64_t)uni((uint32_t)(r.bb >> 32)) << 32) | uni((uint32_t)r.bb);
-      uint32_t nb = uni(r.nb), room = uni(o.room);
-      const uint32_t why = literal_run(bb, nb, p, room, ll, vsel, vdum);
-      r.bb = bb;
-      r.nb = nb;
+      r.bb = ((uint64_t)uni((uint32_t)(r.bb >> 32)) << 32) | uni((uint32_t)r.bb);
+      r.nb = uni(r.nb);
+      r.P = uni(r.P);
+      r.q = uni(r.q);
+      uint32_t room = uni(o.room);
+      const uint32_t why = literal_run(r, p, room, ll, vsel, vdum);
       o.room = room;
       o.pos += p - p0;
       if (!why) continue;
@@ -522,6 +573,10 @@ __device__ int32_t codes(Lds &s, Reader &r, Out &o, const LLTab &ll, const DTab 
     r.drop(e_len(e));
     const uint32_t len = e_val(e) + r.peek(e_extra(e));
     r.drop(e_extra(e));
+    if (r.nb <= 32 && !r.refill()) {  // <= 8 bytes past the slide check: still resident
+      st = ZCRC_INFLATE_ERR_INPUT;
+      break;
+    }
     const uint32_t jx = (uint32_t)r.bb & ((1u << kDRoot) - 1u);
     uint32_t d = lane_get(dd[jx >> 6], jx);
     if (__builtin_expect(e_kind(d) == K_LONG, 0)) d = uni(decode_slow(r.peek(15), &s.ddm, s.ddsym, kDRoot, A_DIST));
@@ -588,12 +643,12 @@ __device__ int32_t dynamic_tables(Lds &s, Reader &r, LLTab &ll, DTab &dd) {
   // field k from a 30-bit then a 27-bit window
   {
     const uint32_t n1 = ncode < 10 ? ncode : 10;
-    r.refill();
+    r.ensure();
     const uint32_t w1 = r.peek(30);
     r.drop(3 * n1);
     uint32_t w2 = 0;
     if (ncode > 10) {
-      r.refill();
+      r.ensure();
       w2 = r.peek(27);
       r.drop(3 * (ncode - 10));
     }
@@ -608,7 +663,7 @@ __device__ int32_t dynamic_tables(Lds &s, Reader &r, LLTab &ll, DTab &dd) {
   uint32_t idx = 0, prev = 0;
   const uint32_t total = nlen + ndist;
   while (idx < total) {
-    if (r.nb < 32 && !r.refill()) return ZCRC_INFLATE_ERR_INPUT;
+    if (!r.ensure()) return ZCRC_INFLATE_ERR_INPUT;
     const uint32_t ix = r.peek(kCLRoot);
     const uint32_t e = lane_get(cl[ix >> 6], ix & 63u);
     if (e_kind(e) != K_LIT || e_len(e) == 0) return bad_symbol(r, e, ZCRC_INFLATE_ERR_CODES);
@@ -695,7 +750,7 @@ __global__ __launch_bounds__(64) void inflate_kernel(InflateArgs a) {
     DTab dd;
     uint32_t last = 0;
     do {
-      if (!r.refill()) {
+      if (!r.ensure()) {
         st = ZCRC_INFLATE_ERR_INPUT;
         break;
       }
