@@ -44,7 +44,10 @@
 namespace zcrc {
 namespace {
 
-constexpr uint32_t kWin = 32768, kWinMask = kWin - 1;
+// The LDS ring holds the last kWin bytes; DEFLATE distances reach 32 KiB,
+// and the older bytes are read back from dst (they are flushed by then):
+// a 16 KiB ring fits eight streams per CU instead of four.
+constexpr uint32_t kWin = 16384, kWinMask = kWin - 1;
 constexpr uint32_t kLLRoot = 10, kDRoot = 8, kCLRoot = 7;
 constexpr uint32_t kLLRegs = (1u << kLLRoot) / 64, kDRegs = (1u << kDRoot) / 64, kCLRegs = (1u << kCLRoot) / 64;
 constexpr uint32_t kFlushLag = 8192;  // bytes decoded ahead of the last flush
@@ -379,6 +382,9 @@ __device__ __forceinline__ void flush_to(Lds &s, Out &o, uint64_t upto) {
     }
     o.fl += m;
   }
+  // far matches read flushed bytes back with sc1 (L2) loads: let these
+  // stores reach L2 first (once per kFlushLag batch)
+  __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
 }
 
 // flush one kFlushLag batch when due (pending < kFlushLag + 1024 here, so
@@ -391,11 +397,26 @@ __device__ __forceinline__ void settle(Lds &s, Out &o) {
 }
 
 // lane-parallel copy of `len` bytes from `dist` back (dist <= pos checked);
-// lanes past `len` write to the dummy tail
-__device__ __forceinline__ void copy_match(Lds &s, uint32_t p0, uint32_t len, uint32_t dist) {
+// lanes past `len` write to the dummy tail.  Sources older than the ring
+// (dist > kWin) are flushed already (pos - fl < kFlushLag + 1024 + 258 <
+// kWin) and are read back from dst with sc1 loads, which bypass the CU's
+// L1 (a line cached there may predate the flush of its other bytes).
+__device__ __forceinline__ void copy_match(Lds &s, const Out &o, uint32_t p0, uint32_t len, uint32_t dist) {
   const uint32_t lane = threadIdx.x;
   const uint32_t src = p0 - dist;
-  if (dist >= 64u || len <= dist) {
+  if (dist > kWin) {
+    const __amdgpu_buffer_rsrc_t far =
+        __builtin_amdgcn_make_buffer_rsrc(o.dst + (o.pos - dist), (short)0, (int)len, 0x00020000);
+    uint32_t v[5];  // len <= 258
+#pragma unroll
+    for (uint32_t k = 0; k < 5; k++)
+      v[k] = (64u * k < len) ? __builtin_amdgcn_raw_buffer_load_b8(far, 64u * k + lane, 0, 16) : 0u;
+#pragma unroll
+    for (uint32_t k = 0; k < 5; k++) {
+      const uint32_t i = 64u * k + lane;
+      if (64u * k < len) s.ring[i < len ? (p0 + i) & kWinMask : kDummy + 4u * lane] = (uint8_t)v[k];
+    }
+  } else if (dist >= 64u || len <= dist) {
     // every source byte precedes the 64-byte step that writes it
     for (uint32_t i0 = 0; i0 < len; i0 += 64) {
       const uint32_t i = i0 + lane;
@@ -487,7 +508,7 @@ __device__ __forceinline__ uint32_t literal_run(Reader &r, uint32_t &p, uint32_t
       "s_lshr_b64 s[60:61], s[60:61], %[t0]\n\t"
       "s_sub_u32 %[nb], %[nb], %[t0]\n\t"
       "s_lshr_b32 %[t1], %[t1], 11\n\t"
-      "s_and_b32 %[t0], %[p], 0x7fff\n\t"
+      "s_and_b32 %[t0], %[p], %[wm]\n\t"
       "v_mov_b32 v57, %[t1]\n\t"
       "v_mad_u32_u24 v58, %[t0], %[vsel], %[vdum]\n\t"
       "ds_write_b8 v58, v57\n\t"
@@ -497,7 +518,7 @@ __device__ __forceinline__ uint32_t literal_run(Reader &r, uint32_t &p, uint32_t
       "L_out_%=:"
       : [nb] "+s"(nb), [room] "+s"(room), [p] "+s"(p), [P] "+s"(P), [why] "=&s"(why), [t0] "=&s"(t0),
         [t1] "=&s"(t1), [t2] "=&s"(t2), "+{s[60:61]}"(bb), "+{s[62:63]}"(qr)
-      : [vdum] "v"(vdum), [vsel] "v"(vsel), [end] "s"(r.end), [ka] "s"(r.kA), [sh8] "s"(r.sh8),
+      : [vdum] "v"(vdum), [vsel] "v"(vsel), [end] "s"(r.end), [ka] "s"(r.kA), [sh8] "s"(r.sh8), [wm] "i"(kWinMask),
         "{v[40:55]}"(ll), "{v[60:75]}"(r.st)
       : "memory", "scc", "v56", "v57", "v58", "s64", "s65");
   r.bb = bb;
@@ -596,7 +617,7 @@ __device__ int32_t codes(Lds &s, Reader &r, Out &o, const LLTab &ll, const DTab 
       break;
     }
 #ifndef ZI_ABL_NOCOPY
-    copy_match(s, (uint32_t)o.pos, len, dist);
+    copy_match(s, o, (uint32_t)o.pos, len, dist);
 #endif
     o.pos += len;
     if (__builtin_expect(len >= o.room, 0)) settle(s, o);  // may overshoot the lag by < 258
