@@ -67,7 +67,9 @@ typedef VecOf<kLLRegs>::T LLTab;
 typedef VecOf<kDRegs>::T DTab;
 typedef VecOf<kCLRegs>::T CLTab;
 
-// LUT entry: [0:4) code length, [4:7) kind, [7:11) extra bits, [11:27) value
+// LUT entry: [0:4) code length, [4:7) kind, [7:11) extra bits, [11:27) value;
+// literal/length literals also set bit 31 (one sign test in literal_run)
+constexpr uint32_t kLitFlag = 0x80000000u;
 enum : uint32_t { K_BAD = 0, K_LIT = 1, K_BASE = 2, K_EOB = 3, K_LONG = 4 };
 enum : uint32_t { A_LITLEN = 0, A_DIST = 1, A_CLEN = 2 };
 
@@ -90,7 +92,7 @@ __device__ __forceinline__ uint32_t lane_get(uint32_t v, uint32_t lane) {
 // d + 1 below 4, else e = d / 2 - 1 extra bits and base ((2 + d % 2) << e) + 1.
 __device__ __forceinline__ uint32_t symbol_entry(uint32_t alphabet, uint32_t sym, uint32_t len) {
   if (alphabet == A_LITLEN) {
-    if (sym < 256) return mk(len, K_LIT, 0, sym);
+    if (sym < 256) return mk(len, K_LIT, 0, sym) | kLitFlag;  // bit 31: literal (asm sign test)
     if (sym == 256) return mk(len, K_EOB, 0, 0);
     if (sym < 285) {
       const uint32_t k = sym - 257;
@@ -438,9 +440,12 @@ __device__ __forceinline__ void copy_match(Lds &s, const Out &o, uint32_t p0, ui
 }
 
 // Literal runs, the hot path of poorly compressible data (~93% of the
-// symbols of the spectrum payloads), as one hand-scheduled loop: ~22
-// instructions per literal plus a ~24-instruction 32-bit refill every ~3.5
-// literals (compiled C++ spent ~90 per literal on predicate flow).
+// symbols of the spectrum payloads), as one hand-scheduled loop, unrolled
+// twice: ~20 instructions per literal, one taken branch per two, plus a
+// ~24-instruction 32-bit refill every ~3.5 literals (compiled C++ spent ~90
+// per literal on predicate flow).  The ring address of the next byte is
+// computed while the LUT lookup is in flight; bit 31 of an entry marks a
+// literal (one sign test); room is decremented and checked in one step.
 // Keeps >= 33 bits buffered, refilling inline; decodes literals while room
 // remains; lane 0 writes each byte into the ring, the other lanes into the
 // dummy tail (address = pos * sel + dummy, sel = 1 on lane 0 only).
@@ -464,16 +469,56 @@ __device__ __forceinline__ uint32_t literal_run(Reader &r, uint32_t &p, uint32_t
   uint32_t nb = r.nb, P = r.P;
   asm volatile(
       "L_top_%=:\n\t"
-      "s_cmp_gt_u32 %[nb], 32\n\t"
-      "s_cbranch_scc1 L_have_%=\n\t"
-      // refill 32 bits: exit if past the end or into the next block
-      "s_mov_b32 %[why], 0\n\t"
+      "s_cmp_le_u32 %[nb], 32\n\t"
+      "s_cbranch_scc1 L_ref_%=\n\t"
+      "L_have_%=:\n\t"
+      "s_bfe_u32 %[t0], s60, 0x40006\n\t"
+      "s_set_gpr_idx_on %[t0], gpr_idx(SRC0)\n\t"
+      "v_mov_b32 v56, v40\n\t"
+      "s_set_gpr_idx_off\n\t"
+      "s_and_b32 %[t2], %[p], %[wm]\n\t"
+      "v_mad_u32_u24 v58, %[t2], %[vsel], %[vdum]\n\t"
+      "v_readlane_b32 %[t1], v56, s60\n\t"
+      "s_cmp_gt_i32 %[t1], -1\n\t"
+      "s_cbranch_scc1 L_gen_%=\n\t"
+      "s_sub_u32 %[room], %[room], 1\n\t"
+      "s_cbranch_scc1 L_full_%=\n\t"
+      "s_and_b32 %[t0], %[t1], 15\n\t"
+      "s_lshr_b64 s[60:61], s[60:61], %[t0]\n\t"
+      "s_sub_u32 %[nb], %[nb], %[t0]\n\t"
+      "s_lshr_b32 %[t1], %[t1], 11\n\t"
+      "v_mov_b32 v57, %[t1]\n\t"
+      "ds_write_b8 v58, v57\n\t"
+      "s_add_u32 %[p], %[p], 1\n\t"
+      "s_cmp_le_u32 %[nb], 32\n\t"
+      "s_cbranch_scc1 L_ref_%=\n\t"
+      "s_bfe_u32 %[t0], s60, 0x40006\n\t"
+      "s_set_gpr_idx_on %[t0], gpr_idx(SRC0)\n\t"
+      "v_mov_b32 v56, v40\n\t"
+      "s_set_gpr_idx_off\n\t"
+      "s_and_b32 %[t2], %[p], %[wm]\n\t"
+      "v_mad_u32_u24 v58, %[t2], %[vsel], %[vdum]\n\t"
+      "v_readlane_b32 %[t1], v56, s60\n\t"
+      "s_cmp_gt_i32 %[t1], -1\n\t"
+      "s_cbranch_scc1 L_gen_%=\n\t"
+      "s_sub_u32 %[room], %[room], 1\n\t"
+      "s_cbranch_scc1 L_full_%=\n\t"
+      "s_and_b32 %[t0], %[t1], 15\n\t"
+      "s_lshr_b64 s[60:61], s[60:61], %[t0]\n\t"
+      "s_sub_u32 %[nb], %[nb], %[t0]\n\t"
+      "s_lshr_b32 %[t1], %[t1], 11\n\t"
+      "v_mov_b32 v57, %[t1]\n\t"
+      "ds_write_b8 v58, v57\n\t"
+      "s_add_u32 %[p], %[p], 1\n\t"
+      "s_branch L_top_%=\n\t"
+      // refill 32 bits: exit (0) if past the end or into the next block
+      "L_ref_%=:\n\t"
       "s_add_u32 %[t2], %[P], 4\n\t"
       "s_cmp_gt_u32 %[t2], %[end]\n\t"
-      "s_cbranch_scc1 L_out_%=\n\t"
+      "s_cbranch_scc1 L_zero_%=\n\t"
       "s_lshr_b32 %[t0], %[P], 10\n\t"
       "s_cmp_lg_u32 %[t0], %[ka]\n\t"
-      "s_cbranch_scc1 L_out_%=\n\t"
+      "s_cbranch_scc1 L_zero_%=\n\t"
       "s_lshr_b32 %[t1], %[P], 2\n\t"
       "s_add_u32 %[t1], %[t1], 1\n\t"
       "s_lshr_b32 %[t0], %[t1], 6\n\t"
@@ -492,29 +537,14 @@ __device__ __forceinline__ uint32_t literal_run(Reader &r, uint32_t &p, uint32_t
       "s_mov_b32 s62, s63\n\t"
       "s_add_u32 %[nb], %[nb], 32\n\t"
       "s_add_u32 %[P], %[P], 4\n\t"
-      "L_have_%=:\n\t"
-      "s_bfe_u32 %[t0], s60, 0x40006\n\t"
-      "s_set_gpr_idx_on %[t0], gpr_idx(SRC0)\n\t"
-      "v_mov_b32 v56, v40\n\t"
-      "s_set_gpr_idx_off\n\t"
-      "v_readlane_b32 %[t1], v56, s60\n\t"
+      "s_branch L_have_%=\n\t"
+      "L_full_%=:\n\t"
+      "s_add_u32 %[room], %[room], 1\n\t"
+      "L_gen_%=:\n\t"
       "s_mov_b32 %[why], 1\n\t"
-      "s_bfe_u32 %[t0], %[t1], 0x30004\n\t"
-      "s_cmp_lg_u32 %[t0], 1\n\t"
-      "s_cbranch_scc1 L_out_%=\n\t"
-      "s_cmp_eq_u32 %[room], 0\n\t"
-      "s_cbranch_scc1 L_out_%=\n\t"
-      "s_and_b32 %[t0], %[t1], 15\n\t"
-      "s_lshr_b64 s[60:61], s[60:61], %[t0]\n\t"
-      "s_sub_u32 %[nb], %[nb], %[t0]\n\t"
-      "s_lshr_b32 %[t1], %[t1], 11\n\t"
-      "s_and_b32 %[t0], %[p], %[wm]\n\t"
-      "v_mov_b32 v57, %[t1]\n\t"
-      "v_mad_u32_u24 v58, %[t0], %[vsel], %[vdum]\n\t"
-      "ds_write_b8 v58, v57\n\t"
-      "s_add_u32 %[p], %[p], 1\n\t"
-      "s_sub_u32 %[room], %[room], 1\n\t"
-      "s_branch L_top_%=\n\t"
+      "s_branch L_out_%=\n\t"
+      "L_zero_%=:\n\t"
+      "s_mov_b32 %[why], 0\n\t"
       "L_out_%=:"
       : [nb] "+s"(nb), [room] "+s"(room), [p] "+s"(p), [P] "+s"(P), [why] "=&s"(why), [t0] "=&s"(t0),
         [t1] "=&s"(t1), [t2] "=&s"(t2), "+{s[60:61]}"(bb), "+{s[62:63]}"(qr)
