@@ -314,7 +314,7 @@ def main() -> None:
                 "traffic_unit": "bytes per launch (HBM read+write, PMC)",
                 "traffic_source": traffic_src,
                 "algorithmic_bytes_per_launch": wl.bytes_local,
-                "kernel": "zcrc::crc32_batch_kernel<false, 4u, 0, true, false, 1>",
+                "kernel": "zcrc::crc32_batch_kernel<false, 4u, 0, true, false, 1, 2>",
                 "avg_kernel_ms": round(avg_kernel_ms, 4),
                 "launches_timed": prof.launches,
             },
