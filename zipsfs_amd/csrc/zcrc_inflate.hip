@@ -462,8 +462,9 @@ __device__ __forceinline__ void copy_match(Lds &s, const Out &o, uint32_t p0, ui
 // SALU, VALU and readlane lane selects; the only VALU->SALU edges are
 // v_readlane results.
 __device__ __forceinline__ uint32_t literal_run(Reader &r, uint32_t &p, uint32_t &room, const LLTab &ll,
-                                                uint32_t vsel, uint32_t vdum) {
-  uint32_t why, t0, t1, t2;
+                                                const DTab &dd, uint32_t vsel, uint32_t vdum, uint32_t vdm,
+                                                uint32_t vlane, uint32_t ringl, uint32_t &mlen, uint32_t &mdist) {
+  uint32_t why, t0, t1, t2, t3, t4, t5;
   uint64_t bb = r.bb;
   uint64_t qr = r.q;
   uint32_t nb = r.nb, P = r.P;
@@ -540,17 +541,86 @@ __device__ __forceinline__ uint32_t literal_run(Reader &r, uint32_t &p, uint32_t
       "s_branch L_have_%=\n\t"
       "L_full_%=:\n\t"
       "s_add_u32 %[room], %[room], 1\n\t"
-      "L_gen_%=:\n\t"
+      "L_one_%=:\n\t"
       "s_mov_b32 %[why], 1\n\t"
       "s_branch L_out_%=\n\t"
+      // ---- length/distance pair (t1 = literal/length entry, not a literal).
+      // Everything is checked before a bit is consumed, except the copy
+      // conditions: a pair that decodes but needs the compiled path (far,
+      // long, overlapping, no room, or an error) returns 2 with len/dist.
+      "L_gen_%=:\n\t"
+      "s_bfe_u32 %[t0], %[t1], 0x30004\n\t"
+      "s_cmp_lg_u32 %[t0], 2\n\t"
+      "s_cbranch_scc1 L_one_%=\n\t"  // EOB, long code, bad symbol
+      "s_and_b32 %[t2], %[t1], 15\n\t"  // L
+      "s_bfe_u32 %[t3], %[t1], 0x40007\n\t"  // x (length extra bits)
+      "s_add_u32 %[t4], %[t2], %[t3]\n\t"
+      "s_lshr_b64 s[64:65], s[60:61], %[t4]\n\t"
+      "s_bfe_u32 %[t0], s64, 0x20006\n\t"
+      "s_set_gpr_idx_on %[t0], gpr_idx(SRC0)\n\t"
+      "v_mov_b32 v56, v76\n\t"
+      "s_set_gpr_idx_off\n\t"
+      "v_readlane_b32 %[t5], v56, s64\n\t"  // distance entry
+      "s_bfe_u32 %[t0], %[t5], 0x30004\n\t"
+      "s_cmp_lg_u32 %[t0], 2\n\t"
+      "s_cbranch_scc1 L_one_%=\n\t"  // long or invalid distance code
+      "s_and_b32 %[t0], %[t5], 15\n\t"
+      "s_add_u32 %[t4], %[t4], %[t0]\n\t"  // L + x + dL
+      "s_bfe_u32 %[t0], %[t5], 0x40007\n\t"  // dx
+      "s_add_u32 %[t0], %[t4], %[t0]\n\t"  // c = L + x + dL + dx
+      "s_cmp_gt_u32 %[t0], %[nb]\n\t"
+      "s_cbranch_scc1 L_one_%=\n\t"  // not all buffered (nb 33..35)
+      "s_lshl_b32 %[t3], %[t3], 16\n\t"
+      "s_or_b32 %[t3], %[t3], %[t2]\n\t"
+      "s_bfe_u32 %[t3], s60, %[t3]\n\t"  // length extra value
+      "s_lshr_b32 %[t2], %[t1], 11\n\t"
+      "s_add_u32 %[ml], %[t2], %[t3]\n\t"  // len
+      "s_bfe_u32 %[t3], %[t5], 0x40007\n\t"
+      "s_lshl_b32 %[t3], %[t3], 16\n\t"
+      "s_or_b32 %[t3], %[t3], %[t4]\n\t"
+      "s_bfe_u64 s[64:65], s[60:61], %[t3]\n\t"  // distance extra value
+      "s_lshr_b32 %[t2], %[t5], 11\n\t"
+      "s_add_u32 %[md], %[t2], s64\n\t"  // dist
+      "s_lshr_b64 s[60:61], s[60:61], %[t0]\n\t"
+      "s_sub_u32 %[nb], %[nb], %[t0]\n\t"
+      "s_mov_b32 %[why], 2\n\t"
+      "s_cmp_gt_u32 %[md], %[p]\n\t"  // too far back (or pos >= 2^32): compiled path
+      "s_cbranch_scc1 L_out_%=\n\t"
+      "s_cmp_gt_u32 %[md], %[win]\n\t"  // older than the ring
+      "s_cbranch_scc1 L_out_%=\n\t"
+      "s_cmp_gt_u32 %[ml], 64\n\t"
+      "s_cbranch_scc1 L_out_%=\n\t"
+      "s_cmp_gt_u32 %[ml], %[room]\n\t"
+      "s_cbranch_scc1 L_out_%=\n\t"
+      "s_cmp_lt_u32 %[md], %[ml]\n\t"  // overlapping copy
+      "s_cbranch_scc1 L_out_%=\n\t"
+      // one 64-lane step: ring[p + i] = ring[p - dist + i], i < len
+      "s_sub_u32 %[t2], %[p], %[md]\n\t"
+      "v_add_u32 v59, %[t2], %[vl]\n\t"
+      "v_and_b32 v59, %[wm], v59\n\t"
+      "v_add_u32 v59, %[rl], v59\n\t"
+      "ds_read_u8 v57, v59\n\t"
+      "v_add_u32 v58, %[p], %[vl]\n\t"
+      "v_and_b32 v58, %[wm], v58\n\t"
+      "v_add_u32 v58, %[rl], v58\n\t"
+      "v_cmp_gt_u32 vcc, %[ml], %[vl]\n\t"
+      "s_nop 1\n\t"
+      "v_cndmask_b32 v58, %[vdm], v58, vcc\n\t"
+      "s_waitcnt lgkmcnt(0)\n\t"
+      "ds_write_b8 v58, v57\n\t"
+      "s_add_u32 %[p], %[p], %[ml]\n\t"
+      "s_sub_u32 %[room], %[room], %[ml]\n\t"
+      "s_branch L_top_%=\n\t"
       "L_zero_%=:\n\t"
       "s_mov_b32 %[why], 0\n\t"
       "L_out_%=:"
       : [nb] "+s"(nb), [room] "+s"(room), [p] "+s"(p), [P] "+s"(P), [why] "=&s"(why), [t0] "=&s"(t0),
-        [t1] "=&s"(t1), [t2] "=&s"(t2), "+{s[60:61]}"(bb), "+{s[62:63]}"(qr)
-      : [vdum] "v"(vdum), [vsel] "v"(vsel), [end] "s"(r.end), [ka] "s"(r.kA), [sh8] "s"(r.sh8), [wm] "i"(kWinMask),
-        "{v[40:55]}"(ll), "{v[60:75]}"(r.st)
-      : "memory", "scc", "v56", "v57", "v58", "s64", "s65");
+        [t1] "=&s"(t1), [t2] "=&s"(t2), [t3] "=&s"(t3), [t4] "=&s"(t4), [t5] "=&s"(t5), [ml] "=&s"(mlen),
+        [md] "=&s"(mdist), "+{s[60:61]}"(bb), "+{s[62:63]}"(qr)
+      : [vdum] "v"(vdum), [vsel] "v"(vsel), [vdm] "v"(vdm), [vl] "v"(vlane), [rl] "s"(ringl), [end] "s"(r.end),
+        [ka] "s"(r.kA), [sh8] "s"(r.sh8), [wm] "i"(kWinMask), [win] "i"(kWin), "{v[40:55]}"(ll),
+        "{v[60:75]}"(r.st), "{v[76:79]}"(dd)
+      : "memory", "scc", "vcc", "v56", "v57", "v58", "v59", "s64", "s65");
   r.bb = bb;
   r.q = (uint32_t)qr;
   r.nb = nb;
@@ -567,8 +637,10 @@ __device__ int32_t codes(Lds &s, Reader &r, Out &o, const LLTab &ll, const DTab 
       (__attribute__((address_space(3))) uint8_t *)(&s.ring[0]));
   const uint32_t vsel = lane == 0 ? 1u : 0u;
   const uint32_t vdum = ring_lds + (lane == 0 ? 0u : kDummy + 4u * lane);
+  const uint32_t vdm = ring_lds + kDummy + 4u * lane;
   int32_t st = ZCRC_INFLATE_OK;
   for (;;) {
+    uint32_t len, dist;
     r.slide_if_needed();  // the only slide site of the symbol loop
     if (r.nb <= 32 && !r.refill()) {
       st = ZCRC_INFLATE_ERR_INPUT;
@@ -584,13 +656,19 @@ __device__ int32_t codes(Lds &s, Reader &r, Out &o, const LLTab &ll, const DTab 
       r.nb = uni(r.nb);
       r.P = uni(r.P);
       r.q = uni(r.q);
-      uint32_t room = uni(o.room);
-      const uint32_t why = literal_run(r, p, room, ll, vsel, vdum);
+      uint32_t room = uni(o.room), ml = 0, md = 0;
+      const uint32_t why = literal_run(r, p, room, ll, dd, vsel, vdum, vdm, lane, ring_lds, ml, md);
       o.room = room;
       o.pos += p - p0;
       if (!why) continue;
+      if (why == 2) {  // a pair decoded in asm: checks and copy below
+        len = ml;
+        dist = md;
+        goto have_pair;
+      }
     }
 #endif
+    {
     const uint32_t ix = (uint32_t)r.bb & ((1u << kLLRoot) - 1u);
     uint32_t e = lane_get(ll[ix >> 6], ix);
     ITRACE("[%u] sym P=%u nb=%u e=%x kind=%u len=%u val=%u pos=%llu\n", blockIdx.x, r.P, r.nb, e, e_kind(e),
@@ -622,7 +700,7 @@ __device__ int32_t codes(Lds &s, Reader &r, Out &o, const LLTab &ll, const DTab 
       break;
     }
     r.drop(e_len(e));
-    const uint32_t len = e_val(e) + r.peek(e_extra(e));
+    len = e_val(e) + r.peek(e_extra(e));
     r.drop(e_extra(e));
     if (r.nb <= 32 && !r.refill()) {  // <= 8 bytes past the slide check: still resident
       st = ZCRC_INFLATE_ERR_INPUT;
@@ -636,8 +714,10 @@ __device__ int32_t codes(Lds &s, Reader &r, Out &o, const LLTab &ll, const DTab 
       break;
     }
     r.drop(e_len(d));
-    const uint32_t dist = e_val(d) + r.peek(e_extra(d));
+    dist = e_val(d) + r.peek(e_extra(d));
     r.drop(e_extra(d));
+    }
+  have_pair:
     if (dist > o.pos) {
       st = ZCRC_INFLATE_ERR_DIST;
       break;
