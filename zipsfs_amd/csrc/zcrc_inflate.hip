@@ -468,6 +468,11 @@ __device__ __forceinline__ uint32_t literal_run(Reader &r, uint32_t &p, uint32_t
   uint64_t bb = r.bb;
   uint64_t qr = r.q;
   uint32_t nb = r.nb, P = r.P;
+  // refills the asm may do on its own: each reads the 4 bytes at P (needs
+  // P + 4 <= end) and dword P/4 + 1, resident while P stays in block kA
+  const uint32_t kend = P + 4u <= r.end ? (r.end - P) >> 2 : 0u;
+  const uint32_t kblk = ((r.kA + 1u) * 1024u - P + 3u) >> 2;
+  uint32_t rb = kend < kblk ? kend : kblk;
   asm volatile(
       "L_top_%=:\n\t"
       "s_cmp_le_u32 %[nb], 32\n\t"
@@ -477,8 +482,8 @@ __device__ __forceinline__ uint32_t literal_run(Reader &r, uint32_t &p, uint32_t
       "s_set_gpr_idx_on %[t0], gpr_idx(SRC0)\n\t"
       "v_mov_b32 v56, v40\n\t"
       "s_set_gpr_idx_off\n\t"
-      "s_and_b32 %[t2], %[p], %[wm]\n\t"
-      "v_mad_u32_u24 v58, %[t2], %[vsel], %[vdum]\n\t"
+      "v_and_b32_e64 v58, %[p], %[vwm]\n\t"
+      "v_mad_u32_u24 v58, v58, %[vsel], %[vdum]\n\t"
       "v_readlane_b32 %[t1], v56, s60\n\t"
       "s_cmp_gt_i32 %[t1], -1\n\t"
       "s_cbranch_scc1 L_gen_%=\n\t"
@@ -487,8 +492,7 @@ __device__ __forceinline__ uint32_t literal_run(Reader &r, uint32_t &p, uint32_t
       "s_and_b32 %[t0], %[t1], 15\n\t"
       "s_lshr_b64 s[60:61], s[60:61], %[t0]\n\t"
       "s_sub_u32 %[nb], %[nb], %[t0]\n\t"
-      "s_lshr_b32 %[t1], %[t1], 11\n\t"
-      "v_mov_b32 v57, %[t1]\n\t"
+      "v_lshrrev_b32_e64 v57, 11, %[t1]\n\t"
       "ds_write_b8 v58, v57\n\t"
       "s_add_u32 %[p], %[p], 1\n\t"
       "s_cmp_le_u32 %[nb], 32\n\t"
@@ -497,8 +501,8 @@ __device__ __forceinline__ uint32_t literal_run(Reader &r, uint32_t &p, uint32_t
       "s_set_gpr_idx_on %[t0], gpr_idx(SRC0)\n\t"
       "v_mov_b32 v56, v40\n\t"
       "s_set_gpr_idx_off\n\t"
-      "s_and_b32 %[t2], %[p], %[wm]\n\t"
-      "v_mad_u32_u24 v58, %[t2], %[vsel], %[vdum]\n\t"
+      "v_and_b32_e64 v58, %[p], %[vwm]\n\t"
+      "v_mad_u32_u24 v58, v58, %[vsel], %[vdum]\n\t"
       "v_readlane_b32 %[t1], v56, s60\n\t"
       "s_cmp_gt_i32 %[t1], -1\n\t"
       "s_cbranch_scc1 L_gen_%=\n\t"
@@ -507,25 +511,19 @@ __device__ __forceinline__ uint32_t literal_run(Reader &r, uint32_t &p, uint32_t
       "s_and_b32 %[t0], %[t1], 15\n\t"
       "s_lshr_b64 s[60:61], s[60:61], %[t0]\n\t"
       "s_sub_u32 %[nb], %[nb], %[t0]\n\t"
-      "s_lshr_b32 %[t1], %[t1], 11\n\t"
-      "v_mov_b32 v57, %[t1]\n\t"
+      "v_lshrrev_b32_e64 v57, 11, %[t1]\n\t"
       "ds_write_b8 v58, v57\n\t"
       "s_add_u32 %[p], %[p], 1\n\t"
       "s_branch L_top_%=\n\t"
       // refill 32 bits: exit (0) if past the end or into the next block
       "L_ref_%=:\n\t"
-      "s_add_u32 %[t2], %[P], 4\n\t"
-      "s_cmp_gt_u32 %[t2], %[end]\n\t"
-      "s_cbranch_scc1 L_zero_%=\n\t"
-      "s_lshr_b32 %[t0], %[P], 10\n\t"
-      "s_cmp_lg_u32 %[t0], %[ka]\n\t"
+      "s_sub_u32 %[rb], %[rb], 1\n\t"  // refills left before the end or the next block
       "s_cbranch_scc1 L_zero_%=\n\t"
       "s_lshr_b32 %[t1], %[P], 2\n\t"
-      "s_add_u32 %[t1], %[t1], 1\n\t"
-      "s_lshr_b32 %[t0], %[t1], 6\n\t"
-      "s_and_b32 %[t0], %[t0], 12\n\t"
+      "s_add_u32 %[t1], %[t1], 1\n\t"  // dword g + 1
+      "s_bfe_u32 %[t0], %[t1], 0x20008\n\t"  // its block's slot
       "s_and_b32 %[t2], %[t1], 3\n\t"
-      "s_or_b32 %[t0], %[t0], %[t2]\n\t"
+      "s_lshl2_add_u32 %[t0], %[t0], %[t2]\n\t"  // register 4 * slot + (g + 1) % 4
       "s_lshr_b32 %[t1], %[t1], 2\n\t"
       "s_set_gpr_idx_on %[t0], gpr_idx(SRC0)\n\t"
       "v_mov_b32 v56, v60\n\t"
@@ -614,11 +612,11 @@ __device__ __forceinline__ uint32_t literal_run(Reader &r, uint32_t &p, uint32_t
       "L_zero_%=:\n\t"
       "s_mov_b32 %[why], 0\n\t"
       "L_out_%=:"
-      : [nb] "+s"(nb), [room] "+s"(room), [p] "+s"(p), [P] "+s"(P), [why] "=&s"(why), [t0] "=&s"(t0),
+      : [nb] "+s"(nb), [room] "+s"(room), [p] "+s"(p), [P] "+s"(P), [rb] "+s"(rb), [why] "=&s"(why), [t0] "=&s"(t0),
         [t1] "=&s"(t1), [t2] "=&s"(t2), [t3] "=&s"(t3), [t4] "=&s"(t4), [t5] "=&s"(t5), [ml] "=&s"(mlen),
         [md] "=&s"(mdist), "+{s[60:61]}"(bb), "+{s[62:63]}"(qr)
-      : [vdum] "v"(vdum), [vsel] "v"(vsel), [vdm] "v"(vdm), [vl] "v"(vlane), [rl] "s"(ringl), [end] "s"(r.end),
-        [ka] "s"(r.kA), [sh8] "s"(r.sh8), [wm] "i"(kWinMask), [win] "i"(kWin), "{v[40:55]}"(ll),
+      : [vdum] "v"(vdum), [vsel] "v"(vsel), [vdm] "v"(vdm), [vl] "v"(vlane), [vwm] "v"(kWinMask), [rl] "s"(ringl),
+        [sh8] "s"(r.sh8), [wm] "i"(kWinMask), [win] "i"(kWin), "{v[40:55]}"(ll),
         "{v[60:75]}"(r.st), "{v[76:79]}"(dd)
       : "memory", "scc", "vcc", "v56", "v57", "v58", "v59", "s64", "s65");
   r.bb = bb;
