@@ -111,3 +111,27 @@ def test_inflate_host_batch_with_crc():
     for (name, _, data), (st, out, crc) in zip(items, res):
         assert st == 0 and out == data and crc == zlib.crc32(data), name
     assert res[-2][0] == 1 and res[-1][0] == 7
+
+
+def test_inflate_random_bytes_terminate_like_oracle():
+    """Arbitrary bytes as deflate streams (the adversarial shape: random
+    headers, over-subscribed codes, distances before the start, streams that
+    end anywhere).  Every launch must terminate, and every status (and every
+    output, where one is produced) must equal the oracle's."""
+    import random
+    rnd = random.Random(11)
+    streams, caps = [], []
+    for k in range(3000):
+        n = rnd.choice([1, 2, 3, 5, 8, 16, 40, 100, 600, 4000])
+        b = bytearray(rnd.randrange(256) for _ in range(n))
+        if k % 3 == 0 and n > 2:  # force a fixed or dynamic block header on some
+            b[0] = (b[0] & ~6) | (2 if k % 2 else 4)
+        streams.append(bytes(b))
+        caps.append(rnd.choice([0, 1, 64, 5000, 1 << 16]))
+    st, ol, outs, *_ = _run(streams, caps)
+    want = [o.inflate(s_, c) for s_, c in zip(streams, caps)]
+    for k, (ws, wout, _) in enumerate(want):
+        assert st[k] == ws, (k, z.INFLATE_STATUS[int(st[k])], z.INFLATE_STATUS[ws])
+        if ws == 0:
+            assert outs[k] == wout, k
+    assert sum(1 for w in want if w[0] == 0) >= 5  # a few decode cleanly
