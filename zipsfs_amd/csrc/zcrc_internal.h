@@ -67,7 +67,7 @@ struct InflateArgs {
   uint64_t n;
 };
 constexpr uint64_t kInflateMaxSrc = 0xF0000000ull;  // 32-bit buffer range and block arithmetic
-hipError_t launch_inflate(const InflateArgs &args, hipStream_t stream);
+hipError_t launch_inflate(const InflateArgs &args, int num_cus, hipStream_t stream);
 
 inline uint64_t plan_tiles(uint64_t n) { return n == 0 ? 1 : (n + kPlanTile - 1) / kPlanTile; }
 hipError_t launch_plan(const uint64_t *d_lens, uint64_t n, uint64_t *d_prefix, uint64_t *d_tile_sum,

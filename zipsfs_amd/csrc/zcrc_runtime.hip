@@ -628,7 +628,7 @@ int zcrc_inflate_batch_device(const void *const *d_src, const uint64_t *d_src_le
   a.out_len = d_out_len;
   a.status = d_status;
   a.n = n;
-  ZCRC_HIP_TRY(launch_inflate(a, static_cast<hipStream_t>(stream)));
+  ZCRC_HIP_TRY(launch_inflate(a, dc->num_cus, static_cast<hipStream_t>(stream)));
   return ZCRC_OK;
 }
 
