@@ -152,7 +152,7 @@ def wave_ranges(batch: Batch, num_cus: int, dyn_shift: int = K_DYN_SHIFT, unit: 
     crc32_batch_kernel).  Which wave claims a unit does not matter for the
     result, so the model lists them in order."""
     total = batch.total
-    want = max(1, (total + K_MIN_RANGE - 1) // K_MIN_RANGE)
+    want = max(1, (total + K_MIN_RANGE - 1) // K_MIN_RANGE, batch.n)
     W = min(want, num_cus * K_WAVES)
     if dyn_shift == K_DYN_AUTO:
         dyn_shift = 1 if batch.n and total // batch.n < K_DYN_SMALL_AVG else 2

@@ -27,6 +27,24 @@ def test_library_exports_header_symbols():
     assert set(names) <= exported
 
 
+def test_hip_symbols_resolve_against_torch_runtime():
+    """libzcrc is loaded next to PyTorch's bundled libamdhip64 (ROCm 7.0):
+    every versioned HIP symbol it imports must exist there (a hip_7.1-only
+    call made the library fail to load on the GPU box)."""
+    import re
+    torch = pytest.importorskip("torch")
+    hip = os.path.join(os.path.dirname(torch.__file__), "lib", "libamdhip64.so")
+    if not os.path.exists(hip):
+        pytest.skip("no bundled libamdhip64")
+    need = subprocess.run(["objdump", "-T", _lib.LIB_PATH], capture_output=True, text=True, check=True).stdout
+    have = subprocess.run(["objdump", "-T", hip], capture_output=True, text=True, check=True).stdout
+    have_syms = {(m.group(1), m.group(2)) for m in re.finditer(r"\(?(hip_[0-9.]+)\)?\s+(\w+)$", have, re.M)}
+    und = list(re.finditer(r"\*UND\*\s+\S+\s+\(?(hip_[0-9.]+)\)?\s+(\w+)$", need, re.M))
+    assert len(und) > 10, "objdump format not understood"
+    for m in und:
+        assert (m.group(1), m.group(2)) in have_syms, f"{m.group(2)}@{m.group(1)} missing from torch's HIP runtime"
+
+
 def test_combine_matches_zlib():
     rnd = random.Random(1)
     for _ in range(200):

@@ -248,6 +248,40 @@ def test_dynamic_part_mixed_batches(shape):
     del host
 
 
+def test_fused_plan_back_to_back_vs_two_launch_path():
+    """zcrc32_batch_device scans the lengths inside the CRC kernel for
+    batches of <= 8192 buffers (workgroup 0 publishes the prefix with a
+    per-launch epoch; zcrc_batch_kernel.h fused_plan).  Many launches queued
+    back to back on one stream, each with different lengths, pool-recycled
+    scratch and the dynamic work counter, must equal the graph-safe
+    two-launch path (zcrc32_batch_device_ws) and the oracle."""
+    rnd = random.Random(31)
+    total = 96 << 20
+    mem = torch.randint(0, 256, (total,), dtype=torch.uint8, device=DEV)
+    host = mem.cpu().numpy()
+    cases = []
+    for n in [1, 2, 63, 64, 1000, 8191, 8192, 8193, 20000] + [rnd.randint(1, 8192) for _ in range(23)]:
+        cap = total // n - 64
+        lens = [min(cap, rnd.choice([0, rnd.randint(1, 100), rnd.randint(100, 70_000),
+                                     rnd.randint(0, 600_000)])) for _ in range(n)]
+        offs = [rnd.randrange(0, total - L) for L in lens]
+        ptrs = torch.tensor([mem.data_ptr() + q for q in offs], dtype=torch.int64, device=DEV)
+        lt = torch.tensor(lens, dtype=torch.int64, device=DEV)
+        cases.append((offs, lens, ptrs, lt))
+    outs = [z.crc32_batch_device(ptrs, lt) for (_, _, ptrs, lt) in cases]  # no sync in between
+    ws = []
+    for (_, lens, ptrs, lt) in cases:
+        scratch = torch.empty(z.scratch_bytes(len(lens)), dtype=torch.uint8, device=DEV)
+        ws.append(z.crc32_batch_device_ws(ptrs, lt, scratch))
+    torch.cuda.synchronize()
+    for k, ((offs, lens, _, _), a, b) in enumerate(zip(cases, outs, ws)):
+        ga, gb = u32(a), u32(b)
+        np.testing.assert_array_equal(ga, gb, err_msg=f"case {k} n={len(lens)}")
+        ap = np.array([host.ctypes.data + q for q in offs], dtype=np.uint64)
+        exp = o.crc32_batch(ap, np.array(lens, dtype=np.uint64), np.zeros(len(lens), dtype=np.uint32), nthreads=8)
+        np.testing.assert_array_equal(ga, exp, err_msg=f"case {k} n={len(lens)}")
+
+
 def test_strided_api_seeds_and_stride():
     n, L, stride = 300, 200_000, 200_064
     mem, ptrs, lens = _strided_fill(n, L, stride=stride, index0=1000)

@@ -150,14 +150,31 @@ int main(int argc, char **argv) {
     a.dyn_unit = unit;
     const uint64_t nw = (uint64_t)cus * kWaves;
     uint64_t *dst;
-    CHECK(hipMalloc(&dst, nw * 32));
-    CHECK(hipMemset(dst, 0, nw * 32));
+    CHECK(hipMalloc(&dst, nw * 64));
+    CHECK(hipMemset(dst, 0, nw * 64));
     CHECK(hipMemset(d_counter, 0, 32));
     a.stamps = dst;
     hipLaunchKernelGGL(k, dim3(cus), dim3(kThreads), 0, 0, a);
     CHECK(hipDeviceSynchronize());
-    std::vector<uint64_t> st(nw * 4);
-    CHECK(hipMemcpy(st.data(), dst, nw * 32, hipMemcpyDeviceToHost));
+    std::vector<uint64_t> st8(nw * 8), st(nw * 4);
+    CHECK(hipMemcpy(st8.data(), dst, nw * 64, hipMemcpyDeviceToHost));
+    for (uint64_t w = 0; w < nw; w++)
+      for (int k = 0; k < 4; k++) st[4 * w + k] = st8[8 * w + k];
+    {  // prologue: kernel entry -> range search done -> LDS written + barrier
+      uint64_t e0 = ~0ull, e1 = 0, b0 = ~0ull;
+      std::vector<double> fill, srch;  // search (table loads in flight), then LDS writes + barrier
+      for (uint64_t w = 0; w < nw; w++)
+        if (st8[8 * w + 1]) {
+          e0 = std::min(e0, st8[8 * w + 4]), e1 = std::max(e1, st8[8 * w + 4]), b0 = std::min(b0, st8[8 * w]);
+          srch.push_back((st8[8 * w + 5] - st8[8 * w + 4]) * 1e-2);
+          fill.push_back((st8[8 * w + 0] - st8[8 * w + 5]) * 1e-2);
+        }
+      std::sort(fill.begin(), fill.end());
+      std::sort(srch.begin(), srch.end());
+      printf("prologue %-8s entry spread %.1f us | first entry->first begin %.1f us | search us p50 %.1f p100 %.1f | "
+             "LDS fill us p50 %.1f p100 %.1f\n", name, (e1 - e0) * 1e-2, (b0 - e0) * 1e-2, srch[srch.size() / 2],
+             srch.back(), fill[fill.size() / 2], fill.back());
+    }
     uint64_t t0 = ~0ull, t1 = 0;
     for (uint64_t w = 0; w < nw; w++)
       if (st[4 * w + 1]) t0 = std::min(t0, st[4 * w]), t1 = std::max(t1, st[4 * w + 1]);

@@ -244,6 +244,87 @@ struct BatchView {
   }
 };
 
+// ------------------------------------------------------------ plan scan
+// Exclusive prefix helpers for the plan (zcrc_kernels.hip) and the fused plan.
+
+__device__ __forceinline__ uint64_t wave_incl_scan(uint64_t v) {
+  const uint32_t lane = threadIdx.x & 63u;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint64_t o = __shfl_up(v, d, 64);
+    if (lane >= (uint32_t)d) v += o;
+  }
+  return v;
+}
+
+__device__ uint64_t block_excl_scan(uint64_t v, uint64_t *s_tmp /* 16 */, uint64_t *total) {
+  const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+  const uint64_t inc = wave_incl_scan(v);
+  if (lane == 63) s_tmp[wv] = inc;
+  __syncthreads();
+  uint64_t off = 0, tot = 0;
+  for (uint32_t k = 0; k < blockDim.x / 64; k++) {
+    const uint64_t s = s_tmp[k];
+    if (k < wv) off += s;
+    tot += s;
+  }
+  __syncthreads();
+  *total = tot;
+  return off + inc - v;
+}
+
+// Fused plan (BatchArgs::plan_lens set; pointer form, n <= kPlanTile):
+// workgroup 0 writes prefix[0..n], zeroes out[] and the work counter, then
+// publishes plan_epoch at *plan_flag with an agent-scope release; the other
+// workgroups poll the flag (one lane each) and acquire.  Workgroup 0 is
+// dispatched first and waits for nobody, so the wait needs no co-residency.
+// Saves the plan launch and the dependent-launch gap (~15 us per call for
+// config 2).  The poll is bounded: a flag that never arrives traps (a HIP
+// error at the next synchronisation) instead of hanging the device.
+__device__ __forceinline__ void fused_plan(const BatchArgs &args, uint32_t *s_lds) {
+  const uint32_t tid = threadIdx.x;
+  if (blockIdx.x == 0) {
+    uint64_t *prefix = const_cast<uint64_t *>(args.prefix);
+    const uint64_t n = args.n;
+    uint64_t v[kPlanPerThread];
+    uint64_t acc = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < kPlanPerThread; k++) {
+      const uint64_t idx = (uint64_t)tid * kPlanPerThread + k;
+      v[k] = idx < n ? args.plan_lens[idx] : 0;
+      if (idx < n) args.out[idx] = 0u;
+      acc += v[k];
+    }
+    uint64_t tot;
+    uint64_t run = block_excl_scan(acc, reinterpret_cast<uint64_t *>(s_lds), &tot);
+#pragma unroll
+    for (uint32_t k = 0; k < kPlanPerThread; k++) {
+      const uint64_t idx = (uint64_t)tid * kPlanPerThread + k;
+      if (idx < n) prefix[idx] = run;
+      run += v[k];
+      if (idx + 1 == n) prefix[n] = run;
+    }
+    if (tid == 0 && args.ctr) *args.ctr = 0u;
+    __syncthreads();
+    if (tid == 0) __hip_atomic_store(args.plan_flag, args.plan_epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+  } else {
+    if (tid == 0) {
+      uint32_t polls = 0;
+      while (__hip_atomic_load(args.plan_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != args.plan_epoch) {
+        __builtin_amdgcn_s_sleep(2);
+        if (++polls == (1u << 26)) __builtin_trap();
+      }
+    }
+    __syncthreads();
+  }
+  // No agent-scope acquire (buffer_inv sc1): issued by every wave it
+  // invalidated the XCD's L2 4096 times per launch (+32 us on config 2).
+  // None is needed: the dispatch itself invalidates L1/L2 at kernel start,
+  // no wave touches a prefix/out line before the flag, and the writer's
+  // release wrote its L2 back, so the first read of each line misses to
+  // memory and sees the plan.
+}
+
 // ------------------------------------------------------------ the kernel
 
 // kD: 1 KiB blocks per register group (two groups in flight); kAblate != 0
@@ -430,36 +511,44 @@ template <bool kStrided, uint32_t kD = kDepth, int kAblate = 0, bool kRotate = t
           int kPrio = 1, int kAux = kLoadNt>
 __global__ __launch_bounds__(kThreads) void crc32_batch_kernel(BatchArgs args) {
   __shared__ __attribute__((aligned(16))) uint32_t s_lds[kLdsBytes / 4];
-  const BatchView<kStrided> bv{args};
   const TableBlob *tab = args.tab;
+  const uint64_t t_entry = kStamp ? __builtin_amdgcn_s_memrealtime() : 0;
 
+  // ---- prologue: the table loads are issued first; the plan (fused form)
+  // and the wave's range search run while they are in flight; the LDS
+  // writes and the barrier come last.  (Fill, then search, measured 4.2 +
+  // 3.4 us of a 53 us config-2 launch: tools/crc_variants stamps.)
+  // LDS byte o of the braided area holds braid[j][v] with j = 2 * (o >> 16)
+  // + ((o >> 7) & 1), v = (o >> 8) & 255 (32 replicas of each entry, 4 B
+  // apart).  Thread t writes the 16-B chunks t + 1024 k, so a wave's writes
+  // are consecutive (writing one entry's 128 B per lane put every lane on
+  // the same banks: 3.6 us of bank conflicts per launch).
+  const uint32_t tid = threadIdx.x;
+  uint32_t braid_val[8];
+#pragma unroll
+  for (int k = 0; k < 8; k++) {
+    const uint32_t o = 16u * (tid + 1024u * k);
+    braid_val[k] = tab->braid[(((o >> 16) << 1) | ((o >> 7) & 1u)) * 256u + ((o >> 8) & 255u)];
+  }
+  const uint4 *comb_src = reinterpret_cast<const uint4 *>(tab->comb);
+  const uint4 comb0 = comb_src[tid], comb1 = comb_src[tid + 1024u];
+
+  if (!kStrided && args.plan_lens) fused_plan(args, s_lds);
+  const BatchView<kStrided> bv{args};
   const uint64_t total = bv.total();
   const uint64_t max_waves = (uint64_t)gridDim.x * kWaves;
   const uint64_t min_range = args.min_range ? args.min_range : kMinRange;
   uint64_t want = (total + min_range - 1) / min_range;
+  // many small buffers: at least a wave per buffer -- per-buffer latency,
+  // not bytes, bounds them (4096 x 64 B took 1.8 ms on the 4 waves that
+  // 256 KiB asks for by bytes; tools/host_overhead.py)
+  if (want < args.n) want = args.n;
   if (want < 1) want = 1;
   const uint64_t W = want < max_waves ? want : max_waves;
   if ((uint64_t)blockIdx.x * kWaves >= W) return;  // whole workgroup idle (uniform)
 
-  // ---- LDS fill: braided table x32 replicas + 8 combine tables ----------
-  {
-    const uint32_t tid = threadIdx.x;  // 0..1023 = (table j, byte v)
-    const uint32_t j = tid >> 8, v = tid & 255u;
-    const uint32_t val = tab->braid[tid];
-    const uint4 q = make_uint4(val, val, val, val);
-    char *dst = reinterpret_cast<char *>(s_lds) + (j >> 1) * 65536u + v * 256u + (j & 1u) * 128u;
-#pragma unroll
-    for (int r = 0; r < 8; r++) *reinterpret_cast<uint4 *>(dst + 16 * r) = q;
-    const uint4 *src = reinterpret_cast<const uint4 *>(tab->comb) + tid * 2;
-    uint4 *cdst = reinterpret_cast<uint4 *>(s_lds + kLdsCombDword) + tid * 2;
-    cdst[0] = src[0];
-    cdst[1] = src[1];
-  }
-  __syncthreads();
-
   const uint32_t lane = threadIdx.x & 63u;
   const uint64_t w = (uint64_t)blockIdx.x * kWaves + (threadIdx.x >> 6);
-  if (w >= W) return;  // no barrier after this point
 
   // Static part: the first Ts = total - Td bytes in W equal snapped ranges,
   // issue priority banded by progress (kPrio).  Dynamic part: the last
@@ -482,9 +571,24 @@ __global__ __launch_bounds__(kThreads) void crc32_batch_kernel(BatchArgs args) {
   // nominal boundary of wave k: floor(k * Ts / W), without 128-bit math
   const uint64_t q_tot = Ts / W, r_tot = Ts % W;
   bool last = (w + 1 == W) && !Td;
-  uint64_t S0, S1, lb0, lb1;
-  bv.range(q_tot * w + (r_tot * w) / W, (w + 1 == W) ? Ts : q_tot * (w + 1) + (r_tot * (w + 1)) / W, last, S0,
-           S1, lb0, lb1);
+  uint64_t S0 = 0, S1 = 0, lb0 = 0, lb1 = 0;
+  if (w < W)
+    bv.range(q_tot * w + (r_tot * w) / W, (w + 1 == W) ? Ts : q_tot * (w + 1) + (r_tot * (w + 1)) / W, last, S0,
+             S1, lb0, lb1);
+  const uint64_t t_search = kStamp ? __builtin_amdgcn_s_memrealtime() : 0;
+
+  // ---- LDS: braided table x32 replicas + 8 combine tables ---------------
+  {
+    uint4 *dst = reinterpret_cast<uint4 *>(s_lds);
+#pragma unroll
+    for (int k = 0; k < 8; k++)
+      dst[tid + 1024u * k] = make_uint4(braid_val[k], braid_val[k], braid_val[k], braid_val[k]);
+    uint4 *cdst = reinterpret_cast<uint4 *>(s_lds + kLdsCombDword);
+    cdst[tid] = comb0;
+    cdst[tid + 1024u] = comb1;
+  }
+  __syncthreads();
+  if (w >= W) return;  // no barrier after this point
   bool band = true;
 
   // diagnostic build: wall-clock stamps (s_memrealtime, 100 MHz) per wave
@@ -519,10 +623,12 @@ __global__ __launch_bounds__(kThreads) void crc32_batch_kernel(BatchArgs args) {
     band = false;
   }
   if (kStamp && lane == 0) {
-    args.stamps[4 * w + 0] = t_begin;
-    args.stamps[4 * w + 1] = __builtin_amdgcn_s_memrealtime();
-    args.stamps[4 * w + 2] = npieces;
-    args.stamps[4 * w + 3] = static_bytes;
+    args.stamps[8 * w + 0] = t_begin;
+    args.stamps[8 * w + 1] = __builtin_amdgcn_s_memrealtime();
+    args.stamps[8 * w + 2] = npieces;
+    args.stamps[8 * w + 3] = static_bytes;
+    args.stamps[8 * w + 4] = t_entry;
+    args.stamps[8 * w + 5] = t_search;
   }
 }
 

@@ -46,16 +46,24 @@ struct BatchArgs {
   uint64_t n;
   const TableBlob *tab;
   uint64_t min_range;  // bytes per wave at least (0 = kMinRange)
-  uint64_t *stamps;    // diagnostic builds only (kStamp): 4 words per wave
+  uint64_t *stamps;    // diagnostic builds only (kStamp): 8 words per wave
   // dynamic part: the last total >> dyn_shift bytes are handed out in units
   // of dyn_unit bytes (0 = kDynUnit) through *ctr, which must be zero at
   // launch; ctr == nullptr or dyn_shift == 0 -> purely static partition
   uint32_t *ctr;
   uint32_t dyn_shift;
   uint64_t dyn_unit;
+  // fused plan (pointer form, n <= kPlanTile; crc32_batch_kernel's
+  // fused_plan): lengths to scan into prefix (writable), the flag that
+  // publishes it and this launch's unique epoch.  nullptr: prefix is ready.
+  const uint64_t *plan_lens;
+  uint64_t *plan_flag;
+  uint64_t plan_epoch;
 };
 
-hipError_t launch_batch(const BatchArgs &args, bool strided, int num_cus, hipStream_t stream);
+// t0/t1: optional events stamped with the kernel's own start and end
+hipError_t launch_batch(const BatchArgs &args, bool strided, int num_cus, hipStream_t stream,
+                        hipEvent_t t0 = nullptr, hipEvent_t t1 = nullptr);
 // batched raw-DEFLATE decode (zcrc_inflate.hip): device arrays of n
 struct InflateArgs {
   const uint8_t *const *src;

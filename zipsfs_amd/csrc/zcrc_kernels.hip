@@ -1,6 +1,7 @@
 // zcrc_kernels.hip -- instantiations of the batched CRC-32 kernel, the plan
 // (prefix-scan) kernels and their launchers.  The kernel itself lives in
 // zcrc_batch_kernel.h (shared with the measurement tools under tools/).
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -12,31 +13,7 @@ namespace zcrc {
 // Exclusive prefix over lengths: prefix[0..n] (prefix[n] = total), and zero
 // out[] (split pieces xor into it).  Tile = kPlanTile buffers per workgroup.
 
-__device__ __forceinline__ uint64_t wave_incl_scan(uint64_t v) {
-  const uint32_t lane = threadIdx.x & 63u;
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    const uint64_t o = __shfl_up(v, d, 64);
-    if (lane >= (uint32_t)d) v += o;
-  }
-  return v;
-}
-
-__device__ uint64_t block_excl_scan(uint64_t v, uint64_t *s_tmp /* 16 */, uint64_t *total) {
-  const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
-  const uint64_t inc = wave_incl_scan(v);
-  if (lane == 63) s_tmp[wv] = inc;
-  __syncthreads();
-  uint64_t off = 0, tot = 0;
-  for (uint32_t k = 0; k < blockDim.x / 64; k++) {
-    const uint64_t s = s_tmp[k];
-    if (k < wv) off += s;
-    tot += s;
-  }
-  __syncthreads();
-  *total = tot;
-  return off + inc - v;
-}
+// wave_incl_scan / block_excl_scan: zcrc_batch_kernel.h (the fused plan uses them too)
 
 __global__ __launch_bounds__(1024) void plan_tile_sums(const uint64_t *lens, uint64_t n, uint64_t *tile_sum,
                                                        uint32_t *out) {
@@ -93,12 +70,15 @@ __global__ __launch_bounds__(1024) void plan_tile_scan(const uint64_t *lens, uin
 
 // ------------------------------------------------------------ launchers
 
-hipError_t launch_batch(const BatchArgs &args, bool strided, int num_cus, hipStream_t stream) {
+hipError_t launch_batch(const BatchArgs &args, bool strided, int num_cus, hipStream_t stream, hipEvent_t t0,
+                        hipEvent_t t1) {
   const dim3 grid((unsigned)num_cus), block(kThreads);
+  // t0/t1 (profiling): timestamps carried by the dispatch packet itself --
+  // event records around the launch add ~11 us of queue bubbles per launch
   if (strided)
-    hipLaunchKernelGGL((crc32_batch_kernel<true, kDepth, 0>), grid, block, 0, stream, args);
+    hipExtLaunchKernelGGL((crc32_batch_kernel<true, kDepth, 0>), grid, block, 0, stream, t0, t1, 0, args);
   else
-    hipLaunchKernelGGL((crc32_batch_kernel<false, kDepth, 0>), grid, block, 0, stream, args);
+    hipExtLaunchKernelGGL((crc32_batch_kernel<false, kDepth, 0>), grid, block, 0, stream, t0, t1, 0, args);
   return hipGetLastError();
 }
 

@@ -14,6 +14,7 @@
 #include <algorithm>
 #include <atomic>
 #include <condition_variable>
+#include <map>
 #include <mutex>
 #include <new>
 #include <string>
@@ -111,6 +112,7 @@ int device_ctx(DeviceCtx **out) {
 std::atomic<int> g_prof_on{0};
 std::mutex g_prof_mu;
 std::vector<std::pair<hipEvent_t, hipEvent_t>> g_prof_pending;
+std::vector<hipEvent_t> g_prof_free;  // recycled: no hipEventCreate per launch
 double g_prof_ms = 0.0;
 int g_prof_count = 0;
 
@@ -118,13 +120,16 @@ int launch_main(const BatchArgs &args, bool strided, const DeviceCtx &dc, hipStr
   hipEvent_t e0 = nullptr, e1 = nullptr;
   const bool prof = g_prof_on.load(std::memory_order_relaxed) != 0;
   if (prof) {
-    ZCRC_HIP_TRY(hipEventCreate(&e0));
-    ZCRC_HIP_TRY(hipEventCreate(&e1));
-    ZCRC_HIP_TRY(hipEventRecord(e0, stream));
+    {
+      std::lock_guard<std::mutex> lk(g_prof_mu);
+      if (!g_prof_free.empty()) e0 = g_prof_free.back(), g_prof_free.pop_back();
+      if (!g_prof_free.empty()) e1 = g_prof_free.back(), g_prof_free.pop_back();
+    }
+    if (!e0) ZCRC_HIP_TRY(hipEventCreate(&e0));
+    if (!e1) ZCRC_HIP_TRY(hipEventCreate(&e1));
   }
-  ZCRC_HIP_TRY(launch_batch(args, strided, dc.num_cus, stream));
+  ZCRC_HIP_TRY(launch_batch(args, strided, dc.num_cus, stream, e0, e1));
   if (prof) {
-    ZCRC_HIP_TRY(hipEventRecord(e1, stream));
     std::lock_guard<std::mutex> lk(g_prof_mu);
     g_prof_pending.emplace_back(e0, e1);
   }
@@ -133,22 +138,42 @@ int launch_main(const BatchArgs &args, bool strided, const DeviceCtx &dc, hipStr
 
 // ------------------------------------------------------------- device batch
 
+// Epochs of fused-plan launches: unique per launch in this process and far
+// from the small integers stale scratch tends to hold (splitmix64 of a counter).
+uint64_t next_plan_epoch() {
+  static std::atomic<uint64_t> ctr{0};
+  uint64_t z = ctr.fetch_add(1, std::memory_order_relaxed) + 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return (z ^ (z >> 31)) | 1u;
+}
+
+// fuse: batches of <= kPlanTile buffers scan their lengths inside the CRC
+// kernel (one launch instead of two).  Not for zcrc32_batch_device_ws: a
+// captured graph would replay one epoch, and the flag must change per launch.
 int batch_device_ws(const void *const *d_ptrs, const uint64_t *d_lens, const uint32_t *d_seeds,
-                    uint32_t *d_out, size_t n, void *scratch, size_t scratch_bytes, hipStream_t stream) {
+                    uint32_t *d_out, size_t n, void *scratch, size_t scratch_bytes, hipStream_t stream,
+                    bool fuse) {
   if (n == 0) return ZCRC_OK;
   if (!d_ptrs || !d_lens || !d_out || !scratch) return fail(ZCRC_ERR_ARG, "null argument");
   if (scratch_bytes < zcrc32_batch_device_scratch_bytes(n)) return fail(ZCRC_ERR_ARG, "scratch too small");
   DeviceCtx *dc = nullptr;
   int rc = device_ctx(&dc);
   if (rc) return rc;
-  // scratch: work counter (own kCtrBytes line, zeroed by the plan) |
-  // prefix[n+1] | tile sums.  The counter must not share a cache line with
+  // scratch: work counter (zeroed by the plan) and, 128 B further, the fused
+  // plan's flag (own kCtrBytes area) | prefix[n+1] | tile sums.  The counter must not share a cache line with
   // the prefix, which every wave reads while claims hammer the counter.
   uint32_t *d_ctr = static_cast<uint32_t *>(scratch);
   uint64_t *d_prefix = reinterpret_cast<uint64_t *>(static_cast<uint8_t *>(scratch) + kCtrBytes);
   uint64_t *d_tiles = d_prefix + (n + 1);
-  ZCRC_HIP_TRY(launch_plan(d_lens, n, d_prefix, d_tiles, d_out, d_ctr, stream));
   BatchArgs a{};
+  if (fuse && n <= kPlanTile) {
+    a.plan_lens = d_lens;
+    a.plan_flag = reinterpret_cast<uint64_t *>(static_cast<uint8_t *>(scratch) + kCtrBytes / 2);
+    a.plan_epoch = next_plan_epoch();
+  } else {
+    ZCRC_HIP_TRY(launch_plan(d_lens, n, d_prefix, d_tiles, d_out, d_ctr, stream));
+  }
   a.ptrs = reinterpret_cast<const uint8_t *const *>(d_ptrs);
   a.prefix = d_prefix;
   a.seeds = d_seeds;
@@ -550,7 +575,7 @@ size_t zcrc32_batch_device_scratch_bytes(size_t n) { return 8 * (n + 1) + 8 * zc
 int zcrc32_batch_device_ws(const void *const *d_ptrs, const uint64_t *d_lens, const uint32_t *d_seeds_or_null,
                            uint32_t *d_out, size_t n, void *d_scratch, size_t scratch_bytes, void *stream) {
   return batch_device_ws(d_ptrs, d_lens, d_seeds_or_null, d_out, n, d_scratch, scratch_bytes,
-                         static_cast<hipStream_t>(stream));
+                         static_cast<hipStream_t>(stream), false);
 }
 
 int zcrc32_batch_device(const void *const *d_ptrs, const uint64_t *d_lens, const uint32_t *d_seeds_or_null,
@@ -559,13 +584,49 @@ int zcrc32_batch_device(const void *const *d_ptrs, const uint64_t *d_lens, const
   if (!d_ptrs || !d_lens || !d_out) return fail(ZCRC_ERR_ARG, "null argument");
   hipStream_t st = static_cast<hipStream_t>(stream);
   const size_t bytes = zcrc32_batch_device_scratch_bytes(n);
-  void *scratch = nullptr;
-  ZCRC_HIP_TRY(hipMallocAsync(&scratch, bytes, st));
-  const int rc = batch_device_ws(d_ptrs, d_lens, d_seeds_or_null, d_out, n, scratch, bytes, st);
-  const hipError_t e = hipFreeAsync(scratch, st);
-  if (rc) return rc;
-  if (e != hipSuccess) return fail(ZCRC_ERR_HIP, std::string("hipFreeAsync: ") + hipGetErrorString(e));
-  return ZCRC_OK;
+  hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+  ZCRC_HIP_TRY(hipStreamIsCapturing(st, &cap));
+  if (cap != hipStreamCaptureStatusNone) {
+    // inside graph capture: stream-ordered scratch, two-launch plan (a
+    // replayed graph cannot hand the fused plan a fresh epoch)
+    void *scratch = nullptr;
+    ZCRC_HIP_TRY(hipMallocAsync(&scratch, bytes, st));
+    const int rc = batch_device_ws(d_ptrs, d_lens, d_seeds_or_null, d_out, n, scratch, bytes, st, false);
+    const hipError_t e = hipFreeAsync(scratch, st);
+    if (rc) return rc;
+    if (e != hipSuccess) return fail(ZCRC_ERR_HIP, std::string("hipFreeAsync: ") + hipGetErrorString(e));
+    return ZCRC_OK;
+  }
+  // Eager calls reuse a grow-only scratch per (device, stream): launches on
+  // one stream run in order, so one buffer serves them all.  A
+  // hipMallocAsync/hipFreeAsync pair per call blocked the host until the
+  // previous launch had finished (tools/host_overhead.py: 56 us of host time
+  // per config-2 call, 11 us with reused scratch), so back-to-back calls
+  // could not queue.  The lock is held across the launch so that a growth
+  // never frees a buffer another thread is about to launch with.
+  // Keyed by the stream handle: a destroyed stream's object lives on until
+  // its queued work completes (commands hold references to it), so a
+  // handle cannot come back for a new stream while a launch that used its
+  // scratch is still pending.  (hipStreamGetId would be cleaner but is
+  // newer than the HIP runtime PyTorch ships.)
+  static std::mutex mu;
+  static std::map<std::pair<int, hipStream_t>, std::pair<void *, size_t>> cache;
+  int dev = 0;
+  ZCRC_HIP_TRY(hipGetDevice(&dev));
+  std::lock_guard<std::mutex> lk(mu);
+  auto &slot = cache[{dev, st}];
+  if (slot.second < bytes) {
+    if (slot.first) {  // rare: a bigger batch than any before on this stream
+      ZCRC_HIP_TRY(hipStreamSynchronize(st));
+      ZCRC_HIP_TRY(hipFree(slot.first));
+      slot = {nullptr, 0};
+    }
+    const size_t nb = std::max<size_t>(bytes, 64u << 10);
+    ZCRC_HIP_TRY(hipMalloc(&slot.first, nb));
+    ZCRC_HIP_TRY(hipMemset(slot.first, 0, nb));
+    slot.second = nb;
+  }
+  return batch_device_ws(d_ptrs, d_lens, d_seeds_or_null, d_out, n, slot.first, slot.second, st, true);
 }
 
 int zcrc32_batch_device_strided(const void *d_base, uint64_t stride, uint64_t len, size_t n,
@@ -824,8 +885,8 @@ int zcrc_profile_read(double *total_ms, int *launches) {
     if (e != hipSuccess) return fail(ZCRC_ERR_HIP, std::string("profile elapsed: ") + hipGetErrorString(e));
     g_prof_ms += ms;
     g_prof_count++;
-    (void)hipEventDestroy(p.first);
-    (void)hipEventDestroy(p.second);
+    g_prof_free.push_back(p.first);
+    g_prof_free.push_back(p.second);
   }
   g_prof_pending.clear();
   if (total_ms) *total_ms = g_prof_ms;
