@@ -29,5 +29,5 @@ timeout -k 10 400 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ
 
 python3 tools/pmc_summary.py "$W/kt" "$W/fetch" "$W/write" "$W/sq" "$OUT/pmc_summary_config${CFG}.json" > /dev/null
 cp "$(find "$W/kt" -name '*kernel_stats.csv' | head -1)" "$OUT/rocprof_kernel_stats_config${CFG}.csv"
-tail -1 "$W/kt.log" > "$OUT/rocprof_bench_config${CFG}.jsonl"
+grep '^{"metric"' "$W/kt.log" | tail -1 > "$OUT/rocprof_bench_config${CFG}.jsonl"
 echo "profiles for config $CFG in $OUT"
