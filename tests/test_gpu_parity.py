@@ -282,6 +282,41 @@ def test_fused_plan_back_to_back_vs_two_launch_path():
         np.testing.assert_array_equal(ga, exp, err_msg=f"case {k} n={len(lens)}")
 
 
+def test_graph_capture_replays_with_new_data():
+    """Both device entry points captured in a HIP graph (torch.cuda.graph)
+    and replayed after the payload and lengths change in place: every replay
+    must checksum the current bytes.  zcrc32_batch_device switches to
+    stream-ordered scratch and the two-launch plan under capture (a fused
+    plan's epoch would be frozen into the graph); zcrc32_batch_device_ws
+    always uses the two-launch plan."""
+    rnd = random.Random(5)
+    n, cap = 3000, 20_000
+    mem = torch.zeros(n * cap, dtype=torch.uint8, device=DEV)
+    ptrs = mem.data_ptr() + torch.arange(n, dtype=torch.int64, device=DEV) * cap
+    lens = torch.zeros(n, dtype=torch.int64, device=DEV)
+    out_a = torch.empty(n, dtype=torch.int32, device=DEV)
+    out_b = torch.empty(n, dtype=torch.int32, device=DEV)
+    scratch = torch.empty(z.scratch_bytes(n), dtype=torch.uint8, device=DEV)
+    z.crc32_batch_device(ptrs, lens, out=out_a)  # warm-up outside capture
+    z.crc32_batch_device_ws(ptrs, lens, scratch, out=out_b)
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        z.crc32_batch_device(ptrs, lens, out=out_a)
+        z.crc32_batch_device_ws(ptrs, lens, scratch, out=out_b)
+    for rep in range(3):
+        ln = [rnd.choice([0, rnd.randint(1, 64), rnd.randint(64, cap)]) for _ in range(n)]
+        lens.copy_(torch.tensor(ln, dtype=torch.int64))
+        mem.copy_(torch.randint(0, 256, (n * cap,), dtype=torch.uint8, device=DEV))
+        g.replay()
+        torch.cuda.synchronize()
+        host = mem.cpu().numpy()
+        exp = o.crc32_batch(host.ctypes.data + np.arange(n, dtype=np.uint64) * cap, np.array(ln, dtype=np.uint64),
+                            np.zeros(n, dtype=np.uint32), nthreads=8)
+        np.testing.assert_array_equal(u32(out_a), exp, err_msg=f"batch_device replay {rep}")
+        np.testing.assert_array_equal(u32(out_b), exp, err_msg=f"batch_device_ws replay {rep}")
+
+
 def test_strided_api_seeds_and_stride():
     n, L, stride = 300, 200_000, 200_064
     mem, ptrs, lens = _strided_fill(n, L, stride=stride, index0=1000)
