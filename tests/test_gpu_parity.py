@@ -455,3 +455,40 @@ def test_concurrent_host_threads_dropin():
     for k in range(4):
         e = exp[k::4]
         assert res[k] == e + e
+
+
+def test_concurrent_device_calls_shared_and_private_streams():
+    """Host threads issuing zcrc32_batch_device at once, on one shared stream
+    and on private streams, with growing batch sizes (the per-stream scratch
+    cache grows under its lock while other threads launch): every result vs
+    the oracle."""
+    from concurrent.futures import ThreadPoolExecutor
+    rnd = random.Random(77)
+    total = 64 << 20
+    mem = torch.randint(0, 256, (total,), dtype=torch.uint8, device=DEV)
+    host = mem.cpu().numpy()
+    jobs = []
+    for k in range(24):
+        n = [5, 300, 2000, 8000, 12000][k % 5] + k
+        ln = [rnd.randint(0, 3000) for _ in range(n)]
+        offs = [rnd.randrange(0, total - L) for L in ln]
+        jobs.append((offs, ln))
+    shared = torch.cuda.Stream(device=DEV)
+    private = [torch.cuda.Stream(device=DEV) for _ in range(4)]
+
+    def work(k):
+        offs, ln = jobs[k]
+        st = shared if k % 2 == 0 else private[k % 4]
+        with torch.cuda.stream(st):
+            ptrs = torch.tensor([mem.data_ptr() + q for q in offs], dtype=torch.int64, device=DEV)
+            lt = torch.tensor(ln, dtype=torch.int64, device=DEV)
+            out = z.crc32_batch_device(ptrs, lt)
+            st.synchronize()
+            return u32(out)
+
+    with ThreadPoolExecutor(8) as ex:
+        res = list(ex.map(work, range(len(jobs))))
+    for k, ((offs, ln), got) in enumerate(zip(jobs, res)):
+        ap = np.array([host.ctypes.data + q for q in offs], dtype=np.uint64)
+        exp = o.crc32_batch(ap, np.array(ln, dtype=np.uint64), np.zeros(len(ln), dtype=np.uint32), nthreads=8)
+        np.testing.assert_array_equal(got, exp, err_msg=f"job {k}")
