@@ -140,11 +140,13 @@ def test_inflate_random_bytes_terminate_like_oracle():
 def test_inflate_corpus_both_window_kernels():
     """launch_inflate picks the 32 KiB-window kernel when every stream of the
     batch is resident at once (<= 4 per CU) and the 16 KiB-ring kernel (far
-    matches read back from dst) above that: run the corpus on both."""
+    matches read back from dst) above that; above 8 per CU the streams are
+    also dispatched longest-first through a device-sorted order: run the
+    corpus on all three."""
     items = S.corpus()
     cus = z.device_info()["num_cus"]
     assert len(items) <= 4 * cus
-    for reps in (1, (4 * cus) // len(items) + 2):
+    for reps in (1, (4 * cus) // len(items) + 2, (8 * cus) // len(items) + 2):
         batch = items * reps
         st, ol, outs, *_ = _run([s for _, s, _ in batch], [len(d) for _, _, d in batch])
         for k, (name, _, data) in enumerate(batch):

@@ -53,13 +53,53 @@ namespace w32 {  // the whole 32 KiB window in LDS: four streams per CU
 #undef ZI_WIN
 }  // namespace w32
 
+// Longest-first dispatch.  Workgroups start in index order, so when a batch
+// has more streams than can be resident, a slow stream that happens to sit
+// at the end of the batch starts last and finishes alone.  Decode time
+// tracks the compressed size, so one workgroup counting-sorts the streams
+// by quarter-octave of src_len, largest first (order within a bucket is
+// arbitrary; every stream's result is its own).
+__global__ __launch_bounds__(1024) void inflate_order_kernel(const uint64_t *src_len, uint64_t n, uint32_t *order) {
+  constexpr int kBuckets = 4 * 40;  // quarter octaves up to 2^40
+  __shared__ uint32_t cnt[kBuckets];
+  for (int b = threadIdx.x; b < kBuckets; b += blockDim.x) cnt[b] = 0;
+  __syncthreads();
+  auto bucket = [&](uint64_t len) -> int {  // descending: bucket 0 holds the largest
+    if (len < 2) return kBuckets - 1;
+    const int lg = 63 - __builtin_clzll(len);
+    const int q = lg >= 2 ? (int)((len >> (lg - 2)) & 3u) : 0;
+    const int k = 4 * (lg < 39 ? lg : 39) + q;
+    return kBuckets - 1 - k;
+  };
+  for (uint64_t i = threadIdx.x; i < n; i += blockDim.x) atomicAdd(&cnt[bucket(src_len[i])], 1u);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t run = 0;
+    for (int b = 0; b < kBuckets; b++) {
+      const uint32_t c = cnt[b];
+      cnt[b] = run;
+      run += c;
+    }
+  }
+  __syncthreads();
+  for (uint64_t i = threadIdx.x; i < n; i += blockDim.x) order[atomicAdd(&cnt[bucket(src_len[i])], 1u)] = (uint32_t)i;
+}
+
 // Up to four streams per CU all fit at once with the full window (no reads
 // back from dst: text-like streams decode ~20% faster); larger batches take
-// the 16 KiB ring and twice the streams per CU (profiles/r01/v8).
-hipError_t launch_inflate(const InflateArgs &args, int num_cus, hipStream_t stream) {
+// the 16 KiB ring and twice the streams per CU (profiles/r01/v8), and are
+// dispatched longest-first.
+hipError_t launch_inflate(const InflateArgs &args, int num_cus, hipStream_t stream, uint32_t *order_scratch) {
   if (args.n == 0) return hipSuccess;
   if (args.n <= 4ull * (uint64_t)num_cus) return w32::launch(args, stream);
-  return w16::launch(args, stream);
+  InflateArgs a = args;
+  if (order_scratch && args.n > 8ull * (uint64_t)num_cus && args.n <= 0xFFFFFFFFull) {
+    hipLaunchKernelGGL(inflate_order_kernel, dim3(1), dim3(1024), 0, stream, args.src_len, args.n, order_scratch);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    a.order = order_scratch;
+  }
+  return w16::launch(a, stream);
 }
 
 }  // namespace zcrc

@@ -809,8 +809,8 @@ __device__ void fixed_tables(Lds &s, LLTab &ll, DTab &dd) {
 
 __global__ __launch_bounds__(64) void inflate_kernel(InflateArgs a) {
   __shared__ __attribute__((aligned(16))) Lds s;
-  const uint64_t i = blockIdx.x;
-  if (i >= a.n) return;
+  if (blockIdx.x >= a.n) return;
+  const uint64_t i = a.order ? a.order[blockIdx.x] : blockIdx.x;
   const uint8_t *src = a.src[i];
   const uint64_t src_len = a.src_len[i];
   Out o;

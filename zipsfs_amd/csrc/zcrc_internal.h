@@ -73,9 +73,16 @@ struct InflateArgs {
   uint64_t *out_len;
   int32_t *status;
   uint64_t n;
+  // optional dispatch order (workgroup b decodes stream order[b]); nullptr:
+  // stream b.  launch_inflate fills it longest-first when streams queue.
+  const uint32_t *order;
 };
 constexpr uint64_t kInflateMaxSrc = 0xF0000000ull;  // 32-bit buffer range and block arithmetic
-hipError_t launch_inflate(const InflateArgs &args, int num_cus, hipStream_t stream);
+// order_scratch: >= 4 * n bytes of device memory for the dispatch order
+// (used when the batch exceeds the streams resident at once; may be null)
+hipError_t launch_inflate(const InflateArgs &args, int num_cus, hipStream_t stream, uint32_t *order_scratch);
+// purposes of the runtime's per-stream scratch cache (zcrc_runtime.hip)
+enum ScratchUse { kScratchBatch = 0, kScratchInflateOrder = 1 };
 
 inline uint64_t plan_tiles(uint64_t n) { return n == 0 ? 1 : (n + kPlanTile - 1) / kPlanTile; }
 hipError_t launch_plan(const uint64_t *d_lens, uint64_t n, uint64_t *d_prefix, uint64_t *d_tile_sum,

@@ -19,6 +19,7 @@
 #include <new>
 #include <string>
 #include <thread>
+#include <tuple>
 #include <vector>
 
 #include "../../include/zcrc.h"
@@ -137,6 +138,41 @@ int launch_main(const BatchArgs &args, bool strided, const DeviceCtx &dc, hipStr
 }
 
 // ------------------------------------------------------------- device batch
+
+// Eager calls reuse a grow-only scratch per (device, stream, purpose):
+// launches on one stream run in order, so one buffer serves them all.  A
+// hipMallocAsync/hipFreeAsync pair per call blocked the host until the
+// previous launch had finished (tools/host_overhead.py: 56 us of host time
+// per config-2 call, 8.6 us with reused scratch), so back-to-back calls
+// could not queue.  *lk holds the cache lock until the caller has launched,
+// so that a growth never frees a buffer another thread is about to launch
+// with.  Keyed by the stream handle: a destroyed stream's object lives on
+// until its queued work completes (commands hold references to it), so a
+// handle cannot come back for a new stream while a launch that used its
+// scratch is still pending.  (hipStreamGetId would be cleaner but is newer
+// than the HIP runtime PyTorch ships.)
+int stream_scratch(hipStream_t st, int use, size_t bytes, void **out, size_t *have, std::unique_lock<std::mutex> *lk) {
+  static std::mutex mu;
+  static std::map<std::tuple<int, hipStream_t, int>, std::pair<void *, size_t>> cache;
+  int dev = 0;
+  ZCRC_HIP_TRY(hipGetDevice(&dev));
+  *lk = std::unique_lock<std::mutex>(mu);
+  auto &slot = cache[{dev, st, use}];
+  if (slot.second < bytes) {
+    if (slot.first) {  // rare: a bigger batch than any before on this stream
+      ZCRC_HIP_TRY(hipStreamSynchronize(st));
+      ZCRC_HIP_TRY(hipFree(slot.first));
+      slot = {nullptr, 0};
+    }
+    const size_t nb = std::max<size_t>(bytes, 64u << 10);
+    ZCRC_HIP_TRY(hipMalloc(&slot.first, nb));
+    ZCRC_HIP_TRY(hipMemset(slot.first, 0, nb));
+    slot.second = nb;
+  }
+  *out = slot.first;
+  *have = slot.second;
+  return ZCRC_OK;
+}
 
 // Epochs of fused-plan launches: unique per launch in this process and far
 // from the small integers stale scratch tends to hold (splitmix64 of a counter).
@@ -597,36 +633,12 @@ int zcrc32_batch_device(const void *const *d_ptrs, const uint64_t *d_lens, const
     if (e != hipSuccess) return fail(ZCRC_ERR_HIP, std::string("hipFreeAsync: ") + hipGetErrorString(e));
     return ZCRC_OK;
   }
-  // Eager calls reuse a grow-only scratch per (device, stream): launches on
-  // one stream run in order, so one buffer serves them all.  A
-  // hipMallocAsync/hipFreeAsync pair per call blocked the host until the
-  // previous launch had finished (tools/host_overhead.py: 56 us of host time
-  // per config-2 call, 11 us with reused scratch), so back-to-back calls
-  // could not queue.  The lock is held across the launch so that a growth
-  // never frees a buffer another thread is about to launch with.
-  // Keyed by the stream handle: a destroyed stream's object lives on until
-  // its queued work completes (commands hold references to it), so a
-  // handle cannot come back for a new stream while a launch that used its
-  // scratch is still pending.  (hipStreamGetId would be cleaner but is
-  // newer than the HIP runtime PyTorch ships.)
-  static std::mutex mu;
-  static std::map<std::pair<int, hipStream_t>, std::pair<void *, size_t>> cache;
-  int dev = 0;
-  ZCRC_HIP_TRY(hipGetDevice(&dev));
-  std::lock_guard<std::mutex> lk(mu);
-  auto &slot = cache[{dev, st}];
-  if (slot.second < bytes) {
-    if (slot.first) {  // rare: a bigger batch than any before on this stream
-      ZCRC_HIP_TRY(hipStreamSynchronize(st));
-      ZCRC_HIP_TRY(hipFree(slot.first));
-      slot = {nullptr, 0};
-    }
-    const size_t nb = std::max<size_t>(bytes, 64u << 10);
-    ZCRC_HIP_TRY(hipMalloc(&slot.first, nb));
-    ZCRC_HIP_TRY(hipMemset(slot.first, 0, nb));
-    slot.second = nb;
-  }
-  return batch_device_ws(d_ptrs, d_lens, d_seeds_or_null, d_out, n, slot.first, slot.second, st, true);
+  void *scratch = nullptr;
+  size_t have = 0;
+  std::unique_lock<std::mutex> lk;
+  const int rc = stream_scratch(st, kScratchBatch, bytes, &scratch, &have, &lk);
+  if (rc) return rc;
+  return batch_device_ws(d_ptrs, d_lens, d_seeds_or_null, d_out, n, scratch, have, st, true);
 }
 
 int zcrc32_batch_device_strided(const void *d_base, uint64_t stride, uint64_t len, size_t n,
@@ -689,7 +701,19 @@ int zcrc_inflate_batch_device(const void *const *d_src, const uint64_t *d_src_le
   a.out_len = d_out_len;
   a.status = d_status;
   a.n = n;
-  ZCRC_HIP_TRY(launch_inflate(a, dc->num_cus, static_cast<hipStream_t>(stream)));
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+  ZCRC_HIP_TRY(hipStreamIsCapturing(st, &cap));
+  if (cap != hipStreamCaptureStatusNone) {  // graph capture: index-order dispatch, no scratch
+    ZCRC_HIP_TRY(launch_inflate(a, dc->num_cus, st, nullptr));
+    return ZCRC_OK;
+  }
+  void *order = nullptr;
+  size_t have = 0;
+  std::unique_lock<std::mutex> lk;
+  rc = stream_scratch(st, kScratchInflateOrder, 4 * n, &order, &have, &lk);
+  if (rc) return rc;
+  ZCRC_HIP_TRY(launch_inflate(a, dc->num_cus, st, static_cast<uint32_t *>(order)));
   return ZCRC_OK;
 }
 
