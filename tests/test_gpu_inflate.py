@@ -139,10 +139,10 @@ def test_inflate_random_bytes_terminate_like_oracle():
 
 def test_inflate_corpus_both_window_kernels():
     """launch_inflate picks the 32 KiB-window kernel when every stream of the
-    batch is resident at once (<= 4 per CU) and the 16 KiB-ring kernel (far
-    matches read back from dst) above that; above 8 per CU the streams are
-    also dispatched longest-first through a device-sorted order: run the
-    corpus on all three."""
+    batch is resident at once (<= 4 per CU), the 16 KiB-ring kernel (far
+    matches read back from dst) up to 8 per CU, and above that the 8 KiB-ring
+    kernel (16 per CU) with the streams dispatched longest-first through a
+    device-sorted order: run the corpus on all three."""
     items = S.corpus()
     cus = z.device_info()["num_cus"]
     assert len(items) <= 4 * cus

@@ -47,6 +47,13 @@ namespace w16 {  // 16 KiB ring: eight streams per CU, far matches read back fro
 #include "zcrc_inflate_impl.h"
 #undef ZI_WIN
 }  // namespace w16
+namespace w8 {  // 8 KiB ring, sixteen streams per CU (four waves per SIMD)
+#define ZI_WIN 8192u
+#define ZI_WPE 4
+#include "zcrc_inflate_impl.h"
+#undef ZI_WPE
+#undef ZI_WIN
+}  // namespace w8
 namespace w32 {  // the whole 32 KiB window in LDS: four streams per CU
 #define ZI_WIN 32768u
 #include "zcrc_inflate_impl.h"
@@ -86,19 +93,22 @@ __global__ __launch_bounds__(1024) void inflate_order_kernel(const uint64_t *src
 }
 
 // Up to four streams per CU all fit at once with the full window (no reads
-// back from dst: text-like streams decode ~20% faster); larger batches take
-// the 16 KiB ring and twice the streams per CU (profiles/r01/v8), and are
-// dispatched longest-first.
+// back from dst: text-like streams decode ~20% faster); up to eight take
+// the 16 KiB ring (profiles/r01/v8); larger batches take the 8 KiB ring at
+// sixteen streams per CU -- more waves to hide the scalar dependency chains:
+// binary-like streams +32%, text-like -4% from the extra reads back from
+// dst (profiles/r01/v9) -- and are dispatched longest-first.
 hipError_t launch_inflate(const InflateArgs &args, int num_cus, hipStream_t stream, uint32_t *order_scratch) {
   if (args.n == 0) return hipSuccess;
   if (args.n <= 4ull * (uint64_t)num_cus) return w32::launch(args, stream);
   InflateArgs a = args;
-  if (order_scratch && args.n > 8ull * (uint64_t)num_cus && args.n <= 0xFFFFFFFFull) {
+  if (order_scratch && args.n > 8ull * (uint64_t)num_cus && args.n <= 0xFFFFFFFFull) {  // queued streams
     hipLaunchKernelGGL(inflate_order_kernel, dim3(1), dim3(1024), 0, stream, args.src_len, args.n, order_scratch);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     a.order = order_scratch;
   }
+  if (args.n > 8ull * (uint64_t)num_cus) return w8::launch(a, stream);
   return w16::launch(a, stream);
 }
 

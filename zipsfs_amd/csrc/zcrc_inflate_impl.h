@@ -11,7 +11,10 @@ namespace {
 constexpr uint32_t kWin = ZI_WIN, kWinMask = kWin - 1;
 constexpr uint32_t kLLRoot = 10, kDRoot = 8, kCLRoot = 7;
 constexpr uint32_t kLLRegs = (1u << kLLRoot) / 64, kDRegs = (1u << kDRoot) / 64, kCLRegs = (1u << kCLRoot) / 64;
-constexpr uint32_t kFlushLag = 8192;  // bytes decoded ahead of the last flush
+// bytes decoded ahead of the last flush; pos - fl stays below
+// kFlushLag + 1024 + 258, which must be < kWin (copy_match)
+constexpr uint32_t kFlushLag = kWin >= 16384 ? 8192 : kWin / 2;
+static_assert(kFlushLag + 1024 + 258 < kWin, "flush lag must leave the window's far bytes flushed");
 
 // Register-resident tables are LLVM vectors: a dynamic subscript lowers to
 // s_set_gpr_idx + v_mov (no scratch), where a local array would be demoted
@@ -807,7 +810,13 @@ __device__ void fixed_tables(Lds &s, LLTab &ll, DTab &dd) {
   build_code<kDRoot, kDRegs>(s.lens + 288, 32, s.ddsym, &s.ddm, A_DIST, dd);
 }
 
-__global__ __launch_bounds__(64) void inflate_kernel(InflateArgs a) {
+// ZI_WPE: waves per SIMD the register allocation must allow (LDS decides
+// how many streams actually share a CU)
+#ifndef ZI_WPE
+#define ZI_WPE 1
+#define ZI_WPE_DEFAULTED
+#endif
+__global__ __launch_bounds__(64, ZI_WPE) void inflate_kernel(InflateArgs a) {
   __shared__ __attribute__((aligned(16))) Lds s;
   if (blockIdx.x >= a.n) return;
   const uint64_t i = a.order ? a.order[blockIdx.x] : blockIdx.x;
@@ -880,3 +889,7 @@ hipError_t launch(const InflateArgs &args, hipStream_t stream) {
   hipLaunchKernelGGL(inflate_kernel, dim3((unsigned)args.n), dim3(64), 0, stream, args);
   return hipGetLastError();
 }
+#ifdef ZI_WPE_DEFAULTED
+#undef ZI_WPE
+#undef ZI_WPE_DEFAULTED
+#endif
