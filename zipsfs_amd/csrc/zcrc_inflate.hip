@@ -19,14 +19,15 @@
 //     the symbol chain.  Literal/length root 10 (16 VGPRs), distance root 8
 //     (4 VGPRs), code-length root 7 (2 VGPRs); longer codes take a canonical
 //     slow path with per-length (first, count, offset) kept in LDS;
-//   * LDS (~34 KiB, four streams per CU) holds the 32 KiB window as a ring
-//     (back-references are lane-parallel LDS copies) and the canonical symbol
-//     order the table builds need;
+//   * LDS holds the window as a ring (back-references are lane-parallel LDS
+//     copies; older bytes are read back from dst) and the canonical symbol
+//     order the table builds need.  Three instantiations by batch size:
+//     32 KiB ring at 4 streams per CU, 16 KiB at 8, 8 KiB at 16;
 //   * input: three 1 KiB blocks staged in VGPRs (16 B per lane, coalesced
 //     buffer loads issued one block ahead of use); the bit reader gathers
 //     dwords with v_readlane;
-//   * output leaves the ring in 8 KiB batches of 16-B stores, lagging the
-//     decode (a byte is overwritten only 32 KiB later);
+//   * output leaves the ring in batches of 16-B stores (8 KiB; 4 KiB for the
+//     8 KiB ring), lagging the decode by less than the ring size;
 //   * table builds are wave-parallel: ballot counts, ballot-ranked
 //     canonical order, every lane decodes its own LUT indices.
 #include <hip/hip_runtime.h>
