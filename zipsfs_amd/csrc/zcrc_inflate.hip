@@ -50,7 +50,10 @@ namespace w16 {  // 16 KiB ring: eight streams per CU, far matches read back fro
 }  // namespace w16
 namespace w8 {  // 8 KiB ring, sixteen streams per CU (four waves per SIMD)
 #define ZI_WIN 8192u
-#define ZI_WPE 4
+#ifndef ZI_W8_WPE
+#define ZI_W8_WPE 4
+#endif
+#define ZI_WPE ZI_W8_WPE
 #include "zcrc_inflate_impl.h"
 #undef ZI_WPE
 #undef ZI_WIN

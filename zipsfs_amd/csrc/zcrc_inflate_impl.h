@@ -46,6 +46,16 @@ __device__ __forceinline__ uint32_t e_extra(uint32_t e) { return (e >> 7) & 15u;
 __device__ __forceinline__ uint32_t e_val(uint32_t e) { return e >> 11; }
 
 __device__ __forceinline__ uint32_t uni(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); }
+// The lane id through a volatile move: values derived from it (lane + 64 r,
+// their bit reversals) are then recomputed where they are used instead of
+// being hoisted to the kernel entry and kept live across the symbol loop
+// (at four waves per SIMD they were 32 spilled VGPRs, reloaded in the copy
+// loops).
+__device__ __forceinline__ uint32_t lane_id() {
+  uint32_t l;
+  asm volatile("v_mov_b32 %0, %1" : "=v"(l) : "v"(threadIdx.x));
+  return l;
+}
 __device__ __forceinline__ uint32_t lane_get(uint32_t v, uint32_t lane) {
   return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)lane);
 }
@@ -114,7 +124,7 @@ struct Lds {
 template <uint32_t ROOT, uint32_t NREG>
 __device__ bool build_code(const uint8_t *lens, uint32_t n, uint16_t *sym, CodeMeta *meta, uint32_t alphabet,
                            typename VecOf<NREG>::T &lut) {
-  const uint32_t lane = threadIdx.x;
+  const uint32_t lane = lane_id();
   const uint32_t nch = (n + 63) >> 6;  // <= 5
   const uint64_t lt = (1ull << lane) - 1ull;
   uint32_t lv[5], rk[5];
@@ -327,7 +337,7 @@ struct Out {
 // Stores go through a buffer resource sized to the bytes due, so the
 // hardware drops the lanes past `upto` (no divergent branch).
 __device__ __forceinline__ void flush_to(Lds &s, Out &o, uint64_t upto) {
-  const uint32_t lane = threadIdx.x;
+  const uint32_t lane = lane_id();
   while (o.fl < upto) {
     const uint32_t roff = (uint32_t)(o.fl & kWinMask);
     const uint32_t m = (upto - o.fl < 1024u) ? (uint32_t)(upto - o.fl) : 1024u;
@@ -368,7 +378,7 @@ __device__ __forceinline__ void settle(Lds &s, Out &o) {
 // kWin) and are read back from dst with sc1 loads, which bypass the CU's
 // L1 (a line cached there may predate the flush of its other bytes).
 __device__ __forceinline__ void copy_match(Lds &s, const Out &o, uint32_t p0, uint32_t len, uint32_t dist) {
-  const uint32_t lane = threadIdx.x;
+  const uint32_t lane = lane_id();
   const uint32_t src = p0 - dist;
   if (dist > kWin) {
     const __amdgpu_buffer_rsrc_t far =
@@ -699,7 +709,7 @@ __device__ int32_t codes(Lds &s, Reader &r, Out &o, const LLTab &ll, const DTab 
 }
 
 __device__ int32_t stored(Lds &s, Reader &r, Out &o) {
-  const uint32_t lane = threadIdx.x;
+  const uint32_t lane = lane_id();
   r.drop(r.nb & 7u);  // byte boundary
   const uint32_t len = r.bits(16);
   const uint32_t nlen = r.bits(16);
@@ -729,7 +739,7 @@ __device__ int32_t stored(Lds &s, Reader &r, Out &o) {
 }
 
 __device__ int32_t dynamic_tables(Lds &s, Reader &r, LLTab &ll, DTab &dd) {
-  const uint32_t lane = threadIdx.x;
+  const uint32_t lane = lane_id();
   const uint32_t nlen = r.bits(5) + 257, ndist = r.bits(5) + 1, ncode = r.bits(4) + 4;
   if (nlen > 286 || ndist > 30) return ZCRC_INFLATE_ERR_CODES;
   // code-length code lengths: 3 bits each, in kClenOrder order; lane k takes
@@ -795,7 +805,7 @@ __device__ int32_t dynamic_tables(Lds &s, Reader &r, LLTab &ll, DTab &dd) {
 }
 
 __device__ void fixed_tables(Lds &s, LLTab &ll, DTab &dd) {
-  const uint32_t lane = threadIdx.x;
+  const uint32_t lane = lane_id();
   for (uint32_t k = lane; k < 320; k += 64) {
     uint8_t l;
     if (k < 144) l = 8;
