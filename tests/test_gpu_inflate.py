@@ -151,3 +151,36 @@ def test_inflate_corpus_both_window_kernels():
         st, ol, outs, *_ = _run([s for _, s, _ in batch], [len(d) for _, _, d in batch])
         for k, (name, _, data) in enumerate(batch):
             assert st[k] == 0 and outs[k] == data, (reps, name)
+
+
+def test_inflate_host_batch_large_mixed_sizes_longest_first():
+    """The host entry point with more streams than the GPU holds at once
+    (> 8 per CU: 8 KiB-ring kernel, longest-first order built on the device
+    from per-stream scratch), sizes spread over four octaves so the order
+    really permutes, plus error entries scattered through the batch: every
+    result lands at its own index with zlib's bytes and CRC."""
+    import random
+    rnd = random.Random(11)
+    cus = z.device_info()["num_cus"]
+    n = 8 * cus + 300
+    base = [it for it in S.corpus() if it[0].startswith(("text", "spectrum"))]
+    streams, caps, want = [], [], []
+    for k in range(n):
+        if k % 97 == 13:  # invalid block type / empty input
+            streams.append(b"\x07" if k % 2 else b"")
+            caps.append(10)
+            want.append(None)
+            continue
+        name, s, data = base[rnd.randrange(len(base))]
+        cut = rnd.choice([len(data), len(data) // 3, len(data) // 9, 4000])
+        d = data[:cut]
+        streams.append(zlib.compress(d, 6)[2:-4])
+        caps.append(len(d))
+        want.append(d)
+    res = z.inflate_batch(streams, caps)
+    assert len(res) == n
+    for k, ((st, out, crc), w) in enumerate(zip(res, want)):
+        if w is None:
+            assert st != 0, k
+        else:
+            assert st == 0 and out == w and crc == zlib.crc32(w), k
