@@ -37,7 +37,7 @@ def main():
     el = time.perf_counter() - t
     res["dropin_single_512MiB_GiBs"] = round(0.5 / el, 2)
     # latency of the drop-in for small entries (median ZIP entry ~4 KiB)
-    for n in (4096, 65536, 1 << 20, 16 << 20):
+    for n in (64, 4096, 16384, 32768, 65536, 1 << 20, 16 << 20):
         d = big[:n]
         lat = []
         for _ in range(20):
