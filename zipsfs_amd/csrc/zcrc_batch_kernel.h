@@ -591,6 +591,7 @@ __global__ __launch_bounds__(kThreads) void crc32_batch_kernel(BatchArgs args) {
   if (w >= W) return;  // no barrier after this point
   bool band = true;
 
+
   // diagnostic build: wall-clock stamps (s_memrealtime, 100 MHz) per wave
   const uint64_t t_begin = kStamp ? __builtin_amdgcn_s_memrealtime() : 0;
   const uint64_t static_bytes = S1 - S0;
@@ -608,6 +609,7 @@ __global__ __launch_bounds__(kThreads) void crc32_batch_kernel(BatchArgs args) {
   // held-but-unstarted unit would become a straggler.
   uint32_t u = 0, nx = 0;
   bool have_next = false, first_claim = true;
+  uint64_t t_unit_search = 0;  // diagnostic build: time in the unit range searches
   for (;;) {
     if (!band && u + 2 * (uint32_t)W < units) {
       if (lane == 0) nx = (uint32_t)W + atomicAdd(args.ctr, 1u);
@@ -630,7 +632,9 @@ __global__ __launch_bounds__(kThreads) void crc32_batch_kernel(BatchArgs args) {
     if (u >= units) break;
     const uint64_t t0 = Ts + (uint64_t)u * unit;
     last = (u + 1 == units);
+    const uint64_t ts0 = kStamp ? __builtin_amdgcn_s_memrealtime() : 0;
     bv.range(t0, t0 + unit, last, S0, S1, lb0, lb1);
+    if (kStamp) t_unit_search += __builtin_amdgcn_s_memrealtime() - ts0;
     salt = u ^ 0x9E3779B9u;
     if (kPrio && band) __builtin_amdgcn_s_setprio(0);
     band = false;
@@ -642,6 +646,7 @@ __global__ __launch_bounds__(kThreads) void crc32_batch_kernel(BatchArgs args) {
     args.stamps[8 * w + 3] = static_bytes;
     args.stamps[8 * w + 4] = t_entry;
     args.stamps[8 * w + 5] = t_search;
+    args.stamps[8 * w + 6] = t_unit_search;
   }
 }
 
