@@ -129,6 +129,7 @@ int main(int argc, char **argv) {
       {"prio", crc32_batch_kernel<false, 4, 0, true, false, 1>, true, 0, 0},
       {"product", crc32_batch_kernel<false, 4, 0, true, false, 1>, true, kDynShift, kDynUnit},
       {"product+sc1nt", crc32_batch_kernel<false, 4, 0, true, false, 1, 18>, true, kDynShift, kDynUnit},
+      {"prod-u256k", crc32_batch_kernel<false, 4, 0, true, false, 1>, true, kDynShift, 256u << 10},
       {"prod-u512k", crc32_batch_kernel<false, 4, 0, true, false, 1>, true, kDynShift, 512u << 10},
       {"prod-q", crc32_batch_kernel<false, 4, 0, true, false, 1>, true, 2, kDynUnit},
       {"prod-q-u512k", crc32_batch_kernel<false, 4, 0, true, false, 1>, true, 2, 512u << 10},
