@@ -609,7 +609,7 @@ __global__ __launch_bounds__(kThreads) void crc32_batch_kernel(BatchArgs args) {
   // held-but-unstarted unit would become a straggler.
   uint32_t u = 0, nx = 0;
   bool have_next = false, first_claim = true;
-  uint64_t t_unit_search = 0;  // diagnostic build: time in the unit range searches
+  uint64_t t_unit_search = 0, t_unit_drain = 0;  // diagnostic build: time in the unit range searches
   for (;;) {
     if (!band && u + 2 * (uint32_t)W < units) {
       if (lane == 0) nx = (uint32_t)W + atomicAdd(args.ctr, 1u);
@@ -632,7 +632,13 @@ __global__ __launch_bounds__(kThreads) void crc32_batch_kernel(BatchArgs args) {
     if (u >= units) break;
     const uint64_t t0 = Ts + (uint64_t)u * unit;
     last = (u + 1 == units);
-    const uint64_t ts0 = kStamp ? __builtin_amdgcn_s_memrealtime() : 0;
+    uint64_t ts0 = 0;
+    if (kStamp) {  // split the search time into draining the previous piece's stores/atomics and the search
+      const uint64_t tw = __builtin_amdgcn_s_memrealtime();
+      __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+      ts0 = __builtin_amdgcn_s_memrealtime();
+      t_unit_drain += ts0 - tw;
+    }
     bv.range(t0, t0 + unit, last, S0, S1, lb0, lb1);
     if (kStamp) t_unit_search += __builtin_amdgcn_s_memrealtime() - ts0;
     salt = u ^ 0x9E3779B9u;
@@ -647,6 +653,7 @@ __global__ __launch_bounds__(kThreads) void crc32_batch_kernel(BatchArgs args) {
     args.stamps[8 * w + 4] = t_entry;
     args.stamps[8 * w + 5] = t_search;
     args.stamps[8 * w + 6] = t_unit_search;
+    args.stamps[8 * w + 7] = t_unit_drain;
   }
 }
 
