@@ -179,7 +179,26 @@ def cpu_baseline(cfg: int, budget_s: float) -> dict:
             "sample": sample + (" -- src/cg_crc32.c compiled -O2 by oracle/Makefile" if use_ref else
                                 " -- CPU restatement oracle/crc32_port.c -O2"),
             "single_core_gibs": round(single, 3),
-            "single_core_O0_as_shipped_gibs": None if o0 is None else round(o0, 3)}
+            "single_core_O0_as_shipped_gibs": None if o0 is None else round(o0, 3),
+            "host": host_cpu()}
+
+
+def host_cpu() -> dict:
+    """CPU model and counts of the box the baseline ran on."""
+    model = None
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    try:
+        allowed = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        allowed = None
+    return {"model": model, "logical_cpus": os.cpu_count(), "cpus_allowed": allowed}
 
 
 def main() -> None:
