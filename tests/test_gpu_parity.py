@@ -492,3 +492,46 @@ def test_concurrent_device_calls_shared_and_private_streams():
         ap = np.array([host.ctypes.data + q for q in offs], dtype=np.uint64)
         exp = o.crc32_batch(ap, np.array(ln, dtype=np.uint64), np.zeros(len(ln), dtype=np.uint32), nthreads=8)
         np.testing.assert_array_equal(got, exp, err_msg=f"job {k}")
+
+
+def test_fused_plan_concurrent_streams_no_deadlock():
+    """Fused-plan launches (<= 8192 buffers) from six host threads on six
+    streams at once, each queueing twelve launches without synchronising:
+    the launches overlap on the GPU, and whichever workgroup of a launch runs
+    first must do its plan (a fixed planner workgroup could queue behind the
+    other launches' spinning workgroups: deadlock, then the poll bound's
+    trap).  Every result vs the oracle."""
+    from concurrent.futures import ThreadPoolExecutor
+    rnd = random.Random(123)
+    total = 32 << 20
+    mem = torch.randint(0, 256, (total,), dtype=torch.uint8, device=DEV)
+    host = mem.cpu().numpy()
+    streams = [torch.cuda.Stream(device=DEV) for _ in range(6)]
+    plans = []
+    for t in range(6):
+        jobs = []
+        for _ in range(12):
+            n = rnd.randint(4000, 8192)
+            ln = [rnd.randint(0, 4000) for _ in range(n)]
+            offs = [rnd.randrange(0, total - L) for L in ln]
+            jobs.append((offs, ln))
+        plans.append(jobs)
+
+    def work(t):
+        st = streams[t]
+        outs = []
+        with torch.cuda.stream(st):
+            for offs, ln in plans[t]:
+                ptrs = torch.tensor([mem.data_ptr() + q for q in offs], dtype=torch.int64, device=DEV)
+                lt = torch.tensor(ln, dtype=torch.int64, device=DEV)
+                outs.append((z.crc32_batch_device(ptrs, lt), ptrs, lt))
+            st.synchronize()
+        return [u32(o) for o, _, _ in outs]
+
+    with ThreadPoolExecutor(6) as ex:
+        res = list(ex.map(work, range(6)))
+    for t in range(6):
+        for j, ((offs, ln), got) in enumerate(zip(plans[t], res[t])):
+            ap = np.array([host.ctypes.data + q for q in offs], dtype=np.uint64)
+            exp = o.crc32_batch(ap, np.array(ln, dtype=np.uint64), np.zeros(len(ln), dtype=np.uint32), nthreads=8)
+            np.testing.assert_array_equal(got, exp, err_msg=f"thread {t} job {j}")

@@ -273,17 +273,31 @@ __device__ uint64_t block_excl_scan(uint64_t v, uint64_t *s_tmp /* 16 */, uint64
   return off + inc - v;
 }
 
-// Fused plan (BatchArgs::plan_lens set; pointer form, n <= kPlanTile):
-// workgroup 0 writes prefix[0..n], zeroes out[] and the work counter, then
-// publishes plan_epoch at *plan_flag with an agent-scope release; the other
-// workgroups poll the flag (one lane each) and acquire.  Workgroup 0 is
-// dispatched first and waits for nobody, so the wait needs no co-residency.
+// Fused plan (BatchArgs::plan_lens set; pointer form, n <= kPlanTile): the
+// first workgroup of the launch to run writes prefix[0..n], zeroes out[]
+// and the work counter, then publishes plan_epoch at *plan_flag with an
+// agent-scope release; the others poll the flag (one lane each).
+// "First to run" is decided by an atomic exchange of the epoch into a claim
+// word (plan_flag + 8): the planner is a running workgroup that waits for
+// nobody, so the wait is deadlock-free whatever else shares the GPU.  (With
+// "workgroup 0 plans", two fused launches on different streams deadlocked:
+// each one's spinning workgroups filled the CUs of the XCD the other's
+// workgroup 0 was queued for, and the poll bound fired.)
 // Saves the plan launch and the dependent-launch gap (~15 us per call for
 // config 2).  The poll is bounded: a flag that never arrives traps (a HIP
 // error at the next synchronisation) instead of hanging the device.
 __device__ __forceinline__ void fused_plan(const BatchArgs &args, uint32_t *s_lds) {
   const uint32_t tid = threadIdx.x;
-  if (blockIdx.x == 0) {
+  uint32_t *s_planner = s_lds + 64;  // past block_excl_scan's 16 words
+  if (tid == 0) {
+    const uint64_t prev =
+        __hip_atomic_exchange(args.plan_flag + 8, args.plan_epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    *s_planner = prev != args.plan_epoch ? 1u : 0u;
+  }
+  __syncthreads();
+  const bool planner = *s_planner != 0u;
+  __syncthreads();  // everyone has read it before the scan reuses LDS
+  if (planner) {
     uint64_t *prefix = const_cast<uint64_t *>(args.prefix);
     const uint64_t n = args.n;
     uint64_t v[kPlanPerThread];

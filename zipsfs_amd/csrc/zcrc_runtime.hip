@@ -197,7 +197,8 @@ int batch_device_ws(const void *const *d_ptrs, const uint64_t *d_lens, const uin
   int rc = device_ctx(&dc);
   if (rc) return rc;
   // scratch: work counter (zeroed by the plan) and, 128 B further, the fused
-  // plan's flag (own kCtrBytes area) | prefix[n+1] | tile sums.  The counter must not share a cache line with
+  // plan's flag and (64 B after it) its claim word (own kCtrBytes area) |
+  // prefix[n+1] | tile sums.  The counter must not share a cache line with
   // the prefix, which every wave reads while claims hammer the counter.
   uint32_t *d_ctr = static_cast<uint32_t *>(scratch);
   uint64_t *d_prefix = reinterpret_cast<uint64_t *>(static_cast<uint8_t *>(scratch) + kCtrBytes);
