@@ -184,8 +184,12 @@ int main(int argc, char **argv) {
         double dr = 0;
         for (uint64_t w = 0; w < nw; w++)
           if (st8[8 * w + 1]) dr += st8[8 * w + 7] * 1e-2;
-        printf("unit searches %-8s mean %.1f us per wave, max %.1f us; draining stores first %.1f us per wave\n",
-               name, us / (cnt ? cnt : 1), mx, dr / (cnt ? cnt : 1));
+        double tl = 0;
+        for (uint64_t w = 0; w < nw; w++)
+          if (st8[8 * w + 1]) tl += st8[8 * w + 3] * 1e-2;
+        printf("unit searches %-8s mean %.1f us per wave, max %.1f us; draining stores first %.1f us per wave; "
+               "padding MCTs %.1f us per wave\n",
+               name, us / (cnt ? cnt : 1), mx, dr / (cnt ? cnt : 1), tl / (cnt ? cnt : 1));
       }
       printf("prologue %-8s entry spread %.1f us | first entry->first begin %.1f us | search us p50 %.1f p100 %.1f | "
              "LDS fill us p50 %.1f p100 %.1f\n", name, (e1 - e0) * 1e-2, (b0 - e0) * 1e-2, srch[srch.size() / 2],

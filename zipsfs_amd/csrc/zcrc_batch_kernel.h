@@ -65,6 +65,20 @@ __device__ __forceinline__ uint32_t comb_apply(const uint32_t *lds, int c, uint3
   return t[r & 0xFFu] ^ t[256 + ((r >> 8) & 0xFFu)] ^ t[512 + ((r >> 16) & 0xFFu)] ^ t[768 + (r >> 24)];
 }
 
+// r * x^(-8t), t < 16 (the piece's 16-B alignment padding): the LDS combine
+// tables for the 4-byte multiples (x^-32, x^-64), then the exact inverse
+// step x^-1 (zcrc_gf2.h) for the remaining 0-3 bytes, on the wave-uniform
+// register.  It replaced a global-memory MCT of x^(-8t): four loads that
+// cost ~4 us per piece under the stream, 7.6% of a wave's time on config 4
+// (tools/crc_variants padding-MCT stamps).
+__device__ __forceinline__ uint32_t shift_back(const uint32_t *lds, uint32_t r, uint32_t t) {
+  const uint32_t a = t >> 2;
+  if (a & 2u) r = (uint32_t)__builtin_amdgcn_readfirstlane((int)comb_apply(lds, 1, r));
+  if (a & 1u) r = (uint32_t)__builtin_amdgcn_readfirstlane((int)comb_apply(lds, 0, r));
+  for (uint32_t i = 0; i < 8u * (t & 3u); i++) r = gf2_times_xinv(r);
+  return r;
+}
+
 // r * c for a multiply-by-constant table in global memory (L2-resident).
 __device__ __forceinline__ uint32_t mct_apply_global(const uint32_t *t, uint32_t r) {
   return t[r & 0xFFu] ^ t[256 + ((r >> 8) & 0xFFu)] ^ t[512 + ((r >> 16) & 0xFFu)] ^ t[768 + (r >> 24)];
@@ -346,11 +360,11 @@ __device__ __forceinline__ void fused_plan(const BatchArgs &args, uint32_t *s_ld
 // Process every piece of the byte range [S0, S1) of the concatenated batch
 // (S0, S1 snapped; `last_range` also takes the trailing empty buffers).
 // Returns the number of pieces.  Wave-uniform; no barriers.
-template <bool kStrided, uint32_t kD, int kAblate, bool kRotate, int kPrio = 0, int kAux = 0>
+template <bool kStrided, uint32_t kD, int kAblate, bool kRotate, int kPrio = 0, int kAux = 0, bool kStamp = false>
 __device__ __forceinline__ uint64_t process_range(const BatchArgs &args, const BatchView<kStrided> &bv,
                                                   const uint32_t *s_lds, const TableBlob *tab, uint64_t S0,
                                                   uint64_t S1, bool last_wave, uint32_t salt, uint32_t lane,
-                                                  bool band, uint64_t lb0, uint64_t lb1) {
+                                                  bool band, uint64_t lb0, uint64_t lb1, uint64_t *t_tail = nullptr) {
   // lane constants for the braided lookups
   const uint32_t lo0 = (lane & 31u) * 4u;
   const uint32_t o0 = lo0, o1 = lo0 + 128u, o2 = lo0 + 65536u, o3 = lo0 + 65536u + 128u;
@@ -503,7 +517,9 @@ __device__ __forceinline__ uint64_t process_range(const BatchArgs &args, const B
       r ^= moved;
     }
     r = uni32(r);
-    if (tpad) r = mct_apply_global(tab->tshift + tpad * 1024u, r);  // -> register at pend
+    const uint64_t tt0 = kStamp ? __builtin_amdgcn_s_memrealtime() : 0;
+    if (tpad) r = shift_back(s_lds, r, tpad);  // -> register at pend
+    if (kStamp) r = uni32(r), *t_tail += __builtin_amdgcn_s_memrealtime() - tt0;  // diagnostic: padding MCT
 
     if (whole) {
       if (lane == 0) args.out[i] = ~r;
@@ -624,14 +640,15 @@ __global__ __launch_bounds__(kThreads) void crc32_batch_kernel(BatchArgs args) {
   uint32_t u = 0, nx = 0;
   bool have_next = false, first_claim = true;
   uint64_t t_unit_search = 0, t_unit_drain = 0;  // diagnostic build: time in the unit range searches
+  uint64_t t_tail = 0;                              // ... and in the alignment-padding MCTs
   for (;;) {
     if (!band && u + 2 * (uint32_t)W < units) {
       if (lane == 0) nx = (uint32_t)W + atomicAdd(args.ctr, 1u);
       have_next = true;
     }
     if (S0 < S1 || last)
-      npieces += process_range<kStrided, kD, kAblate, kRotate, kPrio, kAux>(args, bv, s_lds, tab, S0, S1, last, salt,
-                                                                             lane, band, lb0, lb1);
+      npieces += process_range<kStrided, kD, kAblate, kRotate, kPrio, kAux, kStamp>(
+          args, bv, s_lds, tab, S0, S1, last, salt, lane, band, lb0, lb1, &t_tail);
     if (!units) break;
     if (first_claim) {
       nx = (uint32_t)w;  // units >= W whenever the dynamic part is on
@@ -668,6 +685,7 @@ __global__ __launch_bounds__(kThreads) void crc32_batch_kernel(BatchArgs args) {
     args.stamps[8 * w + 5] = t_search;
     args.stamps[8 * w + 6] = t_unit_search;
     args.stamps[8 * w + 7] = t_unit_drain;
+    args.stamps[8 * w + 3] = t_tail;  // (replaces the static byte count in this build)
   }
 }
 
