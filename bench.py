@@ -318,8 +318,7 @@ def main() -> None:
                 "workload": wl.desc,
                 "buffers_per_gpu": wl.n_local,
                 "bytes_per_gpu_per_step": wl.bytes_local,
-                "api": ("zcrc32_batch_device (plan scan fused into the persistent CRC kernel)" if wl.n_local <= 8192
-                        else "zcrc32_batch_device (plan scan + persistent CRC kernel)") +
+                "api": "zcrc32_batch_device (plan scan + persistent CRC kernel)" +
                        (f" + {'RCCL' if args.dist_backend == 'nccl' else 'gloo'} all_gather of uint32 CRCs"
                         if world > 1 else ""),
                 "parallelism": f"round-robin buffer sharding over {world} GPU(s)",

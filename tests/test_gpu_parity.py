@@ -249,12 +249,12 @@ def test_dynamic_part_mixed_batches(shape):
 
 
 def test_fused_plan_back_to_back_vs_two_launch_path():
-    """zcrc32_batch_device scans the lengths inside the CRC kernel for
-    batches of <= 8192 buffers (workgroup 0 publishes the prefix with a
-    per-launch epoch; zcrc_batch_kernel.h fused_plan).  Many launches queued
-    back to back on one stream, each with different lengths, pool-recycled
-    scratch and the dynamic work counter, must equal the graph-safe
-    two-launch path (zcrc32_batch_device_ws) and the oracle."""
+    """Many zcrc32_batch_device launches queued back to back on one stream,
+    each with different lengths, the reused per-stream scratch and the
+    dynamic work counter, must equal zcrc32_batch_device_ws with its own
+    scratch per call, and the oracle.  (Named for the fused plan that eager
+    calls used until round 1's last session; they now take the two-launch
+    plan, zcrc_runtime.hip zcrc32_batch_device.)"""
     rnd = random.Random(31)
     total = 96 << 20
     mem = torch.randint(0, 256, (total,), dtype=torch.uint8, device=DEV)
@@ -495,12 +495,12 @@ def test_concurrent_device_calls_shared_and_private_streams():
 
 
 def test_fused_plan_concurrent_streams_no_deadlock():
-    """Fused-plan launches (<= 8192 buffers) from six host threads on six
-    streams at once, each queueing twelve launches without synchronising:
-    the launches overlap on the GPU, and whichever workgroup of a launch runs
-    first must do its plan (a fixed planner workgroup could queue behind the
-    other launches' spinning workgroups: deadlock, then the poll bound's
-    trap).  Every result vs the oracle."""
+    """Small-batch launches (<= 8192 buffers) from six host threads on six
+    streams at once, each queueing twelve launches without synchronising,
+    so that the launches overlap on the GPU.  This once guarded the fused
+    plan's cross-workgroup wait; eager calls no longer wait across
+    workgroups, and the test keeps the overlap covered.  Every result vs the
+    oracle."""
     from concurrent.futures import ThreadPoolExecutor
     rnd = random.Random(123)
     total = 32 << 20

@@ -699,7 +699,13 @@ int zcrc32_batch_device(const void *const *d_ptrs, const uint64_t *d_lens, const
   std::unique_lock<std::mutex> lk;
   const int rc = stream_scratch(st, kScratchBatch, bytes, &scratch, &have, &lk);
   if (rc) return rc;
-  return batch_device_ws(d_ptrs, d_lens, d_seeds_or_null, d_out, n, scratch, have, st, true);
+  // Two-launch plan, not the fused one: the fused plan makes every workgroup
+  // but the planner spin on a flag another workgroup writes, and
+  // test_concurrent_device_calls_shared_and_private_streams aborted on it
+  // again (round 1, profiles/r01/v10/) after the planner-election fix.  No
+  // workgroup of the product kernels waits on another one now; the fused
+  // plan stays for the A/B tools (~15 us per small call).
+  return batch_device_ws(d_ptrs, d_lens, d_seeds_or_null, d_out, n, scratch, have, st, false);
 }
 
 int zcrc32_batch_device_strided(const void *d_base, uint64_t stride, uint64_t len, size_t n,
