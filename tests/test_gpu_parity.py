@@ -248,13 +248,12 @@ def test_dynamic_part_mixed_batches(shape):
     del host
 
 
-def test_fused_plan_back_to_back_vs_two_launch_path():
+def test_back_to_back_launches_vs_caller_scratch_path():
     """Many zcrc32_batch_device launches queued back to back on one stream,
     each with different lengths, the reused per-stream scratch and the
     dynamic work counter, must equal zcrc32_batch_device_ws with its own
-    scratch per call, and the oracle.  (Named for the fused plan that eager
-    calls used until round 1's last session; they now take the two-launch
-    plan, zcrc_runtime.hip zcrc32_batch_device.)"""
+    scratch per call, and the oracle.  (Until round 1's last session this
+    compared the fused plan, since removed, with the two-launch plan.)"""
     rnd = random.Random(31)
     total = 96 << 20
     mem = torch.randint(0, 256, (total,), dtype=torch.uint8, device=DEV)
@@ -494,13 +493,12 @@ def test_concurrent_device_calls_shared_and_private_streams():
         np.testing.assert_array_equal(got, exp, err_msg=f"job {k}")
 
 
-def test_fused_plan_concurrent_streams_no_deadlock():
+def test_small_batches_overlapping_on_six_streams():
     """Small-batch launches (<= 8192 buffers) from six host threads on six
     streams at once, each queueing twelve launches without synchronising,
-    so that the launches overlap on the GPU.  This once guarded the fused
-    plan's cross-workgroup wait; eager calls no longer wait across
-    workgroups, and the test keeps the overlap covered.  Every result vs the
-    oracle."""
+    so that the launches overlap on the GPU.  (Until round 1's last session
+    this guarded the fused plan's cross-workgroup wait, since removed.)
+    Every result vs the oracle."""
     from concurrent.futures import ThreadPoolExecutor
     rnd = random.Random(123)
     total = 32 << 20

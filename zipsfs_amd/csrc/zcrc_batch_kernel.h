@@ -287,71 +287,9 @@ __device__ uint64_t block_excl_scan(uint64_t v, uint64_t *s_tmp /* 16 */, uint64
   return off + inc - v;
 }
 
-// Fused plan (BatchArgs::plan_lens set; pointer form, n <= kPlanTile): the
-// first workgroup of the launch to run writes prefix[0..n], zeroes out[]
-// and the work counter, then publishes plan_epoch at *plan_flag with an
-// agent-scope release; the others poll the flag (one lane each).
-// "First to run" is decided by an atomic exchange of the epoch into a claim
-// word (plan_flag + 8): the planner is a running workgroup that waits for
-// nobody, so the wait is deadlock-free whatever else shares the GPU.  (With
-// "workgroup 0 plans", two fused launches on different streams deadlocked:
-// each one's spinning workgroups filled the CUs of the XCD the other's
-// workgroup 0 was queued for, and the poll bound fired.)
-// Saves the plan launch and the dependent-launch gap (~15 us per call for
-// config 2).  The poll is bounded: a flag that never arrives traps (a HIP
-// error at the next synchronisation) instead of hanging the device.
-__device__ __forceinline__ void fused_plan(const BatchArgs &args, uint32_t *s_lds) {
-  const uint32_t tid = threadIdx.x;
-  uint32_t *s_planner = s_lds + 64;  // past block_excl_scan's 16 words
-  if (tid == 0) {
-    const uint64_t prev =
-        __hip_atomic_exchange(args.plan_flag + 8, args.plan_epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    *s_planner = prev != args.plan_epoch ? 1u : 0u;
-  }
-  __syncthreads();
-  const bool planner = *s_planner != 0u;
-  __syncthreads();  // everyone has read it before the scan reuses LDS
-  if (planner) {
-    uint64_t *prefix = const_cast<uint64_t *>(args.prefix);
-    const uint64_t n = args.n;
-    uint64_t v[kPlanPerThread];
-    uint64_t acc = 0;
-#pragma unroll
-    for (uint32_t k = 0; k < kPlanPerThread; k++) {
-      const uint64_t idx = (uint64_t)tid * kPlanPerThread + k;
-      v[k] = idx < n ? args.plan_lens[idx] : 0;
-      if (idx < n) args.out[idx] = 0u;
-      acc += v[k];
-    }
-    uint64_t tot;
-    uint64_t run = block_excl_scan(acc, reinterpret_cast<uint64_t *>(s_lds), &tot);
-#pragma unroll
-    for (uint32_t k = 0; k < kPlanPerThread; k++) {
-      const uint64_t idx = (uint64_t)tid * kPlanPerThread + k;
-      if (idx < n) prefix[idx] = run;
-      run += v[k];
-      if (idx + 1 == n) prefix[n] = run;
-    }
-    if (tid == 0 && args.ctr) *args.ctr = 0u;
-    __syncthreads();
-    if (tid == 0) __hip_atomic_store(args.plan_flag, args.plan_epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-  } else {
-    if (tid == 0) {
-      uint32_t polls = 0;
-      while (__hip_atomic_load(args.plan_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != args.plan_epoch) {
-        __builtin_amdgcn_s_sleep(2);
-        if (++polls == (1u << 26)) __builtin_trap();
-      }
-    }
-    __syncthreads();
-  }
-  // No agent-scope acquire (buffer_inv sc1): issued by every wave it
-  // invalidated the XCD's L2 4096 times per launch (+32 us on config 2).
-  // None is needed: the dispatch itself invalidates L1/L2 at kernel start,
-  // no wave touches a prefix/out line before the flag, and the writer's
-  // release wrote its L2 back, so the first read of each line misses to
-  // memory and sees the plan.
-}
+// (A fused plan -- the first workgroup to run scanned the lengths and the
+// others waited on a flag -- was removed in round 1: no workgroup of this
+// kernel waits on another one.  DESIGN.md section 4, "Plan".)
 
 // ------------------------------------------------------------ the kernel
 
@@ -563,7 +501,6 @@ __global__ __launch_bounds__(kThreads) void crc32_batch_kernel(BatchArgs args) {
   const uint4 *comb_src = reinterpret_cast<const uint4 *>(tab->comb);
   const uint4 comb0 = comb_src[tid], comb1 = comb_src[tid + 1024u];
 
-  if (!kStrided && args.plan_lens) fused_plan(args, s_lds);
   const BatchView<kStrided> bv{args};
   const uint64_t total = bv.total();
   const uint64_t max_waves = (uint64_t)gridDim.x * kWaves;

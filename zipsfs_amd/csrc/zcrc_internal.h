@@ -53,12 +53,6 @@ struct BatchArgs {
   uint32_t *ctr;
   uint32_t dyn_shift;
   uint64_t dyn_unit;
-  // fused plan (pointer form, n <= kPlanTile; crc32_batch_kernel's
-  // fused_plan): lengths to scan into prefix (writable), the flag that
-  // publishes it and this launch's unique epoch.  nullptr: prefix is ready.
-  const uint64_t *plan_lens;
-  uint64_t *plan_flag;
-  uint64_t plan_epoch;
 };
 
 // t0/t1: optional events stamped with the kernel's own start and end

@@ -13,7 +13,7 @@ namespace zcrc {
 // Exclusive prefix over lengths: prefix[0..n] (prefix[n] = total), and zero
 // out[] (split pieces xor into it).  Tile = kPlanTile buffers per workgroup.
 
-// wave_incl_scan / block_excl_scan: zcrc_batch_kernel.h (the fused plan uses them too)
+// wave_incl_scan / block_excl_scan: zcrc_batch_kernel.h
 
 __global__ __launch_bounds__(1024) void plan_tile_sums(const uint64_t *lens, uint64_t n, uint64_t *tile_sum,
                                                        uint32_t *out) {

@@ -174,43 +174,22 @@ int stream_scratch(hipStream_t st, int use, size_t bytes, void **out, size_t *ha
   return ZCRC_OK;
 }
 
-// Epochs of fused-plan launches: unique per launch in this process and far
-// from the small integers stale scratch tends to hold (splitmix64 of a counter).
-uint64_t next_plan_epoch() {
-  static std::atomic<uint64_t> ctr{0};
-  uint64_t z = ctr.fetch_add(1, std::memory_order_relaxed) + 0x9E3779B97F4A7C15ull;
-  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
-  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
-  return (z ^ (z >> 31)) | 1u;
-}
-
-// fuse: batches of <= kPlanTile buffers scan their lengths inside the CRC
-// kernel (one launch instead of two).  Not for zcrc32_batch_device_ws: a
-// captured graph would replay one epoch, and the flag must change per launch.
 int batch_device_ws(const void *const *d_ptrs, const uint64_t *d_lens, const uint32_t *d_seeds,
-                    uint32_t *d_out, size_t n, void *scratch, size_t scratch_bytes, hipStream_t stream,
-                    bool fuse) {
+                    uint32_t *d_out, size_t n, void *scratch, size_t scratch_bytes, hipStream_t stream) {
   if (n == 0) return ZCRC_OK;
   if (!d_ptrs || !d_lens || !d_out || !scratch) return fail(ZCRC_ERR_ARG, "null argument");
   if (scratch_bytes < zcrc32_batch_device_scratch_bytes(n)) return fail(ZCRC_ERR_ARG, "scratch too small");
   DeviceCtx *dc = nullptr;
   int rc = device_ctx(&dc);
   if (rc) return rc;
-  // scratch: work counter (zeroed by the plan) and, 128 B further, the fused
-  // plan's flag and (64 B after it) its claim word (own kCtrBytes area) |
+  // scratch: work counter (zeroed by the plan; own kCtrBytes area) |
   // prefix[n+1] | tile sums.  The counter must not share a cache line with
   // the prefix, which every wave reads while claims hammer the counter.
   uint32_t *d_ctr = static_cast<uint32_t *>(scratch);
   uint64_t *d_prefix = reinterpret_cast<uint64_t *>(static_cast<uint8_t *>(scratch) + kCtrBytes);
   uint64_t *d_tiles = d_prefix + (n + 1);
+  ZCRC_HIP_TRY(launch_plan(d_lens, n, d_prefix, d_tiles, d_out, d_ctr, stream));
   BatchArgs a{};
-  if (fuse && n <= kPlanTile) {
-    a.plan_lens = d_lens;
-    a.plan_flag = reinterpret_cast<uint64_t *>(static_cast<uint8_t *>(scratch) + kCtrBytes / 2);
-    a.plan_epoch = next_plan_epoch();
-  } else {
-    ZCRC_HIP_TRY(launch_plan(d_lens, n, d_prefix, d_tiles, d_out, d_ctr, stream));
-  }
   a.ptrs = reinterpret_cast<const uint8_t *const *>(d_ptrs);
   a.prefix = d_prefix;
   a.seeds = d_seeds;
@@ -672,7 +651,7 @@ size_t zcrc32_batch_device_scratch_bytes(size_t n) { return 8 * (n + 1) + 8 * zc
 int zcrc32_batch_device_ws(const void *const *d_ptrs, const uint64_t *d_lens, const uint32_t *d_seeds_or_null,
                            uint32_t *d_out, size_t n, void *d_scratch, size_t scratch_bytes, void *stream) {
   return batch_device_ws(d_ptrs, d_lens, d_seeds_or_null, d_out, n, d_scratch, scratch_bytes,
-                         static_cast<hipStream_t>(stream), false);
+                         static_cast<hipStream_t>(stream));
 }
 
 int zcrc32_batch_device(const void *const *d_ptrs, const uint64_t *d_lens, const uint32_t *d_seeds_or_null,
@@ -684,11 +663,11 @@ int zcrc32_batch_device(const void *const *d_ptrs, const uint64_t *d_lens, const
   hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
   ZCRC_HIP_TRY(hipStreamIsCapturing(st, &cap));
   if (cap != hipStreamCaptureStatusNone) {
-    // inside graph capture: stream-ordered scratch, two-launch plan (a
-    // replayed graph cannot hand the fused plan a fresh epoch)
+    // inside graph capture: stream-ordered scratch (the per-stream cache
+    // would be frozen into the graph)
     void *scratch = nullptr;
     ZCRC_HIP_TRY(hipMallocAsync(&scratch, bytes, st));
-    const int rc = batch_device_ws(d_ptrs, d_lens, d_seeds_or_null, d_out, n, scratch, bytes, st, false);
+    const int rc = batch_device_ws(d_ptrs, d_lens, d_seeds_or_null, d_out, n, scratch, bytes, st);
     const hipError_t e = hipFreeAsync(scratch, st);
     if (rc) return rc;
     if (e != hipSuccess) return fail(ZCRC_ERR_HIP, std::string("hipFreeAsync: ") + hipGetErrorString(e));
@@ -699,13 +678,7 @@ int zcrc32_batch_device(const void *const *d_ptrs, const uint64_t *d_lens, const
   std::unique_lock<std::mutex> lk;
   const int rc = stream_scratch(st, kScratchBatch, bytes, &scratch, &have, &lk);
   if (rc) return rc;
-  // Two-launch plan, not the fused one: the fused plan makes every workgroup
-  // but the planner spin on a flag another workgroup writes, and
-  // test_concurrent_device_calls_shared_and_private_streams aborted on it
-  // again (round 1, profiles/r01/v10/) after the planner-election fix.  No
-  // workgroup of the product kernels waits on another one now; the fused
-  // plan stays for the A/B tools (~15 us per small call).
-  return batch_device_ws(d_ptrs, d_lens, d_seeds_or_null, d_out, n, scratch, have, st, false);
+  return batch_device_ws(d_ptrs, d_lens, d_seeds_or_null, d_out, n, scratch, have, st);
 }
 
 int zcrc32_batch_device_strided(const void *d_base, uint64_t stride, uint64_t len, size_t n,
