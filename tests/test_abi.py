@@ -149,3 +149,19 @@ def test_argument_errors_are_reported_not_computed():
     assert b"null" in lib.zcrc_last_error()
     assert lib.zcrc32_batch_device_scratch_bytes(8192) == 256 + 8 * 8193 + 8  # counter line | prefix | one plan tile
     assert lib.zcrc32_batch_device_scratch_bytes(8193) == 256 + 8 * 8194 + 16
+
+
+def test_no_kernel_waits_on_another_workgroup():
+    """No product kernel spins on a flag that another workgroup writes (the
+    fused plan did, and aborted a concurrent-streams GPU test; DESIGN.md
+    section 4, "Plan").  Such a wait needs a poll loop, so none of its
+    markers may appear in the kernel sources: a sleep, an atomic load, or a
+    trap as the loop's bound."""
+    csrc = os.path.join(ROOT, "zipsfs_amd", "csrc")
+    for f in sorted(os.listdir(csrc)):
+        if not f.endswith((".hip", ".h")):
+            continue
+        text = open(os.path.join(csrc, f)).read()
+        code = "\n".join(line.split("//")[0] for line in text.splitlines())
+        for marker in ("s_sleep", "__hip_atomic_load", "__builtin_trap", "__atomic_load"):
+            assert marker not in code, (f, marker)
