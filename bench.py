@@ -56,16 +56,17 @@ def zipf_lens(n: int) -> np.ndarray:
 class Workload:
     """Device buffers + descriptor tensors for this rank's shard."""
 
-    def __init__(self, cfg: int, rank: int, world: int, dev):
+    def __init__(self, cfg: int, rank: int, world: int, dev, n_override=None):
         import torch
         import zipsfs_amd as z
         self.cfg, self.rank, self.world = cfg, rank, world
         self.batches = []  # list of (ptrs, lens) device tensors
         self.mem = []
         if cfg in (3, 5):
-            n = 65536 if cfg == 3 else 131072
+            n = n_override or (65536 if cfg == 3 else 131072)
             L = 1 << 20
-            self.desc = f"config{cfg}: {n} x 1 MiB buffers per GPU (global buffer i on rank i mod N)"
+            self.desc = (f"config{cfg}: {n} x 1 MiB buffers per GPU, {n * world} in all "
+                         f"(global buffer i on rank i mod {world})")
             self._strided(n, L, pools=1, dev=dev)
         elif cfg == 2:
             n, L, pools = 4096, 65536, 16
@@ -126,61 +127,98 @@ def golden_check(cfg: int, glob: np.ndarray) -> str:
         idx, exp = np.arange(k), g["cfg2"][:k]
     elif cfg == 4:
         idx, exp = g["cfg4_idx"].astype(np.int64), g["cfg4"]
-    else:
-        return "no fixture for config 5 (see tests/test_gpu_parity.py)"
+    else:  # config 5: samples spread over [0, 2^20); check those this run holds
+        idx, exp = g["cfg5_idx"].astype(np.int64), g["cfg5"]
+        keep = idx < len(glob)
+        idx, exp = idx[keep], exp[keep]
+        if len(idx) < 256:
+            raise SystemExit(f"PARITY: only {len(idx)} config-5 samples fall inside {len(glob)} buffers")
     ok = int((glob[idx] == exp).sum())
     if ok != len(idx):
         raise SystemExit(f"PARITY FAILURE: {len(idx) - ok} of {len(idx)} sampled CRCs differ from the reference")
     return f"{ok}/{len(idx)} sampled CRCs equal the reference golden vectors"
 
 
-def cpu_baseline(cfg: int, budget_s: float) -> dict:
-    """Reference src/cg_crc32.c (oracle/_ref, -O2) on host cores, bounded sample."""
-    from oracle import oracle as o  # the only oracle use in bench.py
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
-    threads = max(1, min(threads, 64))
+def baseline_sample(cfg: int, sample_bytes: int) -> tuple:
+    """(lens, payload indices, description) of the CPU baseline's host sample:
+    the same synthetic buffers as the GPU workload, at least `sample_bytes`
+    in all, so that the sample is several times the host's L3."""
     if cfg in (3, 5):
-        nb, L = 512, 1 << 20
-        sample = f"512 x 1 MiB buffers of the same synthetic payload (512 MiB host-resident), {threads} threads"
-    elif cfg == 2:
-        nb, L = 4096, 65536
-        sample = f"4096 x 64 KiB buffers (256 MiB host-resident), {threads} threads"
-    else:
-        nb, L = 2000, None
-        sample = f"first 2000 config-4 buffers (host-resident), {threads} threads"
-    lens = zipf_lens(nb) if L is None else np.full(nb, L, dtype=np.int64)
-    bufs = [o.payload(int(lens[i]), i) for i in range(nb)]
-    ptrs = np.array([b.ctypes.data for b in bufs], dtype=np.uint64)
+        L = 1 << 20
+        nb = max(1, -(-sample_bytes // L))
+        return np.full(nb, L, dtype=np.int64), np.arange(nb), f"{nb} x 1 MiB buffers"
+    if cfg == 2:
+        L = 65536
+        nb = max(1, -(-sample_bytes // L))
+        return np.full(nb, L, dtype=np.int64), np.arange(nb), f"{nb} x 64 KiB buffers"
+    lens = zipf_lens(100000)
+    nb = int(np.searchsorted(np.cumsum(lens), sample_bytes)) + 1
+    nb = min(nb, 100000)
+    return lens[:nb], np.arange(nb), f"the first {nb} config-4 buffers"
+
+
+def cpu_baseline(cfg: int, budget_s: float, sample_gib: float) -> dict:
+    """The reference's src/cg_crc32.c (oracle/_ref) on this host's cores.
+
+    SURVEY 8(d): all allowed CPUs (pthread pool, round-robin buffer
+    ownership, wall clock over the sample) and one thread, each at -O2 and
+    at -O0 (as shipped, src/ZIPsFS.compile.sh:319), over a host-resident
+    sample of >= sample_gib GiB of the same payload."""
+    from oracle import oracle as o  # the only oracle use in bench.py
+    host = host_cpu()
+    threads = int(os.environ.get("ZCRC_BASELINE_THREADS", "0") or 0) or host["cpus_allowed"] or os.cpu_count() or 1
+    lens, idx, what = baseline_sample(cfg, int(sample_gib * GiB))
+    offs = np.zeros(len(lens), dtype=np.int64)
+    offs[1:] = np.cumsum((lens + 15) // 16 * 16)[:-1]
+    arena = np.empty(int(offs[-1] + lens[-1] + 16), dtype=np.uint8)
+    base = arena.ctypes.data
+    fill = o.port().oracle_fill_payload
+    for i in range(len(lens)):
+        fill(base + int(offs[i]), int(lens[i]), int(idx[i]), PAYLOAD_SEED)
+    ptrs = (base + offs).astype(np.uint64)
     ln = lens.astype(np.uint64)
     total = float(ln.sum())
     use_ref = o.ref_available()
     kind = "reference" if use_ref else "port"
-    fn = (lambda nt: o.ref_crc32_batch(ptrs, ln, None, nt)) if use_ref else (lambda nt: o.crc32_batch(ptrs, ln, None, nt))
-    fn(threads)  # warm
-    reps, t0 = 0, time.perf_counter()
-    while True:
-        fn(threads)
-        reps += 1
-        el = time.perf_counter() - t0
-        if el >= budget_s * 0.7 or reps >= 200:
-            break
-    rate = reps * total / el / GiB
-    # single core, for context
-    t1 = time.perf_counter()
-    fn(1)
-    single = total / (time.perf_counter() - t1) / GiB
-    o0 = None
-    if use_ref and o.ref_available(o0=True):
-        sub = max(1, nb // 8)
-        t2 = time.perf_counter()
-        o.ref_crc32_batch(ptrs[:sub], ln[:sub], None, 1, o0=True)
-        o0 = float(ln[:sub].sum()) / (time.perf_counter() - t2) / GiB
-    return {"value": round(rate, 3), "unit": "GiB/s", "cores": threads, "kind": kind,
-            "sample": sample + (" -- src/cg_crc32.c compiled -O2 by oracle/Makefile" if use_ref else
-                                " -- CPU restatement oracle/crc32_port.c -O2"),
-            "single_core_gibs": round(single, 3),
-            "single_core_O0_as_shipped_gibs": None if o0 is None else round(o0, 3),
-            "host": host_cpu()}
+
+    def run(nt: int, o0: bool, p=ptrs, l=ln):
+        return o.ref_crc32_batch(p, l, None, nt, o0=o0) if use_ref else o.crc32_batch(p, l, None, nt)
+
+    def rate(nt: int, o0: bool, budget: float) -> float:
+        run(nt, o0)  # warm: page in, spawn
+        reps, t0 = 0, time.perf_counter()
+        while True:
+            run(nt, o0)
+            reps += 1
+            el = time.perf_counter() - t0
+            if el >= budget or reps >= 100:
+                return reps * total / el / GiB
+
+    all_o2 = rate(threads, False, budget_s * 0.35)
+    all_o0 = rate(threads, True, budget_s * 0.2) if use_ref and o.ref_available(o0=True) else None
+    # one thread: a >= 1 GiB prefix of the sample (still > L3), one pass
+    k = max(1, int(np.searchsorted(np.cumsum(lens), min(total, GiB))) + 1)
+    sub_p, sub_l = ptrs[:k], ln[:k]
+    sub_total = float(sub_l.sum())
+
+    def one(o0: bool) -> float:
+        t0 = time.perf_counter()
+        run(1, o0, sub_p, sub_l)
+        return sub_total / (time.perf_counter() - t0) / GiB
+
+    one_o2 = one(False)
+    one_o0 = one(True) if use_ref and o.ref_available(o0=True) else None
+    r3 = lambda v: None if v is None else round(v, 3)
+    return {"value": r3(all_o2), "unit": "GiB/s", "cores": threads, "kind": kind,
+            "sample": (f"{what} ({total / GiB:.2f} GiB host-resident, same synthetic payload), {threads} threads, "
+                       "round-robin buffer ownership, wall clock per pass -- " +
+                       ("src/cg_crc32.c compiled -O2 by oracle/Makefile" if use_ref else
+                        "CPU restatement oracle/crc32_port.c -O2")),
+            "all_cores_O0_as_shipped_gibs": r3(all_o0),
+            "single_core_gibs": r3(one_o2),
+            "single_core_O0_as_shipped_gibs": r3(one_o0),
+            "single_core_sample_gib": round(sub_total / GiB, 3),
+            "host": host}
 
 
 def host_cpu() -> dict:
@@ -201,29 +239,107 @@ def host_cpu() -> dict:
     return {"model": model, "logical_cpus": os.cpu_count(), "cpus_allowed": allowed}
 
 
+def resolve_world(gpus, world_env) -> tuple:
+    """(world size, whether bench.py must start the ranks itself).
+
+    Under torchrun WORLD_SIZE is set and must equal --gpus when both are
+    given; without it, --gpus N > 1 means this process spawns N ranks."""
+    if world_env is not None:
+        world = int(world_env)
+        if gpus is not None and gpus != world:
+            raise SystemExit(f"bench.py: --gpus {gpus} but WORLD_SIZE={world}; they must agree")
+        return world, False
+    n = 1 if gpus is None else int(gpus)
+    if n < 1:
+        raise SystemExit("bench.py: --gpus must be >= 1")
+    return n, n > 1
+
+
+def free_port() -> int:
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return int(s.getsockname()[1])
+
+
+def rank_env(base: dict, rank: int, world: int, port: int) -> dict:
+    env = dict(base)
+    env.update({"RANK": str(rank), "LOCAL_RANK": str(rank), "WORLD_SIZE": str(world),
+                "LOCAL_WORLD_SIZE": str(world), "GROUP_RANK": "0", "MASTER_ADDR": "127.0.0.1",
+                "MASTER_PORT": str(port)})
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return env
+
+
+def spawn_ranks(world: int, argv: list) -> int:
+    """Start `world` fresh bench.py processes (one per GPU) and wait for them.
+
+    Rank 0 prints the JSON line; the exit code is the first non-zero child
+    code.  A failed rank stops the others (by their exact PIDs)."""
+    import subprocess
+    port = free_port()
+    cmd = [sys.executable, os.path.abspath(__file__)] + list(argv)
+    procs = [subprocess.Popen(cmd, env=rank_env(os.environ, r, world, port)) for r in range(world)]
+    rc = 0
+    try:
+        pending = list(procs)
+        while pending:
+            for p in list(pending):
+                code = p.poll()
+                if code is None:
+                    continue
+                pending.remove(p)
+                if code != 0 and rc == 0:
+                    rc = code if code > 0 else 1
+                    for q in pending:
+                        q.terminate()
+            time.sleep(0.05)
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+                p.wait()
+    return rc
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="ranks (one per GPU); without WORLD_SIZE in the env, bench.py starts them itself")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--config", type=int, default=3, choices=[2, 3, 4, 5])
+    ap.add_argument("--config", type=int, default=None, choices=[2, 3, 4, 5],
+                    help="SURVEY 8(d) config; default 3 at one rank, 5 (its per-GPU shard) at N>1")
+    ap.add_argument("--buffers-per-gpu", type=int, default=None,
+                    help="configs 3/5: override the per-GPU buffer count (rehearsals with ranks sharing a GPU)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="nccl = RCCL over xGMI (default); gloo only to rehearse ranks sharing one GPU")
     ap.add_argument("--cpu-budget-s", type=float, default=12.0)
+    ap.add_argument("--cpu-sample-gib", type=float, default=4.0,
+                    help="host-resident CPU-baseline sample (>= 2x the host L3)")
     ap.add_argument("--pmc-traffic-bytes", type=float, default=None,
                     help="HBM bytes per launch from a separate rocprofv3 --pmc pass (corrected)")
     args = ap.parse_args()
+    world, spawn_needed = resolve_world(args.gpus, os.environ.get("WORLD_SIZE"))
+    if spawn_needed:
+        # no launcher: start the ranks here, before this process touches torch
+        # or the GPU (children are fresh interpreters, never an exec of this one)
+        sys.exit(spawn_ranks(world, sys.argv[1:]))
+    if args.config is None:
+        args.config = 3 if world == 1 else 5
 
     import torch
     import torch.distributed as dist
     import zipsfs_amd as z
     from zipsfs_amd import shard
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    ndev = torch.cuda.device_count()
+    ndev = torch.cuda.device_count()  # does not initialise the GPU on this image
+    if world > 1 and args.dist_backend == "nccl" and world > ndev:
+        raise SystemExit(f"bench.py: {world} ranks over RCCL need {world} GPUs, {ndev} visible "
+                         "(--dist-backend gloo rehearses ranks sharing a GPU)")
     gpu = local % max(ndev, 1)
     torch.cuda.set_device(gpu)
     dev = torch.device("cuda", gpu)
@@ -240,7 +356,7 @@ def main() -> None:
             else:
                 dist.barrier()
 
-    wl = Workload(args.config, rank, world, dev)
+    wl = Workload(args.config, rank, world, dev, args.buffers_per_gpu)
     out = torch.empty(wl.n_local, dtype=torch.int32, device=dev)
     result = {"global": out}
 
@@ -297,7 +413,7 @@ def main() -> None:
             traffic_src = pm["source"]
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(args.config, args.cpu_budget_s)
+        cpu = cpu_baseline(args.config, args.cpu_budget_s, args.cpu_sample_gib)
 
     if rank == 0:
         line = {

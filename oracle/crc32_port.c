@@ -189,9 +189,9 @@ static void *batch_worker(void *arg) {
 static int run_batch(crc_fn_t fn, const uint8_t *const *ptrs, const uint64_t *lens,
                      const uint32_t *seeds, uint32_t *out, uint64_t n, int nthreads) {
   if (nthreads < 1) nthreads = 1;
-  if (nthreads > 256) nthreads = 256;
-  pthread_t th[256];
-  batch_job_t jobs[256];
+  if (nthreads > 1024) nthreads = 1024;
+  pthread_t th[1024];
+  batch_job_t jobs[1024];
   for (int t = 0; t < nthreads; t++) {
     jobs[t] = (batch_job_t){ptrs, lens, seeds, out, n, t, nthreads, fn};
     if (t && pthread_create(&th[t], NULL, batch_worker, &jobs[t]) != 0) return -1;

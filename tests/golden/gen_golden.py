@@ -85,8 +85,17 @@ def main() -> None:
     big = [i for i in range(100000) if zl[i] >= (1 << 20)]
     cfg4_idx = np.array(sorted(set(rnd.sample(range(100000), 1000)) | set(big[:24])), dtype=np.uint64)
     cfg4 = np.array([ref(o.payload(int(zl[i]), int(i)).tobytes()) for i in cfg4_idx], dtype=np.uint32)
+    # config 5: 1M x 1 MiB over 8 GPUs (buffer i on rank i mod N).  256
+    # samples in each of [0,2^15), [2^15,2^16), ..., [2^19,2^20), so that runs
+    # with fewer ranks or fewer buffers per rank still hold >= 256 of them.
+    r5 = random.Random(5)
+    cfg5_idx = []
+    for lo, hi in [(0, 1 << 15)] + [(1 << k, 1 << (k + 1)) for k in range(15, 20)]:
+        cfg5_idx += r5.sample(range(lo, hi), 256)
+    cfg5_idx = np.array(sorted(cfg5_idx), dtype=np.uint64)
+    cfg5 = np.array([ref(o.payload(1 << 20, int(i)).tobytes()) for i in cfg5_idx], dtype=np.uint32)
     np.savez_compressed(os.path.join(HERE, "configs.npz"), cfg2=cfg2, cfg3_idx=cfg3_idx, cfg3=cfg3,
-                        cfg4_idx=cfg4_idx, cfg4_len=zl[cfg4_idx], cfg4=cfg4)
+                        cfg4_idx=cfg4_idx, cfg4_len=zl[cfg4_idx], cfg4=cfg4, cfg5_idx=cfg5_idx, cfg5=cfg5)
 
     meta = {
         "generator": "tests/golden/gen_golden.py",

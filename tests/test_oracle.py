@@ -60,6 +60,12 @@ def test_configs(golden):
         assert o.payload_crc(1 << 20, int(i)) == c
     for i, L, c in zip(cfg["cfg4_idx"][:64], cfg["cfg4_len"][:64], cfg["cfg4"][:64]):
         assert o.payload_crc(int(L), int(i)) == c
+    # config 5: 1536 samples, 256 per octave of [0, 2^20)
+    idx5 = cfg["cfg5_idx"].astype(np.int64)
+    assert len(idx5) == 1536 and len(set(idx5.tolist())) == 1536 and idx5.max() < (1 << 20)
+    assert int((idx5 < (1 << 15)).sum()) == 256 and int((idx5 >= (1 << 19)).sum()) == 256
+    for i, c in zip(cfg["cfg5_idx"][::96], cfg["cfg5"][::96]):
+        assert o.payload_crc(1 << 20, int(i)) == c
 
 
 def test_zipf_pinned_totals(golden):

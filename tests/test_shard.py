@@ -59,3 +59,71 @@ def test_shard_partition_covers_all():
         for n in (0, 1, 7, 1000):
             allidx = np.concatenate([shard.shard_indices(n, r, world) for r in range(world)])
             assert sorted(allidx.tolist()) == list(range(n))
+
+
+# ----------------------------------------------------------- bench launcher
+
+def _bench():
+    import importlib.util
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    spec = importlib.util.spec_from_file_location("bench_under_test", os.path.join(root, "bench.py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod
+
+
+def test_bench_world_resolution():
+    """--gpus N without a launcher spawns N ranks; under torchrun WORLD_SIZE
+    must agree with --gpus (--gpus was silently ignored)."""
+    b = _bench()
+    assert b.resolve_world(None, None) == (1, False)
+    assert b.resolve_world(1, None) == (1, False)
+    assert b.resolve_world(8, None) == (8, True)
+    assert b.resolve_world(None, "4") == (4, False)
+    assert b.resolve_world(4, "4") == (4, False)
+    with pytest.raises(SystemExit):
+        b.resolve_world(8, "2")
+    with pytest.raises(SystemExit):
+        b.resolve_world(0, None)
+    env = b.rank_env({"X": "1"}, 3, 8, 29500)
+    assert env["RANK"] == env["LOCAL_RANK"] == "3" and env["WORLD_SIZE"] == "8"
+    assert env["MASTER_ADDR"] == "127.0.0.1" and env["MASTER_PORT"] == "29500" and env["X"] == "1"
+    assert env["HSA_ENABLE_IPC_MODE_LEGACY"] == "0"
+
+
+def test_bench_config5_golden_in_global_order():
+    """The config-5 parity check reads the gathered CRCs in global order and
+    needs >= 256 fixture samples inside the run's buffers."""
+    b = _bench()
+    g = np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "configs.npz"))
+    n_total = 2 * 32768
+    glob = np.zeros(n_total, dtype=np.uint32)
+    idx = g["cfg5_idx"].astype(np.int64)
+    keep = idx < n_total
+    glob[idx[keep]] = g["cfg5"][keep]
+    assert b.golden_check(5, glob).startswith(f"{int(keep.sum())}/{int(keep.sum())}")
+    glob[idx[keep][0]] ^= 1
+    with pytest.raises(SystemExit):
+        b.golden_check(5, glob)
+    with pytest.raises(SystemExit):  # too few samples inside a tiny run
+        b.golden_check(5, np.zeros(1000, dtype=np.uint32))
+
+
+def test_bench_spawn_ranks_exit_codes(tmp_path):
+    """spawn_ranks starts fresh interpreters with the rank env and returns
+    the first failing rank's code (script stands in for bench.py)."""
+    b = _bench()
+    script = tmp_path / "fake_bench.py"
+    script.write_text("import os, sys\n"
+                      "r = int(os.environ['RANK'])\n"
+                      "open(os.path.join(sys.argv[1], f'rank{r}'), 'w').write(os.environ['WORLD_SIZE'])\n"
+                      "sys.exit(int(sys.argv[2]) if r == 1 else 0)\n")
+    orig = b.__file__
+    try:
+        b.__file__ = str(script)
+        assert b.spawn_ranks(3, [str(tmp_path), "0"]) == 0
+        assert sorted(p.name for p in tmp_path.glob("rank*")) == ["rank0", "rank1", "rank2"]
+        assert (tmp_path / "rank2").read_text() == "3"
+        assert b.spawn_ranks(2, [str(tmp_path), "7"]) == 7
+    finally:
+        b.__file__ = orig
