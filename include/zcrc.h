@@ -17,11 +17,11 @@
  * of a previous call (0 for a fresh CRC) -- bit-exact to src/cg_crc32.c.
  *
  * Errors.  The reference has no error path (src/cg_crc32.c always returns).
- * This engine has NO CPU fallback: every CRC is computed on the GPU.
- * Functions returning int return 0 on success and a negative code on
- * failure (zcrc_last_error() gives the text); zcrc32() itself cannot report
- * an error through its return value, so on a GPU failure it prints the
- * reason to stderr and aborts -- loudly, never a silent wrong answer.
+ * Every batched and device-resident entry point computes on the GPU only;
+ * functions returning int return 0 on success and a negative code on
+ * failure (zcrc_last_error() gives the text), never a CPU answer.  The one
+ * exception is the drop-in zcrc32(), which like cg_crc32 cannot fail: see
+ * "Drop-in contract" below.
  *
  * Threading: all functions are thread-safe; device initialisation happens
  * once per process (pthread_once semantics).  Host-pointer functions are
@@ -44,10 +44,25 @@ extern "C" {
 #define ZCRC_ERR_TOO_BIG (-3)  /* one launch limited to 4 TiB of payload        */
 
 /* Replaces cg_crc32(data, n_bytes, crc, mutex), src/cg_crc32.c:26.
- * `data` is host memory, borrowed for the call.  Aborts on GPU failure. */
+ * `data` is host memory, borrowed for the call.
+ *
+ * Drop-in contract: zcrc32 never fails and never aborts -- the
+ * caller holds mutex_fhandle (src/ZIPsFS_preloadfileram.c:309-321).  Entries
+ * of at least zcrc32_set_gpu_min_bytes() bytes (env ZCRC_GPU_MIN_BYTES; the
+ * default is the measured host/GPU crossover) are checksummed
+ * on the GPU; smaller ones, and any call whose GPU attempt fails (no device,
+ * HIP error), are answered by libzcrc's own host CRC-32 (PCLMUL folding,
+ * zcrc_host.cpp).  The first fallback is reported on stderr; all are counted
+ * by zcrc32_dropin_stats. */
 uint32_t zcrc32(const void *data, size_t n_bytes, uint32_t crc);
+/* Sets the drop-in's GPU threshold (bytes); returns the previous value. */
+size_t zcrc32_set_gpu_min_bytes(size_t min_bytes);
+/* Drop-in calls so far: answered on the GPU / on the host below the
+ * threshold / on the host after a GPU failure.  Any pointer may be NULL. */
+void zcrc32_dropin_stats(uint64_t *gpu_calls, uint64_t *host_calls, uint64_t *fallback_calls);
 
-/* Same as zcrc32 but reports failure instead of aborting. */
+/* The GPU path of zcrc32 alone: reports failure instead of answering from
+ * the host (ZCRC_ERR_*), whatever the size. */
 int zcrc32_checked(const void *data, size_t n_bytes, uint32_t crc, uint32_t *out_crc);
 
 /* Host-resident batch: out[i] = crc32(seeds ? seeds[i] : 0, ptrs[i], lens[i]).

@@ -79,8 +79,11 @@ def test_dropin_compiles(tmp_path, compiler, lang):
 def test_product_has_no_cpu_crc_path():
     """The shipped package must not import the oracle or compute CRCs on the CPU.
 
-    Source files may not reference the oracle; Python modules may import zlib
-    only for inflate and never call a zlib/binascii checksum (AST check)."""
+    Source files may not reference the oracle or the reference build; Python
+    modules may import zlib only for inflate and never call a zlib/binascii
+    checksum (AST check).  The C library's one host CRC (zcrc_host.cpp) is
+    reachable only from the drop-in zcrc32(): no other source
+    calls host_crc32."""
     import ast
     pkg = os.path.join(ROOT, "zipsfs_amd")
     banned_attrs = {"crc32", "adler32", "crc_hqx", "crc32_combine"}
@@ -107,6 +110,18 @@ def test_product_has_no_cpu_crc_path():
                     if isinstance(node, ast.Attribute) and isinstance(node.value, ast.Name):
                         if node.value.id in aliases:
                             assert node.attr not in banned_attrs, (f, node.attr)
+    callers = {}
+    csrc = os.path.join(pkg, "csrc")
+    for f in os.listdir(csrc):
+        if f.endswith((".hip", ".h", ".cpp")):
+            text = "\n".join(l.split("//")[0] for l in open(os.path.join(csrc, f)).read().splitlines())
+            if "host_crc32(" in text:
+                callers[f] = text
+    assert set(callers) == {"zcrc_host.cpp", "zcrc_internal.h", "zcrc_runtime.hip"}, sorted(callers)
+    rt = callers["zcrc_runtime.hip"]
+    body = rt[rt.index("uint32_t zcrc32(const void *data"):]
+    body = body[:body.index("\n}\n")]
+    assert rt.count("host_crc32(") == body.count("host_crc32(") == 2  # below threshold or no device; GPU failure
 
 
 def test_missing_gpu_fails_loudly():
@@ -165,3 +180,67 @@ def test_no_kernel_waits_on_another_workgroup():
         code = "\n".join(line.split("//")[0] for line in text.splitlines())
         for marker in ("s_sleep", "__hip_atomic_load", "__builtin_trap", "__atomic_load"):
             assert marker not in code, (f, marker)
+
+
+# ------------------------------------------------- drop-in contract (8(b))
+
+def _dropin_lib():
+    import ctypes
+    lib = _lib.lib()
+    return lib, ctypes
+
+
+def test_host_crc_pinned_by_golden_vectors():
+    """The drop-in's host CRC (zcrc_host.cpp) against the reference-generated
+    fixtures: every length 0..4096 at 16 offsets, seeds/chains, KATs, 1 MiB."""
+    import json
+    import numpy as np
+    from oracle import oracle as o
+    lib, ctypes = _dropin_lib()
+    old = lib.zcrc32_set_gpu_min_bytes(ctypes.c_size_t(-1).value)  # everything on the host
+    try:
+        g = os.path.join(ROOT, "tests", "golden")
+        lo = np.load(os.path.join(g, "lengths_offsets.npz"))
+        base = o.payload(int(lo["payload_len"]), int(lo["payload_index"]))
+        addr = base.ctypes.data
+        for a, L in enumerate(lo["lengths"]):
+            for off in range(16):
+                assert lib.zcrc32(addr + off, int(L), 0) == lo["crc"][a, off], (int(L), off)
+        meta = json.load(open(os.path.join(g, "golden.json")))
+        for c in meta["chains"]:
+            d = o.payload(c["len"], c["index"])
+            assert lib.zcrc32(d.ctypes.data, c["len"], c["seed"]) == c["crc"]
+            cut = c["cut"]
+            mid = lib.zcrc32(d.ctypes.data, cut, c["seed"])
+            assert lib.zcrc32(d.ctypes.data + cut, c["len"] - cut, mid) == c["crc"]
+        d = o.payload(meta["config1"]["len"], meta["config1"]["index"])
+        assert lib.zcrc32(d.ctypes.data, d.size, 0) == meta["config1"]["crc"]
+        assert lib.zcrc32(b"123456789", 9, 0) == 0xCBF43926
+        assert lib.zcrc32(None, 0, 0x1234) == 0x1234
+        gpu, host, fb = (ctypes.c_uint64() for _ in range(3))
+        lib.zcrc32_dropin_stats(ctypes.byref(gpu), ctypes.byref(host), ctypes.byref(fb))
+        assert host.value > 24000
+    finally:
+        lib.zcrc32_set_gpu_min_bytes(old)
+
+
+def test_dropin_never_aborts_without_gpu(tmp_path):
+    """ZIPsFS's call site (fhandle_check_crc32 shape) built against the
+    drop-in, run with no visible GPU: every golden CRC comes back -- the
+    entry above the GPU threshold through the counted fallback -- and a
+    wrong expected CRC is reported as a mismatch, not a crash."""
+    import dropin_util as du
+    exe = du.build_harness(tmp_path)
+    recs = du.golden_records(big=True)
+    path = tmp_path / "recs.bin"
+    du.write_records(path, recs)
+    rc, rows, stats, err = du.run_harness(exe, path, {"HIP_VISIBLE_DEVICES": "", "ROCR_VISIBLE_DEVICES": ""})
+    assert rc == 0, err
+    assert len(rows) == len(recs) and all(ok for _, _, ok in rows)
+    assert [crc for _, crc, _ in rows] == [c & 0xFFFFFFFF for _, c, _ in recs]
+    assert stats["gpu"] == 0 and stats["fallback"] == 1 and stats["host"] == len(recs) - 1
+    assert "answering from the host CRC" in err
+    bad = [(b"123456789", 0xCBF43927, 0)]
+    du.write_records(tmp_path / "bad.bin", bad)
+    rc, rows, _, err = du.run_harness(exe, tmp_path / "bad.bin", {"HIP_VISIBLE_DEVICES": ""})
+    assert rc == 1 and rows == [(0, 0xCBF43926, False)] and "crc32-mismatch" in err

@@ -1,8 +1,9 @@
 """ctypes binding of the in-tree libzcrc.so (include/zcrc.h).
 
-The library is the product: every CRC is computed by its HIP kernels.  If
-the .so is missing or a GPU call fails, the functions here raise -- there is
-no CPU fallback anywhere in this package.
+The library is the product: every CRC this package returns is computed by
+its HIP kernels.  If the .so is missing or a GPU call fails, the functions
+here raise -- there is no CPU fallback anywhere in this package (only the C
+drop-in zcrc32() answers from libzcrc's host CRC).
 """
 from __future__ import annotations
 
@@ -28,6 +29,8 @@ _c_int = ctypes.c_int
 _SIGNATURES = {
     "zcrc32": (_c_u32, [_c_p, _c_sz, _c_u32]),
     "zcrc32_checked": (_c_int, [_c_p, _c_sz, _c_u32, ctypes.POINTER(_c_u32)]),
+    "zcrc32_set_gpu_min_bytes": (_c_sz, [_c_sz]),
+    "zcrc32_dropin_stats": (None, [ctypes.POINTER(_c_u64)] * 3),
     "zcrc32_batch": (_c_int, [_c_p, _c_p, _c_p, _c_p, _c_sz, ctypes.c_uint]),
     "zcrc32_batch_device": (_c_int, [_c_p, _c_p, _c_p, _c_p, _c_sz, _c_p]),
     "zcrc32_batch_device_scratch_bytes": (_c_sz, [_c_sz]),

@@ -6,7 +6,8 @@
  * (fhandle_check_crc32, src/ZIPsFS_preloadfileram.c:243).  This file keeps
  * the reference's include guard (src/cg_crc32.c:1-2) and the exact static
  * signature (src/cg_crc32.c:26) and forwards to libzcrc, which computes the
- * CRC on the MI355X (zlib crc32 semantics, bit-exact to the reference).
+ * CRC (zlib crc32 semantics, bit-exact to the reference): on the MI355X for
+ * entries of at least the GPU threshold, on libzcrc's host CRC below it.
  *
  * Build change on the ZIPsFS side: put this directory
  * before src/ on the include path, add -I<repo>/include and
@@ -15,7 +16,8 @@
  * `mutex` only guarded the reference's lazy table initialisation
  * (src/cg_crc32.c:31-36); libzcrc initialises its device tables once per
  * process internally, so the argument is accepted and unused.
- * There is no CPU fallback: on a GPU failure zcrc32() reports and aborts.
+ * Like the reference, this never fails: zcrc32() answers from libzcrc's
+ * host CRC when the GPU cannot (include/zcrc.h, "Drop-in contract").
  */
 #ifndef _cg_crc32_dot_c
 #define _cg_crc32_dot_c

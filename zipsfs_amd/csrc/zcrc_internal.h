@@ -88,6 +88,11 @@ namespace zcrc {
 // record an error for zcrc_last_error() (this thread) and return `code`
 int set_error(int code, const char *msg);
 
+// libzcrc's host CRC-32 (zcrc_host.cpp): zlib crc32(crc, data, n) on the CPU,
+// used only by the drop-in zcrc32() (include/zcrc.h, "Drop-in contract")
+uint32_t host_crc32(const void *data, size_t n, uint32_t crc);
+bool host_crc32_uses_clmul();
+
 hipError_t launch_fill_synthetic(const uint64_t *d_ptrs, const uint64_t *d_lens, uint64_t n, uint64_t index0,
                                  uint64_t index_step, uint64_t seed, hipStream_t stream);
 }  // namespace zcrc

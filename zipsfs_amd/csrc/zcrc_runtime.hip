@@ -2,9 +2,11 @@
 //
 // Owns: per-device table upload (once, thread-safe), per-thread pinned staging
 // for host-resident batches, stream-ordered scratch for device batches, and
-// optional HIP-event profiling of the main kernel.  There is deliberately no
-// CPU CRC anywhere in this library: every byte is checksummed on the GPU and
-// every failure is reported (or, for the void-error zcrc32(), aborts).
+// optional HIP-event profiling of the main kernel.  Every batched and
+// device-resident entry point checksums on the GPU and reports failures; only
+// the drop-in zcrc32() answers from the host CRC (zcrc_host.cpp) -- below its
+// size threshold and when the GPU fails -- because the function it replaces
+// cannot fail.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdio.h>
@@ -610,6 +612,35 @@ int stream_update(zcrc32_stream *s, const uint8_t *data, size_t n) {
 }  // namespace
 }  // namespace zcrc
 
+// ----- drop-in contract: zcrc32() always answers.
+// Entries below the GPU threshold go to the host CRC (a PCIe round trip
+// costs more than the core needs); larger ones go to the GPU, and any HIP
+// failure (no device, pinned allocation, launch, a reset device) is answered
+// from the host CRC as well, reported once on stderr and counted.
+namespace zcrc {
+namespace {
+constexpr size_t kDefaultGpuMinBytes = 32ull << 20;  // measured crossover, DESIGN.md 10b
+std::atomic<size_t> g_gpu_min{SIZE_MAX};
+std::atomic<int> g_no_device{0};  // the first GPU attempt found no usable device
+std::atomic<uint64_t> g_dropin_gpu{0}, g_dropin_host{0}, g_dropin_fallback{0};
+std::once_flag g_gpu_min_once;
+
+size_t gpu_min_bytes() {
+  std::call_once(g_gpu_min_once, [] {
+    size_t v = kDefaultGpuMinBytes;
+    if (const char *e = getenv("ZCRC_GPU_MIN_BYTES")) {
+      char *end = nullptr;
+      const unsigned long long x = strtoull(e, &end, 0);
+      if (end != e) v = (size_t)x;
+    }
+    size_t expect = SIZE_MAX;
+    g_gpu_min.compare_exchange_strong(expect, v);  // a setter call may have come first
+  });
+  return g_gpu_min.load(std::memory_order_relaxed);
+}
+}  // namespace
+}  // namespace zcrc
+
 // ================================================================= C ABI
 
 using namespace zcrc;
@@ -630,14 +661,34 @@ int zcrc32_checked(const void *data, size_t n_bytes, uint32_t crc, uint32_t *out
 }
 
 uint32_t zcrc32(const void *data, size_t n_bytes, uint32_t crc) {
+  if (n_bytes && !data) return crc;  // nothing readable: the CRC of no bytes
+  if (n_bytes < gpu_min_bytes() || g_no_device.load(std::memory_order_relaxed)) {
+    g_dropin_host.fetch_add(1, std::memory_order_relaxed);
+    return host_crc32(data, n_bytes, crc);
+  }
   uint32_t r = 0;
   const int rc = zcrc32_checked(data, n_bytes, crc, &r);
-  if (rc != ZCRC_OK) {
-    fprintf(stderr, "libzcrc: GPU CRC-32 failed (%d): %s -- aborting (no CPU fallback)\n", rc,
-            t_last_error.c_str());
-    abort();
+  if (rc == ZCRC_OK) {
+    g_dropin_gpu.fetch_add(1, std::memory_order_relaxed);
+    return r;
   }
-  return r;
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) g_no_device.store(1);
+  if (g_dropin_fallback.fetch_add(1, std::memory_order_relaxed) == 0)
+    fprintf(stderr, "libzcrc: GPU CRC-32 failed (%d: %s); answering from the host CRC%s\n", rc,
+            t_last_error.c_str(), g_no_device.load() ? " from now on (no device)" : "");
+  return host_crc32(data, n_bytes, crc);
+}
+
+size_t zcrc32_set_gpu_min_bytes(size_t min_bytes) {
+  (void)gpu_min_bytes();
+  return g_gpu_min.exchange(min_bytes);
+}
+
+void zcrc32_dropin_stats(uint64_t *gpu_calls, uint64_t *host_calls, uint64_t *fallback_calls) {
+  if (gpu_calls) *gpu_calls = g_dropin_gpu.load();
+  if (host_calls) *host_calls = g_dropin_host.load();
+  if (fallback_calls) *fallback_calls = g_dropin_fallback.load();
 }
 
 int zcrc32_batch(const void *const *ptrs, const size_t *lens, const uint32_t *seeds_or_null, uint32_t *out,
