@@ -16,7 +16,8 @@ import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
-BIG = 40 << 20  # above the drop-in's default GPU threshold (32 MiB)
+BIG = 40 << 20  # above the drop-in's default GPU threshold
+DEFAULT_GPU_MIN = 4 << 20  # zcrc_runtime.hip kDefaultGpuMinBytes
 
 
 def build_harness(tmp_path) -> str:

@@ -37,7 +37,7 @@ def test_dropin_executable_default_threshold(tmp_path):
     rc, rows, stats, err = du.run_harness(exe, path, {})
     assert rc == 0, err
     assert [crc for _, crc, _ in rows] == [c & 0xFFFFFFFF for _, c, _ in recs]
-    n_big = sum(1 for d, _, _ in recs if len(d) >= (32 << 20))
+    n_big = sum(1 for d, _, _ in recs if len(d) >= du.DEFAULT_GPU_MIN)
     assert stats == {"gpu": n_big, "host": len(recs) - n_big, "fallback": 0}, stats
 
 

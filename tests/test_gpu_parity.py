@@ -439,6 +439,24 @@ def test_zip_verify_batched(device):
     assert bad[deflated[0].name] in (zv.ZIP_MISMATCH, zv.ZIP_INFLATE_ERROR)
 
 
+@pytest.mark.parametrize("device", [True, False])
+def test_zip_verify_crafted_zip64_sizes(device):
+    """A deflated entry whose ZIP64 extra field claims 2^64 - 16 bytes
+    (the arena size wrapped) is inflated into bounded room and
+    reported as a mismatch -- no fault, no out-of-bounds write; an honest
+    entry in the same form verifies."""
+    from zipsfs_amd import zipverify as zv
+    from test_zip import crafted_zip
+    data = o.payload(70_000, 5).tobytes()
+    res = zv.verify(crafted_zip(data, 8, usize64=0xFFFFFFFFFFFFFFF0), device=device)
+    assert res[0].status == zv.ZIP_MISMATCH and res[0].inflate_status == 0
+    assert res[0].crc_computed == zlib.crc32(data)  # CRC of what the stream really holds
+    res = zv.verify(crafted_zip(data, 8, usize64=len(data)), device=device)
+    assert res[0].status == zv.ZIP_OK and res[0].crc_computed == zlib.crc32(data)
+    res = zv.verify(crafted_zip(data, 0, lho64=0xFFFFFFFFFFFFFFE2), device=device)
+    assert res[0].status == zv.ZIP_BAD
+
+
 def test_concurrent_host_threads_dropin():
     """ZIPsFS runs one preload thread per root (src/ZIPsFS_async.c:468); the
     drop-in must be thread-safe: many threads, each with its own staging."""
@@ -533,3 +551,24 @@ def test_small_batches_overlapping_on_six_streams():
             ap = np.array([host.ctypes.data + q for q in offs], dtype=np.uint64)
             exp = o.crc32_batch(ap, np.array(ln, dtype=np.uint64), np.zeros(len(ln), dtype=np.uint32), nthreads=8)
             np.testing.assert_array_equal(got, exp, err_msg=f"thread {t} job {j}")
+
+
+def test_wrapper_argument_validation():
+    """Short or mistyped out/seeds tensors are refused before any launch
+    (they let the kernel read or write past device memory)."""
+    mem = torch.zeros(1 << 16, dtype=torch.uint8, device=DEV)
+    ptrs = mem.data_ptr() + torch.arange(8, dtype=torch.int64, device=DEV) * 1024
+    lens = torch.full((8,), 1024, dtype=torch.int64, device=DEV)
+    with pytest.raises(ValueError):
+        z.crc32_batch_device(ptrs, lens, out=torch.empty(7, dtype=torch.int32, device=DEV))
+    with pytest.raises(ValueError):
+        z.crc32_batch_device(ptrs, lens, seeds=torch.zeros(7, dtype=torch.int32, device=DEV))
+    with pytest.raises(ValueError):
+        z.crc32_batch_device(ptrs, lens, seeds=torch.zeros(8, dtype=torch.int64, device=DEV))
+    scratch = torch.empty(z.crc32.scratch_bytes(8), dtype=torch.uint8, device=DEV)
+    with pytest.raises(ValueError):
+        z.crc32_batch_device_ws(ptrs, lens[:7], scratch)
+    with pytest.raises(ValueError):
+        z.crc32_batch_strided(mem, 1024, 1024, 8, out=torch.empty(4, dtype=torch.int32, device=DEV))
+    got = u32(z.crc32_batch_device(ptrs, lens))
+    assert (got == zlib.crc32(bytes(1024))).all()

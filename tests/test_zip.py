@@ -70,3 +70,58 @@ def test_malformed_archives():
     ents = zv.scan(bytes(data))
     assert ents[0].status == zv.ZIP_BAD
     assert all(e.status != zv.ZIP_BAD for e in ents[1:])
+
+
+# ------------------------------------------- crafted archives
+import struct  # noqa: E402
+import zlib  # noqa: E402
+
+SAT = 0xFFFFFFFF
+
+
+def crafted_zip(data: bytes, method: int, *, usize64=None, lho64=None, z64_locator_off=None) -> bytes:
+    """One-entry archive written by hand.  usize64 / lho64 put that value in
+    a ZIP64 extra field (header field saturated); z64_locator_off adds a ZIP64
+    EOCD locator pointing there."""
+    payload = zlib.compress(data)[2:-4] if method == 8 else data
+    crc = zlib.crc32(data)
+    name = b"e.bin"
+    local = struct.pack("<IHHHHHIIIHH", 0x04034B50, 20, 0, method, 0, 0, crc, len(payload), len(data), len(name), 0)
+    body = local + name + payload
+    extra = b""
+    fields = []
+    usize = len(data)
+    lho = 0
+    if usize64 is not None:
+        usize = SAT
+        fields.append(usize64)
+    if lho64 is not None:
+        lho = SAT
+        fields.append(lho64)
+    if fields:
+        extra = struct.pack("<HH", 1, 8 * len(fields)) + b"".join(struct.pack("<Q", v) for v in fields)
+    central = struct.pack("<IHHHHHHIIIHHHHHII", 0x02014B50, 45, 45, 0, method, 0, 0, crc, len(payload), usize,
+                          len(name), len(extra), 0, 0, 0, 0, lho) + name + extra
+    cd_off = len(body)
+    tail = b""
+    if z64_locator_off is not None:
+        tail = struct.pack("<IIQI", 0x07064B50, 0, z64_locator_off, 1)
+    eocd = struct.pack("<IHHHHIIH", 0x06054B50, 0, 0, 1, 1, len(central), cd_off, 0)
+    return body + central + tail + eocd
+
+
+def test_crafted_zip64_fields_never_wrap():
+    from zipsfs_amd import ZcrcError
+    data = bytes(range(256)) * 40
+    ok = zv.scan(crafted_zip(data, 8))
+    assert ok[0].uncomp_size == len(data) and ok[0].status == zv.ZIP_UNVERIFIED
+    huge = zv.scan(crafted_zip(data, 8, usize64=0xFFFFFFFFFFFFFFF0))
+    assert huge[0].uncomp_size == 0xFFFFFFFFFFFFFFF0 and huge[0].status == zv.ZIP_UNVERIFIED
+    # a local-header offset near 2^64 must not wrap the bounds check
+    for lho in (0xFFFFFFFFFFFFFFF0, 0xFFFFFFFFFFFFFFE2, 1 << 63):
+        bad = zv.scan(crafted_zip(data, 0, lho64=lho))
+        assert bad[0].status == zv.ZIP_BAD, hex(lho)
+    # a ZIP64 EOCD offset near 2^64 must be rejected, not read before the image
+    for z in (0xFFFFFFFFFFFFFFF0, 0xFFFFFFFFFFFFFFC8):
+        with pytest.raises(ZcrcError):
+            zv.scan(crafted_zip(data, 0, z64_locator_off=z))

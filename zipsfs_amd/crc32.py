@@ -175,6 +175,21 @@ def _check_dev(t, name, dtype=None):
         raise TypeError(f"{name} must be {dtype}, got {t.dtype}")
 
 
+def _check_results(out, n: int) -> None:
+    _check_dev(out, "out")
+    if out.element_size() != 4 or out.numel() < n:
+        raise ValueError(f"out must hold >= {n} 4-byte elements, has {out.numel()} x {out.element_size()} B")
+
+
+def _check_seeds(seeds, n: int):
+    if seeds is None:
+        return None
+    _check_dev(seeds, "seeds")
+    if seeds.element_size() != 4 or seeds.numel() < n:
+        raise ValueError(f"seeds must hold >= {n} 4-byte elements, has {seeds.numel()} x {seeds.element_size()} B")
+    return seeds.data_ptr()
+
+
 def crc32_batch_device(ptrs, lens, seeds=None, out=None, stream=None):
     """Device-resident batch.  ``ptrs``/``lens``: int64 device tensors of n
     device addresses / byte counts; ``seeds``: optional int32/uint32 device
@@ -187,11 +202,8 @@ def crc32_batch_device(ptrs, lens, seeds=None, out=None, stream=None):
         raise ValueError("ptrs/lens length mismatch")
     if out is None:
         out = torch.empty(n, dtype=torch.int32, device=ptrs.device)
-    _check_dev(out, "out")
-    sp = None
-    if seeds is not None:
-        _check_dev(seeds, "seeds")
-        sp = seeds.data_ptr()
+    _check_results(out, n)
+    sp = _check_seeds(seeds, n)
     check(lib().zcrc32_batch_device(ptrs.data_ptr(), lens.data_ptr(), sp, out.data_ptr(), n, _stream_ptr(stream)),
           "zcrc32_batch_device")
     return out
@@ -204,9 +216,12 @@ def crc32_batch_device_ws(ptrs, lens, scratch, seeds=None, out=None, stream=None
     _check_dev(lens, "lens", torch.int64)
     _check_dev(scratch, "scratch")
     n = ptrs.numel()
+    if lens.numel() != n:
+        raise ValueError("ptrs/lens length mismatch")
     if out is None:
         out = torch.empty(n, dtype=torch.int32, device=ptrs.device)
-    sp = None if seeds is None else seeds.data_ptr()
+    _check_results(out, n)
+    sp = _check_seeds(seeds, n)
     check(lib().zcrc32_batch_device_ws(ptrs.data_ptr(), lens.data_ptr(), sp, out.data_ptr(), n,
                                        scratch.data_ptr(), scratch.numel() * scratch.element_size(),
                                        _stream_ptr(stream)), "zcrc32_batch_device_ws")
@@ -225,9 +240,12 @@ def crc32_batch_strided(base, stride: int, length: int, n: int, seeds=None, out=
     need = base_offset + (n - 1) * stride + length if n else 0
     if need > base.numel() * base.element_size():
         raise ValueError("strided batch exceeds the base tensor")
+    if n < 0 or stride < 0 or length < 0 or base_offset < 0:
+        raise ValueError("negative n, stride, length or offset")
     if out is None:
         out = torch.empty(n, dtype=torch.int32, device=base.device)
-    sp = None if seeds is None else seeds.data_ptr()
+    _check_results(out, n)
+    sp = _check_seeds(seeds, n)
     check(lib().zcrc32_batch_device_strided(base.data_ptr() + base_offset, stride, length, n, sp, out.data_ptr(),
                                             _stream_ptr(stream)), "zcrc32_batch_device_strided")
     return out

@@ -619,7 +619,7 @@ int stream_update(zcrc32_stream *s, const uint8_t *data, size_t n) {
 // from the host CRC as well, reported once on stderr and counted.
 namespace zcrc {
 namespace {
-constexpr size_t kDefaultGpuMinBytes = 32ull << 20;  // measured crossover, DESIGN.md 10b
+constexpr size_t kDefaultGpuMinBytes = 4ull << 20;  // measured crossover (profiles/r02/dropin_crossover.json)
 std::atomic<size_t> g_gpu_min{SIZE_MAX};
 std::atomic<int> g_no_device{0};  // the first GPU attempt found no usable device
 std::atomic<uint64_t> g_dropin_gpu{0}, g_dropin_host{0}, g_dropin_fallback{0};

@@ -42,7 +42,8 @@ int find_cd(const uint8_t *a, uint64_t len, uint64_t *cd_off, uint64_t *cd_size,
   uint64_t n = rd16(a + e + 10), size = rd32(a + e + 12), off = rd32(a + e + 16);
   if (e >= 20 && rd32(a + e - 20) == kSigZ64Loc) {  // ZIP64 locator directly before the EOCD
     const uint64_t z = rd64(a + e - 20 + 8);
-    if (z + 56 > len || rd32(a + z) != kSigZ64Eocd) return zfail("bad ZIP64 end-of-central-directory record");
+    if (len < 56 || z > len - 56 || rd32(a + z) != kSigZ64Eocd)
+      return zfail("bad ZIP64 end-of-central-directory record");
     n = rd64(a + z + 32);
     size = rd64(a + z + 40);
     off = rd64(a + z + 48);
@@ -101,7 +102,7 @@ extern "C" int zcrc_zip_scan(const void *archive, size_t archive_len, zcrc_zip_e
       E.name_len = nlen;
       E.status = ZCRC_ZIP_UNVERIFIED;
       // local header -> data offset
-      if (lho + 30 > len || rd32(a + lho) != kSigLocal) {
+      if (len < 30 || lho > len - 30 || rd32(a + lho) != kSigLocal) {  // lho may be any 64-bit value
         E.status = ZCRC_ZIP_BAD;
       } else {
         const uint64_t d = lho + 30 + rd16(a + lho + 26) + rd16(a + lho + 28);
@@ -126,6 +127,17 @@ bool deflatable(const zcrc_zip_entry &E) { return E.status != ZCRC_ZIP_BAD && E.
 
 constexpr uint64_t kArenaBytes = 16ull << 30;  // inflate output per chunk
 
+// Output room for a deflated entry.  DEFLATE expands at most 1032:1 (a
+// 258-byte match in two 1-bit codes), so a stream whose output would exceed
+// 1032 * comp_size + 64 bytes does not exist: capping the room there never
+// changes a verdict (a larger claimed size cannot be produced and is a
+// mismatch), and it keeps a crafted ZIP64 size (up to 2^64) from sizing the
+// arena.  Entries whose room exceeds one arena are left UNVERIFIED.
+uint64_t inflate_room(const zcrc_zip_entry &E) {
+  const uint64_t bound = E.comp_size > (UINT64_MAX - 64) / 1032 ? UINT64_MAX : 1032 * E.comp_size + 64;
+  return E.uncomp_size < bound ? E.uncomp_size : bound;
+}
+
 void finish(zcrc_zip_entry *entries, const std::vector<size_t> &idx, const std::vector<uint32_t> &crc) {
   for (size_t j = 0; j < idx.size(); j++) {
     zcrc_zip_entry &E = entries[idx[j]];
@@ -147,8 +159,8 @@ int verify_deflated_chunk(const uint8_t *d_archive, zcrc_zip_entry *entries, con
     h[j] = reinterpret_cast<uint64_t>(d_archive) + E.data_offset;
     h[m + j] = E.comp_size;
     h[2 * m + j] = arena_bytes;
-    h[3 * m + j] = E.uncomp_size;
-    arena_bytes += E.uncomp_size;
+    h[3 * m + j] = inflate_room(E);  // <= kArenaBytes: the chunking below guarantees it
+    arena_bytes += h[3 * m + j];
   }
   void *d_arena = nullptr, *d_desc = nullptr;
   if (hipMallocAsync(&d_arena, arena_bytes + 16, st) != hipSuccess) return zfail("inflate arena allocation failed");
@@ -170,7 +182,8 @@ int verify_deflated_chunk(const uint8_t *d_archive, zcrc_zip_entry *entries, con
   if (!rc)
     rc = zcrc_inflate_batch_device(reinterpret_cast<const void *const *>(d_src), d_srclen,
                                    reinterpret_cast<void *const *>(d_dst), d_cap, d_olen, d_status, m, st);
-  if (!rc) rc = zcrc32_batch_device(reinterpret_cast<const void *const *>(d_dst), d_cap, nullptr, d_crc, m, st);
+  // CRC of what each inflate produced (0 bytes unless it succeeded)
+  if (!rc) rc = zcrc32_batch_device(reinterpret_cast<const void *const *>(d_dst), d_olen, nullptr, d_crc, m, st);
   if (!rc && (hipMemcpyAsync(olen.data(), d_olen, 8 * m, hipMemcpyDeviceToHost, st) != hipSuccess ||
               hipMemcpyAsync(status.data(), d_status, 4 * m, hipMemcpyDeviceToHost, st) != hipSuccess ||
               hipMemcpyAsync(crc.data(), d_crc, 4 * m, hipMemcpyDeviceToHost, st) != hipSuccess))
@@ -204,12 +217,12 @@ extern "C" int zcrc_zip_verify_device(const void *d_archive, size_t archive_len,
     zcrc_zip_entry &E = entries[i];
     if (E.status == ZCRC_ZIP_BAD) continue;
     E.status = ZCRC_ZIP_UNVERIFIED;  // until checked below
-    if (E.data_offset + E.comp_size > archive_len) continue;
+    if (E.data_offset > archive_len || E.comp_size > archive_len - E.data_offset) continue;
     if (verifiable(E)) {
       idx.push_back(i);
       hp.push_back(reinterpret_cast<uint64_t>(d_archive) + E.data_offset);
       hl.push_back(E.comp_size);
-    } else if (deflatable(E)) {
+    } else if (deflatable(E) && inflate_room(E) <= kArenaBytes) {
       didx.push_back(i);
     }
   }
@@ -236,8 +249,8 @@ extern "C" int zcrc_zip_verify_device(const void *d_archive, size_t archive_len,
   for (size_t a = 0; a < didx.size();) {
     size_t b = a;
     uint64_t bytes = 0;
-    while (b < didx.size() && (b == a || bytes + entries[didx[b]].uncomp_size <= kArenaBytes))
-      bytes += entries[didx[b++]].uncomp_size;
+    while (b < didx.size() && (b == a || bytes + inflate_room(entries[didx[b]]) <= kArenaBytes))
+      bytes += inflate_room(entries[didx[b++]]);  // each <= kArenaBytes: no wrap
     const int rc = verify_deflated_chunk(static_cast<const uint8_t *>(d_archive), entries, didx, a, b, st);
     if (rc) return rc;
     a = b;
