@@ -572,3 +572,40 @@ def test_wrapper_argument_validation():
         z.crc32_batch_strided(mem, 1024, 1024, 8, out=torch.empty(4, dtype=torch.int32, device=DEV))
     got = u32(z.crc32_batch_device(ptrs, lens))
     assert (got == zlib.crc32(bytes(1024))).all()
+
+
+@pytest.mark.parametrize("shape", ["uniform_dynamic", "ragged_split", "tiny_and_huge"])
+def test_fused_small_batch_vs_two_launch_path(shape):
+    """n <= 8192 eager calls run ONE fused launch (the kernel scans the
+    lengths; split pieces meet in self-cleaning scratch words; the claim
+    counter resets itself).  Repeated launches on one stream, each vs the
+    two-launch path (crc32_batch_device_ws) and the oracle on a sample."""
+    rnd = random.Random({"uniform_dynamic": 1, "ragged_split": 2, "tiny_and_huge": 3}[shape])
+    if shape == "uniform_dynamic":  # 4 GiB in 1 MiB buffers: the dynamic part is on
+        lens_l = [1 << 20] * 4096
+    elif shape == "ragged_split":   # many buffers above the 128 KiB split size
+        lens_l = [rnd.choice([0, 3, 4095, 65536, 200_000, 3_000_001, 9_999_999]) for _ in range(3000)]
+    else:
+        lens_l = [rnd.randint(0, 64) for _ in range(8190)] + [700_000_001, 123_456_789]
+    n = len(lens_l)
+    offs = np.zeros(n, dtype=np.int64)
+    offs[1:] = np.cumsum(np.array(lens_l, dtype=np.int64) + 7)[:-1]
+    mem = torch.empty(int(offs[-1] + lens_l[-1] + 64), dtype=torch.uint8, device=DEV)
+    ptrs = mem.data_ptr() + 1 + torch.tensor(offs, device=DEV)
+    lens = torch.tensor(lens_l, dtype=torch.int64, device=DEV)
+    z.fill_synthetic(ptrs, lens, index0=5, index_step=3, seed=SEED)
+    seeds_np = np.array([rnd.getrandbits(32) for _ in range(n)], dtype=np.uint32)
+    seeds = torch.tensor(seeds_np.view(np.int32), device=DEV)
+    scratch = torch.empty(z.crc32.scratch_bytes(n), dtype=torch.uint8, device=DEV)
+    ref = u32(z.crc32_batch_device_ws(ptrs, lens, scratch, seeds=seeds))
+    for rep in range(3):
+        got = u32(z.crc32_batch_device(ptrs, lens, seeds=seeds))
+        np.testing.assert_array_equal(got, ref, err_msg=f"{shape} launch {rep}")
+        got0 = u32(z.crc32_batch_device(ptrs, lens))
+        if rep == 0:
+            ref0 = got0
+        np.testing.assert_array_equal(got0, ref0)
+    sample = sorted(set(rnd.sample(range(n), 24)) | {n - 1, n - 2})
+    for i in sample:
+        exp = o.payload_crc(lens_l[i], 5 + 3 * i, crc=int(seeds_np[i]))
+        assert int(ref[i]) == exp, (shape, i, lens_l[i])

@@ -139,11 +139,18 @@ __device__ __forceinline__ uint32_t hash32(uint32_t x) {
 template <bool kStrided>
 struct BatchView {
   const BatchArgs &a;
-  __device__ uint64_t prefix(uint64_t i) const { return kStrided ? i * a.len : a.prefix[i]; }
+  // fused small batches: the prefix as the workgroup computed it into LDS,
+  // read by the prologue's range search (nullptr afterwards: global copy)
+  const uint64_t *lpre;
+  const uint64_t tot_;
+  __device__ BatchView(const BatchArgs &args, const uint64_t *lds_prefix = nullptr)
+      : a(args), lpre(lds_prefix),
+        // read once per wave: prefix[n] would otherwise be re-read by every snap
+        tot_(kStrided ? args.n * args.len : uni64(lds_prefix ? lds_prefix[args.n] : args.prefix[args.n])) {}
+  __device__ uint64_t pre(uint64_t i) const { return lpre ? lpre[i] : a.prefix[i]; }
+  __device__ uint64_t prefix(uint64_t i) const { return kStrided ? i * a.len : pre(i); }
   __device__ const uint8_t *ptr(uint64_t i) const { return kStrided ? a.base + i * a.stride : a.ptrs[i]; }
   __device__ uint32_t seed(uint64_t i) const { return a.seeds ? a.seeds[i] : 0u; }
-  // read once per wave: prefix[n] would otherwise be re-read by every snap
-  const uint64_t tot_ = kStrided ? a.n * a.len : uni64(a.prefix[a.n]);
   __device__ uint64_t total() const { return tot_; }
 
   // First i in [0, n] with prefix(i) >= t (prefix(n) = total >= t).  Wave-wide
@@ -160,7 +167,7 @@ struct BatchView {
       const uint64_t step = (hi - lo + 63) / 64;
       uint64_t idx = lo + (uint64_t)(lane + 1) * step;
       if (idx > hi) idx = hi;
-      const uint64_t m = __ballot(a.prefix[idx] >= t);
+      const uint64_t m = __ballot(pre(idx) >= t);
       const uint32_t f = (uint32_t)__builtin_ctzll(m);
       const uint64_t nhi = (lo + (uint64_t)(f + 1) * step) < hi ? (lo + (uint64_t)(f + 1) * step) : hi;
       const uint64_t nlo = f == 0 ? lo : lo + (uint64_t)f * step + 1;
@@ -168,7 +175,7 @@ struct BatchView {
       hi = uni64(nhi);
     }
     const uint64_t idx = lo + lane;
-    const bool ok = idx <= hi && a.prefix[idx <= hi ? idx : hi] >= t;
+    const bool ok = idx <= hi && pre(idx <= hi ? idx : hi) >= t;
     const uint64_t m = __ballot(ok);
     return uni64(lo + (uint64_t)__builtin_ctzll(m));
   }
@@ -213,7 +220,7 @@ struct BatchView {
       uint64_t x0 = lo0 + (uint64_t)(lane + 1) * st0, x1 = lo1 + (uint64_t)(lane + 1) * st1;
       if (x0 > hi0) x0 = hi0;
       if (x1 > hi1) x1 = hi1;
-      const uint64_t v0 = a.prefix[x0], v1 = a.prefix[x1];
+      const uint64_t v0 = pre(x0), v1 = pre(x1);
       const uint64_t m0 = __ballot(v0 >= t0), m1 = __ballot(v1 >= t1);
       if (hi0 - lo0 > 63) {
         const uint32_t f = (uint32_t)__builtin_ctzll(m0);
@@ -231,7 +238,7 @@ struct BatchView {
       }
     }
     const uint64_t x0 = lo0 + lane, x1 = lo1 + lane;
-    const uint64_t v0 = a.prefix[x0 <= hi0 ? x0 : hi0], v1 = a.prefix[x1 <= hi1 ? x1 : hi1];
+    const uint64_t v0 = pre(x0 <= hi0 ? x0 : hi0), v1 = pre(x1 <= hi1 ? x1 : hi1);
     const uint64_t m0 = __ballot(x0 <= hi0 && v0 >= t0), m1 = __ballot(x1 <= hi1 && v1 >= t1);
     r0 = uni64(lo0 + (uint64_t)__builtin_ctzll(m0));
     r1 = uni64(lo1 + (uint64_t)__builtin_ctzll(m1));
@@ -291,6 +298,36 @@ __device__ uint64_t block_excl_scan(uint64_t v, uint64_t *s_tmp /* 16 */, uint64
 // others waited on a flag -- was removed in round 1: no workgroup of this
 // kernel waits on another one.  DESIGN.md section 4, "Plan".)
 
+// Fused small batches (zcrc32_batch_device, n <= kFusedMaxN): no plan launch
+// zeroes out[] first, so the pieces of a split buffer meet in a 64-bit word of
+// scratch -- high half: 64 KiB grid cells covered so far, low half: xor of the
+// contributions -- updated lock-free with compare-and-swap.  The piece that
+// completes the cell count stores the result and returns the word to zero,
+// so the scratch is zero again for the next launch (the runtime zero-fills it
+// once, when it is allocated).  A retry only follows another piece's update
+// of the same word: no piece waits for another one to make progress.
+__device__ void split_accumulate(const BatchArgs &a, uint64_t i, uint64_t n, uint64_t lo, uint64_t hi,
+                                 uint32_t contrib) {
+  // split points sit on the end-relative kSplitGrain grid, so every piece but
+  // the first covers whole cells; the first covers the partial cell too
+  const uint64_t cells = (n + kSplitGrain - 1) / kSplitGrain;  // <= 2^26 (kMaxLaunchBytes)
+  const uint64_t mine = lo == 0 ? (hi + kSplitGrain - 1) / kSplitGrain : (hi - lo) / kSplitGrain;
+  unsigned long long *word = reinterpret_cast<unsigned long long *>(a.acc + i);
+  unsigned long long expect = 0;
+  for (;;) {
+    const unsigned long long want = (((expect >> 32) + mine) << 32) | (uint32_t)((uint32_t)expect ^ contrib);
+    const unsigned long long got = atomicCAS(word, expect, want);
+    if (got == expect) {
+      if ((want >> 32) == cells) {
+        a.out[i] = (uint32_t)want;
+        atomicExch(word, 0ull);
+      }
+      return;
+    }
+    expect = got;
+  }
+}
+
 // ------------------------------------------------------------ the kernel
 
 // kD: 1 KiB blocks per register group (two groups in flight); kAblate != 0
@@ -298,7 +335,8 @@ __device__ uint64_t block_excl_scan(uint64_t v, uint64_t *s_tmp /* 16 */, uint64
 // Process every piece of the byte range [S0, S1) of the concatenated batch
 // (S0, S1 snapped; `last_range` also takes the trailing empty buffers).
 // Returns the number of pieces.  Wave-uniform; no barriers.
-template <bool kStrided, uint32_t kD, int kAblate, bool kRotate, int kPrio = 0, int kAux = 0, bool kStamp = false>
+template <bool kStrided, uint32_t kD, int kAblate, bool kRotate, int kPrio = 0, int kAux = 0, bool kStamp = false,
+          bool kFused = false>
 __device__ __forceinline__ uint64_t process_range(const BatchArgs &args, const BatchView<kStrided> &bv,
                                                   const uint32_t *s_lds, const TableBlob *tab, uint64_t S0,
                                                   uint64_t S1, bool last_wave, uint32_t salt, uint32_t lane,
@@ -464,7 +502,11 @@ __device__ __forceinline__ uint64_t process_range(const BatchArgs &args, const B
     } else {
       const uint64_t d = n - rel_hi;  // bytes after this piece, multiple of kSplitGrain
       uint32_t contrib = d ? shift_bytes(tab, r, d) : (r ^ 0xFFFFFFFFu);
-      if (lane == 0) atomicXor(args.out + i, contrib);
+      if (kFused) {
+        if (lane == 0) split_accumulate(args, i, n, rel_lo, rel_hi, contrib);
+      } else if (lane == 0) {
+        atomicXor(args.out + i, contrib);
+      }
     }
   }
   return npieces;
@@ -476,7 +518,7 @@ __device__ __forceinline__ uint64_t process_range(const BatchArgs &args, const B
 // (tools/hbm_probe, tools/crc_variants).
 constexpr int kLoadNt = 2;
 template <bool kStrided, uint32_t kD = kDepth, int kAblate = 0, bool kRotate = true, bool kStamp = false,
-          int kPrio = 1, int kAux = kLoadNt>
+          int kPrio = 1, int kAux = kLoadNt, bool kFused = false>
 __global__ __launch_bounds__(kThreads) void crc32_batch_kernel(BatchArgs args) {
   __shared__ __attribute__((aligned(16))) uint32_t s_lds[kLdsBytes / 4];
   const TableBlob *tab = args.tab;
@@ -501,7 +543,36 @@ __global__ __launch_bounds__(kThreads) void crc32_batch_kernel(BatchArgs args) {
   const uint4 *comb_src = reinterpret_cast<const uint4 *>(tab->comb);
   const uint4 comb0 = comb_src[tid], comb1 = comb_src[tid + 1024u];
 
-  const BatchView<kStrided> bv{args};
+  // Fused small batch: every workgroup scans the <= kFusedMaxN lengths itself
+  // (thread t owns buffers 8t .. 8t+7) while the table loads are in flight,
+  // into LDS for its own range search and into the scratch prefix for the
+  // piece walk and the unit searches.  Every workgroup writes the same
+  // values; each reads only after its own writes and a barrier.
+  uint64_t *const lds_pre = reinterpret_cast<uint64_t *>(s_lds);
+  if (kFused) {
+    static_assert(kFusedMaxN == 8u * kThreads, "fused scan: 8 lengths per thread");
+    static_assert((kFusedMaxN + 1 + 16) * 8 <= kLdsBytes, "fused scan fits in LDS");
+    uint64_t v[8], sum = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < 8; k++) {
+      const uint64_t idx = 8u * tid + k;
+      v[k] = idx < args.n ? args.lens[idx] : 0;
+      sum += v[k];
+    }
+    uint64_t tot;
+    uint64_t run = block_excl_scan(sum, lds_pre + kFusedMaxN + 8, &tot);
+    uint64_t *gpre = const_cast<uint64_t *>(args.prefix);
+#pragma unroll
+    for (uint32_t k = 0; k < 8; k++) {
+      const uint64_t idx = 8u * tid + k;
+      if (idx < args.n) lds_pre[idx] = run, gpre[idx] = run;
+      run += v[k];
+    }
+    if (tid == 0) lds_pre[args.n] = tot, gpre[args.n] = tot;
+    __threadfence_block();
+    __syncthreads();
+  }
+  BatchView<kStrided> bv(args, kFused ? lds_pre : nullptr);
   const uint64_t total = bv.total();
   const uint64_t max_waves = (uint64_t)gridDim.x * kWaves;
   const uint64_t min_range = args.min_range ? args.min_range : kMinRange;
@@ -512,7 +583,7 @@ __global__ __launch_bounds__(kThreads) void crc32_batch_kernel(BatchArgs args) {
   if (want < args.n) want = args.n;
   if (want < 1) want = 1;
   const uint64_t W = want < max_waves ? want : max_waves;
-  if ((uint64_t)blockIdx.x * kWaves >= W) return;  // whole workgroup idle (uniform)
+  if ((uint64_t)blockIdx.x * kWaves >= W) return;  // whole workgroup idle (uniform: no barrier is skipped)
 
   const uint32_t lane = threadIdx.x & 63u;
   const uint64_t w = (uint64_t)blockIdx.x * kWaves + (threadIdx.x >> 6);
@@ -543,6 +614,10 @@ __global__ __launch_bounds__(kThreads) void crc32_batch_kernel(BatchArgs args) {
     bv.range(q_tot * w + (r_tot * w) / W, (w + 1 == W) ? Ts : q_tot * (w + 1) + (r_tot * (w + 1)) / W, last, S0,
              S1, lb0, lb1);
   const uint64_t t_search = kStamp ? __builtin_amdgcn_s_memrealtime() : 0;
+  if (kFused) {
+    __syncthreads();  // every wave's search is done with the LDS prefix
+    bv.lpre = nullptr;
+  }
 
   // ---- LDS: braided table x32 replicas + 8 combine tables ---------------
   {
@@ -584,7 +659,7 @@ __global__ __launch_bounds__(kThreads) void crc32_batch_kernel(BatchArgs args) {
       have_next = true;
     }
     if (S0 < S1 || last)
-      npieces += process_range<kStrided, kD, kAblate, kRotate, kPrio, kAux, kStamp>(
+      npieces += process_range<kStrided, kD, kAblate, kRotate, kPrio, kAux, kStamp, kFused>(
           args, bv, s_lds, tab, S0, S1, last, salt, lane, band, lb0, lb1, &t_tail);
     if (!units) break;
     if (first_claim) {
@@ -612,6 +687,15 @@ __global__ __launch_bounds__(kThreads) void crc32_batch_kernel(BatchArgs args) {
     salt = u ^ 0x9E3779B9u;
     if (kPrio && band) __builtin_amdgcn_s_setprio(0);
     band = false;
+  }
+  if (kFused && units && lane == 0) {
+    // the last wave out returns the claim counter to zero for the next launch
+    // (no plan kernel resets it); every claim of this launch is complete here
+    __threadfence();
+    if (atomicAdd(args.done, 1u) + 1u == (uint32_t)W) {
+      atomicExch(args.ctr, 0u);
+      atomicExch(args.done, 0u);
+    }
   }
   if (kStamp && lane == 0) {
     args.stamps[8 * w + 0] = t_begin;

@@ -20,6 +20,7 @@ constexpr size_t kCtrBytes = 256;              // work counter, own cache lines
 constexpr uint32_t kLdsBytes = 163840;         // all 160 KiB of the CU's LDS
 constexpr uint32_t kLdsCombDword = 32768;      // combine tables start at 128 KiB
 constexpr uint32_t kPlanPerThread = 8;
+constexpr uint64_t kFusedMaxN = 8192;  // one-launch small batches: the kernel scans the lengths itself
 constexpr uint64_t kPlanTile = 1024 * kPlanPerThread;
 // one launch covers at most this many bytes (keeps every piece < 2 GiB)
 constexpr uint64_t kMaxLaunchBytes = 1ull << 42;
@@ -53,11 +54,18 @@ struct BatchArgs {
   uint32_t *ctr;
   uint32_t dyn_shift;
   uint64_t dyn_unit;
+  // fused small batches (kFusedMaxN): lengths to scan in-kernel (the scan is
+  // written to `prefix`), split-piece accumulators (n words) and the
+  // finished-wave counter; acc, *ctr and *done are zero at launch and left
+  // zero by the kernel
+  const uint64_t *lens;
+  uint64_t *acc;
+  uint32_t *done;
 };
 
 // t0/t1: optional events stamped with the kernel's own start and end
 hipError_t launch_batch(const BatchArgs &args, bool strided, int num_cus, hipStream_t stream,
-                        hipEvent_t t0 = nullptr, hipEvent_t t1 = nullptr);
+                        hipEvent_t t0 = nullptr, hipEvent_t t1 = nullptr, bool fused = false);
 // batched raw-DEFLATE decode (zcrc_inflate.hip): device arrays of n
 struct InflateArgs {
   const uint8_t *const *src;
@@ -76,7 +84,7 @@ constexpr uint64_t kInflateMaxSrc = 0xF0000000ull;  // 32-bit buffer range and b
 // (used when the batch exceeds the streams resident at once; may be null)
 hipError_t launch_inflate(const InflateArgs &args, int num_cus, hipStream_t stream, uint32_t *order_scratch);
 // purposes of the runtime's per-stream scratch cache (zcrc_runtime.hip)
-enum ScratchUse { kScratchBatch = 0, kScratchInflateOrder = 1 };
+enum ScratchUse { kScratchBatch = 0, kScratchInflateOrder = 1, kScratchFused = 2 };
 
 inline uint64_t plan_tiles(uint64_t n) { return n == 0 ? 1 : (n + kPlanTile - 1) / kPlanTile; }
 hipError_t launch_plan(const uint64_t *d_lens, uint64_t n, uint64_t *d_prefix, uint64_t *d_tile_sum,

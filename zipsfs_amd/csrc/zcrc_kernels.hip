@@ -114,11 +114,14 @@ __global__ __launch_bounds__(1024) void plan_one_tile(const uint64_t *lens, uint
 // ------------------------------------------------------------ launchers
 
 hipError_t launch_batch(const BatchArgs &args, bool strided, int num_cus, hipStream_t stream, hipEvent_t t0,
-                        hipEvent_t t1) {
+                        hipEvent_t t1, bool fused) {
   const dim3 grid((unsigned)num_cus), block(kThreads);
   // t0/t1 (profiling): timestamps carried by the dispatch packet itself --
   // event records around the launch add ~11 us of queue bubbles per launch
-  if (strided)
+  if (fused)
+    hipExtLaunchKernelGGL((crc32_batch_kernel<false, kDepth, 0, true, false, 1, kLoadNt, true>), grid, block, 0,
+                          stream, t0, t1, 0, args);
+  else if (strided)
     hipExtLaunchKernelGGL((crc32_batch_kernel<true, kDepth, 0>), grid, block, 0, stream, t0, t1, 0, args);
   else
     hipExtLaunchKernelGGL((crc32_batch_kernel<false, kDepth, 0>), grid, block, 0, stream, t0, t1, 0, args);

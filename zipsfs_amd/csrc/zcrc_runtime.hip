@@ -119,7 +119,7 @@ std::vector<hipEvent_t> g_prof_free;  // recycled: no hipEventCreate per launch
 double g_prof_ms = 0.0;
 int g_prof_count = 0;
 
-int launch_main(const BatchArgs &args, bool strided, const DeviceCtx &dc, hipStream_t stream) {
+int launch_main(const BatchArgs &args, bool strided, const DeviceCtx &dc, hipStream_t stream, bool fused = false) {
   hipEvent_t e0 = nullptr, e1 = nullptr;
   const bool prof = g_prof_on.load(std::memory_order_relaxed) != 0;
   if (prof) {
@@ -131,7 +131,7 @@ int launch_main(const BatchArgs &args, bool strided, const DeviceCtx &dc, hipStr
     if (!e0) ZCRC_HIP_TRY(hipEventCreate(&e0));
     if (!e1) ZCRC_HIP_TRY(hipEventCreate(&e1));
   }
-  ZCRC_HIP_TRY(launch_batch(args, strided, dc.num_cus, stream, e0, e1));
+  ZCRC_HIP_TRY(launch_batch(args, strided, dc.num_cus, stream, e0, e1, fused));
   if (prof) {
     std::lock_guard<std::mutex> lk(g_prof_mu);
     g_prof_pending.emplace_back(e0, e1);
@@ -201,6 +201,43 @@ int batch_device_ws(const void *const *d_ptrs, const uint64_t *d_lens, const uin
   a.ctr = d_ctr;
   a.dyn_shift = kDynShift;
   return launch_main(a, false, *dc, stream);
+}
+
+// Small eager batches (n <= kFusedMaxN) in ONE launch: the kernel scans the
+// lengths itself (no plan kernel, no queue gap between two dependent
+// launches).  Its scratch -- claim counter, finished-wave counter, split-piece
+// accumulators, prefix -- is zero-filled when allocated and the kernel leaves
+// the counters and accumulators zero, so it has its own per-stream slot
+// (the two-launch path leaves its counter nonzero).  ZCRC_FUSED=0 turns it off.
+bool fused_enabled() {
+  static const bool on = [] {
+    const char *e = getenv("ZCRC_FUSED");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
+size_t fused_scratch_bytes(size_t n) { return kCtrBytes + 8 * n + 8 * (n + 1); }
+
+int batch_device_fused(const void *const *d_ptrs, const uint64_t *d_lens, const uint32_t *d_seeds, uint32_t *d_out,
+                       size_t n, void *scratch, hipStream_t stream) {
+  DeviceCtx *dc = nullptr;
+  int rc = device_ctx(&dc);
+  if (rc) return rc;
+  uint8_t *sc = static_cast<uint8_t *>(scratch);
+  BatchArgs a{};
+  a.ptrs = reinterpret_cast<const uint8_t *const *>(d_ptrs);
+  a.lens = d_lens;
+  a.seeds = d_seeds;
+  a.out = d_out;
+  a.n = n;
+  a.tab = dc->d_tab;
+  a.ctr = reinterpret_cast<uint32_t *>(sc);
+  a.done = reinterpret_cast<uint32_t *>(sc) + 1;
+  a.dyn_shift = kDynShift;
+  a.acc = reinterpret_cast<uint64_t *>(sc + kCtrBytes);
+  a.prefix = a.acc + n;
+  return launch_main(a, false, *dc, stream, true);
 }
 
 // ------------------------------------------------------------- host batch
@@ -727,6 +764,11 @@ int zcrc32_batch_device(const void *const *d_ptrs, const uint64_t *d_lens, const
   void *scratch = nullptr;
   size_t have = 0;
   std::unique_lock<std::mutex> lk;
+  if (n <= kFusedMaxN && fused_enabled()) {
+    const int rc = stream_scratch(st, kScratchFused, fused_scratch_bytes(n), &scratch, &have, &lk);
+    if (rc) return rc;
+    return batch_device_fused(d_ptrs, d_lens, d_seeds_or_null, d_out, n, scratch, st);
+  }
   const int rc = stream_scratch(st, kScratchBatch, bytes, &scratch, &have, &lk);
   if (rc) return rc;
   return batch_device_ws(d_ptrs, d_lens, d_seeds_or_null, d_out, n, scratch, have, st);
