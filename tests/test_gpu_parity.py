@@ -474,12 +474,14 @@ def test_concurrent_host_threads_dropin():
         assert res[k] == e + e
 
 
-def test_concurrent_device_calls_shared_and_private_streams():
+@pytest.mark.parametrize("fused", ["0", "1"])
+def test_concurrent_device_calls_shared_and_private_streams(fused, monkeypatch):
     """Host threads issuing zcrc32_batch_device at once, on one shared stream
     and on private streams, with growing batch sizes (the per-stream scratch
     cache grows under its lock while other threads launch): every result vs
     the oracle."""
     from concurrent.futures import ThreadPoolExecutor
+    monkeypatch.setenv("ZCRC_FUSED", fused)
     rnd = random.Random(77)
     total = 64 << 20
     mem = torch.randint(0, 256, (total,), dtype=torch.uint8, device=DEV)
@@ -511,13 +513,15 @@ def test_concurrent_device_calls_shared_and_private_streams():
         np.testing.assert_array_equal(got, exp, err_msg=f"job {k}")
 
 
-def test_small_batches_overlapping_on_six_streams():
+@pytest.mark.parametrize("fused", ["0", "1"])
+def test_small_batches_overlapping_on_six_streams(fused, monkeypatch):
     """Small-batch launches (<= 8192 buffers) from six host threads on six
     streams at once, each queueing twelve launches without synchronising,
     so that the launches overlap on the GPU.  (Until round 1's last session
     this guarded the fused plan's cross-workgroup wait, since removed.)
     Every result vs the oracle."""
     from concurrent.futures import ThreadPoolExecutor
+    monkeypatch.setenv("ZCRC_FUSED", fused)
     rnd = random.Random(123)
     total = 32 << 20
     mem = torch.randint(0, 256, (total,), dtype=torch.uint8, device=DEV)
@@ -575,11 +579,12 @@ def test_wrapper_argument_validation():
 
 
 @pytest.mark.parametrize("shape", ["uniform_dynamic", "ragged_split", "tiny_and_huge"])
-def test_fused_small_batch_vs_two_launch_path(shape):
+def test_fused_small_batch_vs_two_launch_path(shape, monkeypatch):
     """n <= 8192 eager calls run ONE fused launch (the kernel scans the
     lengths; split pieces meet in self-cleaning scratch words; the claim
     counter resets itself).  Repeated launches on one stream, each vs the
     two-launch path (crc32_batch_device_ws) and the oracle on a sample."""
+    monkeypatch.setenv("ZCRC_FUSED", "1")  # libzcrc reads it per call
     rnd = random.Random({"uniform_dynamic": 1, "ragged_split": 2, "tiny_and_huge": 3}[shape])
     if shape == "uniform_dynamic":  # 4 GiB in 1 MiB buffers: the dynamic part is on
         lens_l = [1 << 20] * 4096
@@ -609,3 +614,31 @@ def test_fused_small_batch_vs_two_launch_path(shape):
     for i in sample:
         exp = o.payload_crc(lens_l[i], 5 + 3 * i, crc=int(seeds_np[i]))
         assert int(ref[i]) == exp, (shape, i, lens_l[i])
+
+
+@pytest.mark.parametrize("fused", ["0", "1"])
+def test_fused_scratch_reuse_across_batch_sizes(fused, monkeypatch):
+    """Fused launches of different n share one per-stream scratch slot.  A
+    small batch leaves its prefix in the slot; a larger batch that follows
+    must not read it as split-piece accumulators (round-2 bug: the
+    accumulators sat at an n-dependent offset and overlapped an earlier
+    prefix).  Alternating sizes with split buffers, each vs the two-launch
+    path."""
+    monkeypatch.setenv("ZCRC_FUSED", fused)
+    rnd = random.Random(77)
+    for n in [1, 3, 17, 300, 2500, 40, 8192, 2, 5000]:
+        lens_l = [rnd.choice([0, 2, 1000, 65536, 300_001, 2_000_003]) for _ in range(n)]
+        lens_l[0] = 2_000_003  # at least one split buffer
+        offs = np.zeros(n, dtype=np.int64)
+        offs[1:] = np.cumsum(np.array(lens_l, dtype=np.int64) + 5)[:-1]
+        mem = torch.randint(0, 256, (int(offs[-1] + lens_l[-1] + 64),), dtype=torch.uint8, device=DEV)
+        ptrs = mem.data_ptr() + torch.tensor(offs, device=DEV)
+        lens = torch.tensor(lens_l, dtype=torch.int64, device=DEV)
+        got = u32(z.crc32_batch_device(ptrs, lens))
+        scratch = torch.empty(z.crc32.scratch_bytes(n), dtype=torch.uint8, device=DEV)
+        ref = u32(z.crc32_batch_device_ws(ptrs, lens, scratch))
+        np.testing.assert_array_equal(got, ref, err_msg=f"n={n}")
+        host = mem.cpu().numpy()
+        exp = o.crc32_batch(host.ctypes.data + offs.astype(np.uint64), np.array(lens_l, dtype=np.uint64),
+                            np.zeros(n, dtype=np.uint32), nthreads=8)
+        np.testing.assert_array_equal(got, exp, err_msg=f"n={n}")

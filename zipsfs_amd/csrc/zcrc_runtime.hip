@@ -208,16 +208,19 @@ int batch_device_ws(const void *const *d_ptrs, const uint64_t *d_lens, const uin
 // launches).  Its scratch -- claim counter, finished-wave counter, split-piece
 // accumulators, prefix -- is zero-filled when allocated and the kernel leaves
 // the counters and accumulators zero, so it has its own per-stream slot
-// (the two-launch path leaves its counter nonzero).  ZCRC_FUSED=0 turns it off.
+// (the two-launch path leaves its counter nonzero).  Opt-in (ZCRC_FUSED=1):
+// on config 2 the in-kernel scan made the CRC launch 7.7 us longer than the
+// plan launch it replaced, 3,713-3,724 vs 3,810-3,839 GiB/s per step on one
+// box (profiles/r02/fused_vs_two_launch_c2.jsonl).
 bool fused_enabled() {
-  static const bool on = [] {
-    const char *e = getenv("ZCRC_FUSED");
-    return !(e && e[0] == '0');
-  }();
-  return on;
+  const char *e = getenv("ZCRC_FUSED");  // read per call: tests switch it
+  return e && e[0] == '1';
 }
 
-size_t fused_scratch_bytes(size_t n) { return kCtrBytes + 8 * n + 8 * (n + 1); }
+// Fixed layout, whatever n: counters | acc[kFusedMaxN] | prefix[kFusedMaxN+1].
+// The accumulators must never overlap a prefix an earlier, smaller batch left
+// in the same slot (the kernel zeroes only the accumulators it used).
+size_t fused_scratch_bytes() { return kCtrBytes + 8 * kFusedMaxN + 8 * (kFusedMaxN + 1); }
 
 int batch_device_fused(const void *const *d_ptrs, const uint64_t *d_lens, const uint32_t *d_seeds, uint32_t *d_out,
                        size_t n, void *scratch, hipStream_t stream) {
@@ -236,7 +239,7 @@ int batch_device_fused(const void *const *d_ptrs, const uint64_t *d_lens, const 
   a.done = reinterpret_cast<uint32_t *>(sc) + 1;
   a.dyn_shift = kDynShift;
   a.acc = reinterpret_cast<uint64_t *>(sc + kCtrBytes);
-  a.prefix = a.acc + n;
+  a.prefix = a.acc + kFusedMaxN;
   return launch_main(a, false, *dc, stream, true);
 }
 
@@ -765,7 +768,7 @@ int zcrc32_batch_device(const void *const *d_ptrs, const uint64_t *d_lens, const
   size_t have = 0;
   std::unique_lock<std::mutex> lk;
   if (n <= kFusedMaxN && fused_enabled()) {
-    const int rc = stream_scratch(st, kScratchFused, fused_scratch_bytes(n), &scratch, &have, &lk);
+    const int rc = stream_scratch(st, kScratchFused, fused_scratch_bytes(), &scratch, &have, &lk);
     if (rc) return rc;
     return batch_device_fused(d_ptrs, d_lens, d_seeds_or_null, d_out, n, scratch, st);
   }
