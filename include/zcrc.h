@@ -50,10 +50,11 @@ extern "C" {
  * caller holds mutex_fhandle (src/ZIPsFS_preloadfileram.c:309-321).  Entries
  * of at least zcrc32_set_gpu_min_bytes() bytes (env ZCRC_GPU_MIN_BYTES; the
  * default is the measured host/GPU crossover) are checksummed
- * on the GPU; smaller ones, and any call whose GPU attempt fails (no device,
- * HIP error), are answered by libzcrc's own host CRC-32 (PCLMUL folding,
- * zcrc_host.cpp).  The first fallback is reported on stderr; all are counted
- * by zcrc32_dropin_stats. */
+ * on the GPU; smaller ones, calls that find every staging slot busy (the
+ * drop-in never waits for staging: the caller holds the lock), and any call
+ * whose GPU attempt fails (no device, HIP error) are answered by libzcrc's
+ * own host CRC-32 (PCLMUL folding, zcrc_host.cpp).  The first fallback is
+ * reported on stderr; all are counted by zcrc32_dropin_stats. */
 uint32_t zcrc32(const void *data, size_t n_bytes, uint32_t crc);
 /* Sets the drop-in's GPU threshold (bytes); returns the previous value. */
 size_t zcrc32_set_gpu_min_bytes(size_t min_bytes);
@@ -67,15 +68,21 @@ int zcrc32_checked(const void *data, size_t n_bytes, uint32_t crc, uint32_t *out
 
 /* Host-resident batch: out[i] = crc32(seeds ? seeds[i] : 0, ptrs[i], lens[i]).
  * Buffers are staged through pinned memory and checksummed on the GPU in
- * as few launches as fit the staging area.  flags: reserved, pass 0. */
+ * as few launches as fit the staging area.  flags: reserved, pass 0.
+ * Staging: a process-wide pool of 16 MiB pinned + 16 MiB HBM slots, at most
+ * ZCRC_STAGING_MIB (env, default 256) of each per device.  A call leases one
+ * slot (waiting while none is free) plus a second if one is free, and
+ * returns them before it returns; streams hold theirs from the first
+ * update() to final(). */
 int zcrc32_batch(const void *const *ptrs, const size_t *lens, const uint32_t *seeds_or_null,
                  uint32_t *out, size_t n, unsigned flags);
 
 /* Device-resident batch.  d_ptrs: device array of n device pointers;
  * d_lens: device array of n byte counts; d_seeds_or_null: device array or
- * NULL; d_out: device array of n results.  Asynchronous on `stream`; uses a
- * stream-ordered scratch allocation of 256 + 8*(n+1) + 8*ceil(n/8192) bytes
- * (work counter, length prefix, plan tile sums). */
+ * NULL; d_out: device array of n results.  Asynchronous on `stream`; its
+ * scratch (work counter, length prefix, plan tile sums: 256 + 8*(n+1) +
+ * 8*ceil(n/8192) bytes) is a grow-only buffer cached per stream (stream-
+ * ordered allocations under graph capture). */
 int zcrc32_batch_device(const void *const *d_ptrs, const uint64_t *d_lens,
                         const uint32_t *d_seeds_or_null, uint32_t *d_out, size_t n, void *stream);
 
@@ -177,6 +184,24 @@ int zcrc_zip_verify_host(const void *archive, size_t archive_len, zcrc_zip_entry
 int zcrc_zip_verify_device(const void *d_archive, size_t archive_len, zcrc_zip_entry *entries, size_t n,
                            void *stream);
 
+/* Stored-entry extraction: what zip_fread() delivers for
+ * a method-0 entry in preloadram_now (src/ZIPsFS_preloadfileram.c:286-288),
+ * plus the check fhandle_check_crc32 makes on it (:237-250), for a batch.
+ * For every entries[i] (from zcrc_zip_scan) that is stored, unencrypted, in
+ * range and fits dst[i] (cap[i] >= comp_size; dst[i] may be NULL for an
+ * empty entry), the entry's bytes are copied
+ * into dst[i] and the CRC-32 of the copy is compared with the central
+ * directory's: status ZCRC_ZIP_OK or ZCRC_ZIP_MISMATCH, crc_computed set.
+ * Other entries are not copied and come back ZCRC_ZIP_UNVERIFIED (BAD stays
+ * BAD).  _device: d_archive and d_dst[i] are device memory (d_dst itself is a
+ * host array); one batched copy launch and one batched CRC launch on
+ * `stream`, synchronous.  _host: host memory; the copy is a host memcpy and
+ * the CRCs one zcrc32_batch call over the copies. */
+int zcrc_zip_extract_stored_device(const void *d_archive, size_t archive_len, zcrc_zip_entry *entries,
+                                   void *const *d_dst, const size_t *cap, size_t n, void *stream);
+int zcrc_zip_extract_stored_host(const void *archive, size_t archive_len, zcrc_zip_entry *entries,
+                                 void *const *dst, const size_t *cap, size_t n);
+
 /* GF(2) algebra (pure integer math, no data access):
  * crc32(A||B) == zcrc32_combine(crc32(A), crc32(B), |B|)   (zlib semantics). */
 uint32_t zcrc32_combine(uint32_t crc_a, uint32_t crc_b, uint64_t len_b);
@@ -189,6 +214,9 @@ int zcrc_fill_synthetic(const uint64_t *d_ptrs, const uint64_t *d_lens, size_t n
                         uint64_t index_step, uint64_t seed, void *stream);
 
 /* Diagnostics / measurement. */
+/* Host staging pool: pinned bytes allocated (all devices), slots leased now,
+ * most slots ever leased at once, and the per-device slot budget. */
+int zcrc_staging_info(uint64_t *pinned_bytes, uint64_t *slots_in_use, uint64_t *slots_peak, uint64_t *slots_budget);
 const char *zcrc_last_error(void);
 const char *zcrc_version(void);
 int zcrc_device_info(int *num_cus, int *arch_major, int *arch_minor);

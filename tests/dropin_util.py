@@ -78,3 +78,34 @@ def run_harness(exe, records_path, env_extra=None) -> tuple:
             i, crc, st = line.split()
             rows.append((int(i), int(crc, 16), st == "ok"))
     return p.returncode, rows, stats, p.stderr
+
+
+def build_preload_harness(tmp_path) -> str:
+    """tests/dropin/preload_main.c: preloadram_now's read loop + the CRC check."""
+    exe = os.path.join(str(tmp_path), "preload_main")
+    cmd = ["gcc", "-O1", "-Wall", "-Werror", "-I", os.path.join(ROOT, "zipsfs_amd"), "-I",
+           os.path.join(ROOT, "include"), os.path.join(HERE, "dropin", "preload_main.c"), "-o", exe,
+           "-L", os.path.join(ROOT, "zipsfs_amd"), "-lzcrc", "-Wl,-rpath," + os.path.join(ROOT, "zipsfs_amd"),
+           "-pthread", "-ldl"]
+    subprocess.run(cmd, check=True)
+    return exe
+
+
+REF_O0 = os.path.join(ROOT, "oracle", "_ref", "libref_cg_crc32_O0.so")
+
+
+def run_preload(exe, entry_path, expected, reps, modes, env_extra=None) -> tuple:
+    """-> (returncode, {mode: row}, stats, stderr)."""
+    env = dict(os.environ)
+    env["ZCRC_REF_LIB"] = REF_O0
+    env.update(env_extra or {})
+    p = subprocess.run([exe, str(entry_path), f"{expected & 0xFFFFFFFF:08x}", str(reps)] + list(modes),
+                       capture_output=True, text=True, env=env, timeout=600)
+    rows, stats = {}, {}
+    for line in p.stdout.splitlines():
+        d = json.loads(line)
+        if "stats" in d:
+            stats = d["stats"]
+        else:
+            rows[d["mode"]] = d
+    return p.returncode, rows, stats, p.stderr

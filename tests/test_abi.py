@@ -121,7 +121,8 @@ def test_product_has_no_cpu_crc_path():
     rt = callers["zcrc_runtime.hip"]
     body = rt[rt.index("uint32_t zcrc32(const void *data"):]
     body = body[:body.index("\n}\n")]
-    assert rt.count("host_crc32(") == body.count("host_crc32(") == 2  # below threshold or no device; GPU failure
+    # below threshold or no device; every staging slot busy; GPU failure
+    assert rt.count("host_crc32(") == body.count("host_crc32(") == 3
 
 
 def test_missing_gpu_fails_loudly():
@@ -244,3 +245,20 @@ def test_dropin_never_aborts_without_gpu(tmp_path):
     du.write_records(tmp_path / "bad.bin", bad)
     rc, rows, _, err = du.run_harness(exe, tmp_path / "bad.bin", {"HIP_VISIBLE_DEVICES": ""})
     assert rc == 1 and rows == [(0, 0xCBF43926, False)] and "crc32-mismatch" in err
+
+
+def test_preload_harness_without_gpu(tmp_path):
+    """The preloadram_now harness (tests/dropin/preload_main.c) built against
+    the drop-in runs without a GPU: the drop-in answers from libzcrc's host
+    CRC, never aborts, and equals the reference's own cg_crc32 (-O0)."""
+    import dropin_util as du
+    from oracle import oracle as o
+    exe = du.build_preload_harness(tmp_path)
+    path = tmp_path / "entry.bin"
+    o.payload(300_001, 9).tofile(path)
+    exp = o.payload_crc(300_001, 9)
+    modes = ["dropin"] + (["ref"] if os.path.exists(du.REF_O0) else [])
+    rc, rows, stats, err = du.run_preload(exe, path, exp, 2, modes, {"HIP_VISIBLE_DEVICES": ""})
+    assert rc == 0, err
+    assert all(r["ok"] for r in rows.values()), rows
+    assert stats["fallback"] == 0 and stats["gpu"] == 0

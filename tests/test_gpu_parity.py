@@ -642,3 +642,73 @@ def test_fused_scratch_reuse_across_batch_sizes(fused, monkeypatch):
         exp = o.crc32_batch(host.ctypes.data + offs.astype(np.uint64), np.array(lens_l, dtype=np.uint64),
                             np.zeros(n, dtype=np.uint32), nthreads=8)
         np.testing.assert_array_equal(got, exp, err_msg=f"n={n}")
+
+
+@pytest.mark.parametrize("device", [True, False])
+def test_zip_extract_stored(device):
+    """Stored-entry extraction (the zip_fread of a method-0
+    entry, src/ZIPsFS_preloadfileram.c:286-288): bytes equal zipfile's, CRCs
+    equal the central directory's, every length and source alignment the
+    archive produces (names of 1..40 bytes shift the data offsets); a flipped
+    byte is delivered as stored and flagged ZIP_MISMATCH; deflated entries are
+    not extracted."""
+    import io
+    import zipfile
+    from zipsfs_amd import zipverify as zv
+    rnd = random.Random(8)
+    buf = io.BytesIO()
+    payloads = {}
+    with zipfile.ZipFile(buf, "w", allowZip64=True) as zf:
+        for i in range(240):
+            n = rnd.choice([0, 1, 2, 3, 15, 16, 17, 31, 4095, 65535, 65536, 65537, 200_003, 1_500_007])
+            name = f"s{i}_" + "x" * rnd.randint(0, 40)
+            payloads[name] = o.payload(n, 7000 + i).tobytes()
+            zf.writestr(name, payloads[name], compress_type=zipfile.ZIP_DEFLATED if i % 7 == 0 else zipfile.ZIP_STORED)
+    data = bytearray(buf.getvalue())
+    res = zv.extract_stored(bytes(data), device=device)
+    assert len(res) == 240
+    for chk, got in res:
+        if chk.method == 8:
+            assert got is None and chk.status == zv.ZIP_UNVERIFIED
+            continue
+        assert chk.status == zv.ZIP_OK, chk
+        g = got.cpu().numpy().tobytes() if device else got.tobytes()
+        assert g == payloads[chk.name], chk.name
+        assert chk.crc_computed == zlib.crc32(payloads[chk.name])
+    big = [c for c, _ in res if c.method == 0 and c.comp_size > 100_000][0]
+    data[big.data_offset + big.comp_size // 3] ^= 0x04
+    res = zv.extract_stored(bytes(data), device=device)
+    bad = [(c, g) for c, g in res if c.status != zv.ZIP_OK and c.method == 0]
+    assert [c.name for c, _ in bad] == [big.name] and bad[0][0].status == zv.ZIP_MISMATCH
+    g = bad[0][1].cpu().numpy().tobytes() if device else bad[0][1].tobytes()
+    assert g == bytes(data[big.data_offset: big.data_offset + big.comp_size])
+    assert bad[0][0].crc_computed == zlib.crc32(g)
+
+
+@pytest.mark.parametrize("fused", ["0", "1"])
+def test_scratch_growth_is_stream_ordered(fused, monkeypatch):
+    """The per-stream scratch grows while launches are queued on its stream:
+    the new buffer's zero fill must be ordered before the plan that follows
+    on the same stream (a null-stream memset was not, and could zero a prefix
+    the plan had just written).  Fresh streams, growing n, no sync between
+    launches, every result vs the oracle."""
+    monkeypatch.setenv("ZCRC_FUSED", fused)
+    rnd = random.Random(4242)
+    total = 16 << 20
+    mem = torch.randint(0, 256, (total,), dtype=torch.uint8, device=DEV)
+    host = mem.cpu().numpy()
+    for rep in range(3):
+        st = torch.cuda.Stream(device=DEV)
+        jobs = []
+        with torch.cuda.stream(st):
+            for n in [50, 7000, 8192, 9000, 30000, 8100, 70000, 3]:
+                ln = [rnd.randint(0, 300) for _ in range(n)]
+                offs = [rnd.randrange(0, total - L) for L in ln]
+                ptrs = torch.tensor([mem.data_ptr() + q for q in offs], dtype=torch.int64, device=DEV)
+                lt = torch.tensor(ln, dtype=torch.int64, device=DEV)
+                jobs.append((offs, ln, z.crc32_batch_device(ptrs, lt), ptrs, lt))
+        st.synchronize()
+        for offs, ln, got, _, _ in jobs:
+            ap = np.array([host.ctypes.data + q for q in offs], dtype=np.uint64)
+            exp = o.crc32_batch(ap, np.array(ln, dtype=np.uint64), np.zeros(len(ln), dtype=np.uint32), nthreads=8)
+            np.testing.assert_array_equal(u32(got), exp, err_msg=f"rep {rep} n={len(ln)}")

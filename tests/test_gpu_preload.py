@@ -1,0 +1,47 @@
+"""GPU: preloadram_now's read loop with the CRC check (SURVEY 8(a) a6/a5 and
+8(f) rank 1), as a C program against the drop-in and the stream API.
+
+tests/dropin/preload_main.c reads an entry file in 16 MiB read() calls into
+one mmap'd segment (src/ZIPsFS_preloadfileram.c:284-306) and checks the CRC
+under mutex_fhandle (:309-321): with the drop-in cg_crc32 after the loop,
+with zcrc32_stream_update per chunk and zcrc32_stream_final after it, and
+with the reference's own cg_crc32 built -O0 as shipped (oracle/_ref, test
+infrastructure).  Every mode must produce the expected CRC; the lock hold
+times are printed (and written to $ZCRC_PRELOAD_TABLE as JSON lines when
+set, for DESIGN.md section 10b)."""
+import json
+import os
+
+import pytest
+
+import dropin_util as du
+from oracle import oracle as o
+
+pytestmark = pytest.mark.gpu
+
+SIZES = [4 << 10, 1 << 20, 16 << 20, 64 << 20, 256 << 20]
+
+
+@pytest.mark.parametrize("size", SIZES)
+def test_preload_loop_modes(tmp_path, size):
+    exe = du.build_preload_harness(tmp_path)
+    path = tmp_path / "entry.bin"
+    o.payload(size, 41).tofile(path)
+    exp = o.payload_crc(size, 41)
+    reps = 5 if size <= (16 << 20) else 3
+    modes = ["dropin", "stream"] + (["ref"] if os.path.exists(du.REF_O0) else [])
+    rc, rows, stats, err = du.run_preload(exe, path, exp, reps, modes)
+    assert rc == 0, err
+    rc2, rows_gpu, stats2, err2 = du.run_preload(exe, path, exp, reps, ["dropin"], {"ZCRC_GPU_MIN_BYTES": "0"})
+    assert rc2 == 0, err2
+    rows["dropin_all_gpu"] = dict(rows_gpu["dropin"], mode="dropin_all_gpu")
+    for m, r in rows.items():
+        if "skipped" not in r:
+            assert r["ok"] and int(r["crc"], 16) == exp, (m, r)
+    assert stats2 == {"gpu": reps, "host": 0, "fallback": 0}, stats2
+    line = {"size": size, "rows": rows}
+    print(json.dumps(line))
+    out = os.environ.get("ZCRC_PRELOAD_TABLE")
+    if out:
+        with open(out, "a") as f:
+            f.write(json.dumps(line) + "\n")

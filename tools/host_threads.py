@@ -1,0 +1,65 @@
+"""Host-resident path under ZIPsFS's thread model (measurement only).
+
+  * stream open + close latency per ZIP entry (zcrc32_stream_open/close,
+    pooled objects) and the first update + final of a 4 KiB entry;
+  * aggregate host-resident GiB/s of zcrc32_checked (GPU path, staged through
+    the process-wide pinned pool) from 1, 8 and 32 threads, each thread
+    checksumming its own 64 MiB entry 4 times;
+  * the pool's pinned footprint afterwards.
+Prints one JSON object."""
+import ctypes
+import json
+import sys
+import time
+from concurrent.futures import ThreadPoolExecutor
+
+import numpy as np
+
+sys.path.insert(0, ".")
+import zipsfs_amd as z  # noqa: E402
+from zipsfs_amd import _lib  # noqa: E402
+
+lib = _lib.lib()
+res = {}
+small = np.random.default_rng(1).integers(0, 256, 4096, dtype=np.uint8)
+crc = ctypes.c_uint32()
+for _ in range(20):  # warm the pool
+    s = lib.zcrc32_stream_open(0)
+    lib.zcrc32_stream_update(s, small.ctypes.data, small.size)
+    lib.zcrc32_stream_final(s, ctypes.byref(crc))
+    lib.zcrc32_stream_close(s)
+N = 2000
+t0 = time.perf_counter()
+for _ in range(N):
+    lib.zcrc32_stream_close(lib.zcrc32_stream_open(0))
+res["stream_open_close_us"] = (time.perf_counter() - t0) / N * 1e6
+t0 = time.perf_counter()
+for _ in range(200):
+    s = lib.zcrc32_stream_open(0)
+    lib.zcrc32_stream_update(s, small.ctypes.data, small.size)
+    lib.zcrc32_stream_final(s, ctypes.byref(crc))
+    lib.zcrc32_stream_close(s)
+res["stream_4k_entry_us"] = (time.perf_counter() - t0) / 200 * 1e6
+
+ENTRY = 64 << 20
+REPS = 4
+bufs = [np.random.default_rng(10 + t).integers(0, 256, ENTRY, dtype=np.uint8) for t in range(32)]
+
+
+def one(t):
+    out = ctypes.c_uint32()
+    for _ in range(REPS):
+        rc = lib.zcrc32_checked(bufs[t].ctypes.data, ENTRY, 0, ctypes.byref(out))
+        assert rc == 0
+    return out.value
+
+
+for threads in (1, 8, 32):
+    one(0)
+    t0 = time.perf_counter()
+    with ThreadPoolExecutor(threads) as ex:
+        list(ex.map(one, range(threads)))
+    dt = time.perf_counter() - t0
+    res[f"host_resident_gibs_{threads}_threads"] = threads * REPS * ENTRY / dt / 2**30
+res["staging"] = z.staging_info()
+print(json.dumps(res))

@@ -31,6 +31,7 @@ _SIGNATURES = {
     "zcrc32_checked": (_c_int, [_c_p, _c_sz, _c_u32, ctypes.POINTER(_c_u32)]),
     "zcrc32_set_gpu_min_bytes": (_c_sz, [_c_sz]),
     "zcrc32_dropin_stats": (None, [ctypes.POINTER(_c_u64)] * 3),
+    "zcrc_staging_info": (ctypes.c_int, [ctypes.POINTER(_c_u64)] * 4),
     "zcrc32_batch": (_c_int, [_c_p, _c_p, _c_p, _c_p, _c_sz, ctypes.c_uint]),
     "zcrc32_batch_device": (_c_int, [_c_p, _c_p, _c_p, _c_p, _c_sz, _c_p]),
     "zcrc32_batch_device_scratch_bytes": (_c_sz, [_c_sz]),

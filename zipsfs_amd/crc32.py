@@ -372,5 +372,13 @@ def device_info() -> dict:
     return {"num_cus": a.value, "major": b.value, "minor": c.value}
 
 
+def staging_info() -> dict:
+    """Host staging pool (zcrc_staging_info): pinned bytes allocated, slots
+    leased now, most slots leased at once, per-device slot budget."""
+    v = [ctypes.c_uint64() for _ in range(4)]
+    check(lib().zcrc_staging_info(*[ctypes.byref(x) for x in v]), "zcrc_staging_info")
+    return dict(zip(["pinned_bytes", "slots_in_use", "slots_peak", "slots_budget"], [x.value for x in v]))
+
+
 def version() -> str:
     return lib().zcrc_version().decode()

@@ -1,7 +1,8 @@
 // zcrc_runtime.hip -- host runtime and C ABI of libzcrc (include/zcrc.h).
 //
-// Owns: per-device table upload (once, thread-safe), per-thread pinned staging
-// for host-resident batches, stream-ordered scratch for device batches, and
+// Owns: per-device table upload (once, thread-safe), a process-wide pool of
+// pinned staging slots for host-resident calls (fixed budget), per-stream
+// scratch for device batches, and
 // optional HIP-event profiling of the main kernel.  Every batched and
 // device-resident entry point checksums on the GPU and reports failures; only
 // the drop-in zcrc32() answers from the host CRC (zcrc_host.cpp) -- below its
@@ -168,7 +169,12 @@ int stream_scratch(hipStream_t st, int use, size_t bytes, void **out, size_t *ha
     }
     const size_t nb = std::max<size_t>(bytes, 64u << 10);
     ZCRC_HIP_TRY(hipMalloc(&slot.first, nb));
-    ZCRC_HIP_TRY(hipMemset(slot.first, 0, nb));
+    // zero it ON `st`: a null-stream hipMemset is not ordered with a
+    // non-blocking stream, so it could land after the plan kernel queued next
+    // on `st` had written the prefix -- a zeroed, non-monotone prefix sent
+    // the CRC kernel's piece walk outside every buffer (the intermittent
+    // illegal-address fault of the multi-stream tests, rounds 1-2)
+    ZCRC_HIP_TRY(hipMemsetAsync(slot.first, 0, nb, st));
     slot.second = nb;
   }
   *out = slot.first;
@@ -243,15 +249,23 @@ int batch_device_fused(const void *const *d_ptrs, const uint64_t *d_lens, const 
   return launch_main(a, false, *dc, stream, true);
 }
 
-// ------------------------------------------------------------- host batch
-// Per-thread staging: two slots, each a pinned host area + a device area of
-// kStageBytes for payload and metadata.  Slot s is filled by the CPU while
-// the GPU works on slot s^1 (own stream per slot).
+// ------------------------------------------------------------- host staging
+// Process-wide pool of staging slots under a fixed budget.  ZIPsFS calls the
+// drop-in from up to ROOTS=32 preload threads (src/ZIPsFS_configuration.h:110,
+// src/ZIPsFS_async.c:468); per-thread staging pinned 2 x 64 MiB of host memory
+// and 2 x 64 MiB of HBM per thread for the life of the thread.  Now a call
+// leases one slot (blocking only while it holds none) and a second one if one
+// is free (double buffering), and returns them when it ends; a stream holds
+// its slots only between its first update and final().  Slots are created
+// lazily up to ZCRC_STAGING_MIB (default 256 MiB: 16 slots of 16 MiB pinned +
+// 16 MiB HBM) per device and kept for the life of the process.
 
-constexpr size_t kStageBytes = 64ull << 20;
-constexpr size_t kStageItems = 1u << 16;
+constexpr size_t kStageBytes = 16ull << 20;  // = ZIPsFS PRELOADRAM_READ_BYTES_NUM
+constexpr size_t kStageItems = 1u << 14;
+constexpr size_t kDefaultStagingMiB = 256;
 
 struct StageSlot {
+  int dev = -1;
   hipStream_t stream = nullptr;
   hipEvent_t done = nullptr;    // slot reusable after this
   hipEvent_t kernel = nullptr;  // kernel finished (continuation seeds)
@@ -270,44 +284,141 @@ constexpr size_t kMetaSeeds = kMetaPrefix + 8 * (kStageItems + 1);
 constexpr size_t kMetaRes = kMetaSeeds + 4 * kStageItems;
 constexpr size_t kMetaBytes = kMetaRes + 4 * kStageItems;
 
-struct HostCtx {
-  int dev = -1;
-  StageSlot slot[2];
-  ~HostCtx() {
-    for (auto &s : slot) {
-      if (s.stream) (void)hipStreamSynchronize(s.stream);
-      if (s.h_data) (void)hipHostFree(s.h_data);
-      if (s.h_meta) (void)hipHostFree(s.h_meta);
-      if (s.d_data) (void)hipFree(s.d_data);
-      if (s.d_meta) (void)hipFree(s.d_meta);
-      if (s.done) (void)hipEventDestroy(s.done);
-      if (s.kernel) (void)hipEventDestroy(s.kernel);
-      if (s.stream) (void)hipStreamDestroy(s.stream);
-    }
-  }
-};
-
-thread_local HostCtx t_host;
-
-int host_ctx_init() {
-  int dev = 0;
-  ZCRC_HIP_TRY(hipGetDevice(&dev));
-  if (t_host.dev == dev) return ZCRC_OK;
-  if (t_host.dev != -1) return fail(ZCRC_ERR_ARG, "host staging bound to another device in this thread");
-  for (auto &s : t_host.slot) {
-    ZCRC_HIP_TRY(hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking));
-    ZCRC_HIP_TRY(hipEventCreateWithFlags(&s.done, hipEventDisableTiming));
-    ZCRC_HIP_TRY(hipEventCreateWithFlags(&s.kernel, hipEventDisableTiming));
-    ZCRC_HIP_TRY(hipHostMalloc(reinterpret_cast<void **>(&s.h_data), kStageBytes, hipHostMallocDefault));
-    ZCRC_HIP_TRY(hipHostMalloc(reinterpret_cast<void **>(&s.h_meta), kMetaBytes, hipHostMallocDefault));
-    ZCRC_HIP_TRY(hipMalloc(reinterpret_cast<void **>(&s.d_data), kStageBytes));
-    ZCRC_HIP_TRY(hipMalloc(reinterpret_cast<void **>(&s.d_meta), kMetaBytes));
-    ZCRC_HIP_TRY(hipHostGetDevicePointer(reinterpret_cast<void **>(&s.h_data_dev), s.h_data, 0));
-    ZCRC_HIP_TRY(hipHostGetDevicePointer(reinterpret_cast<void **>(&s.h_meta_dev), s.h_meta, 0));
-  }
-  t_host.dev = dev;
+int slot_create(int dev, StageSlot *s) {
+  s->dev = dev;
+  ZCRC_HIP_TRY(hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking));
+  ZCRC_HIP_TRY(hipEventCreateWithFlags(&s->done, hipEventDisableTiming));
+  ZCRC_HIP_TRY(hipEventCreateWithFlags(&s->kernel, hipEventDisableTiming));
+  ZCRC_HIP_TRY(hipHostMalloc(reinterpret_cast<void **>(&s->h_data), kStageBytes, hipHostMallocDefault));
+  ZCRC_HIP_TRY(hipHostMalloc(reinterpret_cast<void **>(&s->h_meta), kMetaBytes, hipHostMallocDefault));
+  ZCRC_HIP_TRY(hipMalloc(reinterpret_cast<void **>(&s->d_data), kStageBytes));
+  ZCRC_HIP_TRY(hipMalloc(reinterpret_cast<void **>(&s->d_meta), kMetaBytes));
+  ZCRC_HIP_TRY(hipHostGetDevicePointer(reinterpret_cast<void **>(&s->h_data_dev), s->h_data, 0));
+  ZCRC_HIP_TRY(hipHostGetDevicePointer(reinterpret_cast<void **>(&s->h_meta_dev), s->h_meta, 0));
   return ZCRC_OK;
 }
+
+void slot_destroy(StageSlot *s) {
+  if (s->stream) (void)hipStreamSynchronize(s->stream);
+  if (s->h_data) (void)hipHostFree(s->h_data);
+  if (s->h_meta) (void)hipHostFree(s->h_meta);
+  if (s->d_data) (void)hipFree(s->d_data);
+  if (s->d_meta) (void)hipFree(s->d_meta);
+  if (s->done) (void)hipEventDestroy(s->done);
+  if (s->kernel) (void)hipEventDestroy(s->kernel);
+  if (s->stream) (void)hipStreamDestroy(s->stream);
+  delete s;
+}
+
+class SlotPool {
+ public:
+  static SlotPool &get() {
+    static SlotPool *pool = new SlotPool();  // never destroyed: slots outlive static destructors
+    return *pool;
+  }
+  // A slot of device `dev`: a free one, a new one while under budget, else
+  // (wait) the next one released -- or *out = nullptr (no wait).
+  int acquire(int dev, bool wait, StageSlot **out) {
+    *out = nullptr;
+    std::unique_lock<std::mutex> lk(mu_);
+    Dev &d = dev_[dev];
+    for (;;) {
+      if (!d.free.empty()) {
+        *out = d.free.back();
+        d.free.pop_back();
+        note_in_use(+1);
+        return ZCRC_OK;
+      }
+      if (d.created < budget_slots_) {
+        d.created++;
+        note_in_use(+1);
+        lk.unlock();
+        StageSlot *s = new (std::nothrow) StageSlot();
+        const int rc = s ? slot_create(dev, s) : fail(ZCRC_ERR_HIP, "out of host memory");
+        if (rc) {
+          if (s) slot_destroy(s);
+          lk.lock();
+          d.created--;
+          note_in_use(-1);
+          cv_.notify_all();
+          return rc;
+        }
+        *out = s;
+        return ZCRC_OK;
+      }
+      if (!wait) return ZCRC_OK;
+      cv_.wait(lk);
+    }
+  }
+  void release(StageSlot *s) {
+    if (!s) return;
+    (void)hipStreamSynchronize(s->stream);  // nothing of the last user still queued
+    s->busy = false;
+    s->scatter.clear();
+    std::lock_guard<std::mutex> lk(mu_);
+    dev_[s->dev].free.push_back(s);
+    note_in_use(-1);
+    cv_.notify_one();
+  }
+  void info(uint64_t *pinned, uint64_t *in_use, uint64_t *peak, uint64_t *budget) {
+    std::lock_guard<std::mutex> lk(mu_);
+    uint64_t created = 0;
+    for (auto &kv : dev_) created += kv.second.created;
+    if (pinned) *pinned = created * (kStageBytes + kMetaBytes);
+    if (in_use) *in_use = in_use_;
+    if (peak) *peak = peak_;
+    if (budget) *budget = budget_slots_;
+  }
+
+ private:
+  struct Dev {
+    std::vector<StageSlot *> free;
+    size_t created = 0;
+  };
+  SlotPool() {
+    size_t mib = kDefaultStagingMiB;
+    if (const char *e = getenv("ZCRC_STAGING_MIB")) {
+      char *end = nullptr;
+      const unsigned long long v = strtoull(e, &end, 0);
+      if (end != e) mib = (size_t)v;
+    }
+    budget_slots_ = std::max<size_t>(1, (mib << 20) / kStageBytes);
+  }
+  void note_in_use(int d) {
+    in_use_ += d;
+    peak_ = std::max(peak_, in_use_);
+  }
+  std::mutex mu_;
+  std::condition_variable cv_;
+  std::map<int, Dev> dev_;
+  size_t budget_slots_ = 1, in_use_ = 0, peak_ = 0;
+};
+
+// Up to two slots for one call, returned on scope exit.
+struct Lease {
+  StageSlot *slot[2] = {nullptr, nullptr};
+  int count = 0;
+  // first slot: waits while none is free (or, !wait, returns with count 0);
+  // second slot only if one is free right now (a holder never waits)
+  int take(bool wait, bool want_two) {
+    int dev = 0;
+    ZCRC_HIP_TRY(hipGetDevice(&dev));
+    int rc = SlotPool::get().acquire(dev, wait, &slot[0]);
+    if (rc || !slot[0]) return rc;
+    count = 1;
+    if (want_two) {
+      rc = SlotPool::get().acquire(dev, false, &slot[1]);
+      if (rc) return ZCRC_OK;  // one slot will do
+      if (slot[1]) count = 2;
+    }
+    return ZCRC_OK;
+  }
+  void give_back() {
+    for (auto &s : slot) SlotPool::get().release(s), s = nullptr;
+    count = 0;
+  }
+  ~Lease() { give_back(); }
+};
 
 // Packing host buffers into pinned staging is the host-side bottleneck of the
 // host-resident path (one core copies ~10 GB/s, PCIe 5 x16 moves ~50).  A
@@ -331,7 +442,13 @@ class CopyPool {
       for (auto &j : jobs) memcpy(j.dst, j.src, j.len);
       return;
     }
-    std::lock_guard<std::mutex> serial(run_mu_);  // one batch at a time
+    // one batch at a time in the pool; a caller that finds it busy copies its
+    // own jobs (concurrent callers copy in parallel instead of queueing)
+    std::unique_lock<std::mutex> serial(run_mu_, std::try_to_lock);
+    if (!serial.owns_lock()) {
+      for (auto &j : jobs) memcpy(j.dst, j.src, j.len);
+      return;
+    }
     pieces_.clear();
     for (auto &j : jobs)
       for (size_t off = 0; off < j.len; off += kPiece)
@@ -416,9 +533,8 @@ int slot_finish(StageSlot &s, uint32_t *out) {
 // 48.3 us staged (tools/bench_host.py), so buffers up to 64 KiB go direct.
 constexpr size_t kDirectBytes = 1u << 20, kDirectItems = 4096, kDirectMaxBuf = 64u << 10;
 
-int batch_host_direct(const DeviceCtx &dc, const void *const *ptrs, const size_t *lens, const uint32_t *seeds,
-                      uint32_t *out, size_t n) {
-  StageSlot &s = t_host.slot[0];
+int batch_host_direct(const DeviceCtx &dc, StageSlot &s, const void *const *ptrs, const size_t *lens,
+                      const uint32_t *seeds, uint32_t *out, size_t n) {
   const size_t off_prefix = 8 * n, off_seeds = off_prefix + 8 * (n + 1);
   uint64_t *h_ptrs = reinterpret_cast<uint64_t *>(s.h_meta);
   uint64_t *h_prefix = reinterpret_cast<uint64_t *>(s.h_meta + off_prefix);
@@ -453,23 +569,27 @@ int batch_host_direct(const DeviceCtx &dc, const void *const *ptrs, const size_t
   return ZCRC_OK;
 }
 
-int batch_host(const void *const *ptrs, const size_t *lens, const uint32_t *seeds, uint32_t *out, size_t n) {
+// kBusy: no staging slot was free and the caller asked not to wait
+constexpr int kBusy = 1;
+
+int batch_host(const void *const *ptrs, const size_t *lens, const uint32_t *seeds, uint32_t *out, size_t n,
+               bool wait = true) {
   if (n == 0) return ZCRC_OK;
   if (!ptrs || !lens || !out) return fail(ZCRC_ERR_ARG, "null argument");
   DeviceCtx *dc = nullptr;
   int rc = device_ctx(&dc);
   if (rc) return rc;
-  rc = host_ctx_init();
-  if (rc) return rc;
-  if (n <= kDirectItems) {
-    size_t staged = 0;
-    bool direct = true;
-    for (size_t i = 0; i < n && direct; i++) {
-      staged += (lens[i] + 15) & ~size_t(15);
-      direct = lens[i] <= kDirectMaxBuf && staged <= kDirectBytes;
-    }
-    if (direct) return batch_host_direct(*dc, ptrs, lens, seeds, out, n);
+  bool direct = n <= kDirectItems;
+  size_t total = 0;
+  for (size_t i = 0; i < n; i++) {
+    total += (lens[i] + 15) & ~size_t(15);
+    direct = direct && lens[i] <= kDirectMaxBuf && total <= kDirectBytes;
   }
+  Lease lease;
+  rc = lease.take(wait, !direct && total > kStageBytes);
+  if (rc) return rc;
+  if (!lease.count) return kBusy;
+  if (direct) return batch_host_direct(*dc, *lease.slot[0], ptrs, lens, seeds, out, n);
 
   int cur = 0;
   size_t i = 0;          // next buffer
@@ -477,7 +597,7 @@ int batch_host(const void *const *ptrs, const size_t *lens, const uint32_t *seed
   int prev_slot = -1;    // slot of the previous launch
   uint32_t prev_item = 0;  // its last item (continuation source)
   while (i < n) {
-    StageSlot &s = t_host.slot[cur];
+    StageSlot &s = *lease.slot[cur];
     rc = slot_finish(s, out);
     if (rc) return rc;
     uint64_t *h_ptrs = reinterpret_cast<uint64_t *>(s.h_meta + kMetaPtrs);
@@ -529,9 +649,10 @@ int batch_host(const void *const *ptrs, const size_t *lens, const uint32_t *seed
     // is ordered after it (kernels use the whole GPU anyway).  This also keeps
     // a continuation's read of the other slot's results ahead of that slot's
     // next memset.
-    if (prev_slot >= 0) ZCRC_HIP_TRY(hipStreamWaitEvent(s.stream, t_host.slot[prev_slot].kernel, 0));
+    if (prev_slot >= 0 && prev_slot != cur)
+      ZCRC_HIP_TRY(hipStreamWaitEvent(s.stream, lease.slot[prev_slot]->kernel, 0));
     if (continuation) {
-      StageSlot &p = t_host.slot[prev_slot];
+      StageSlot &p = *lease.slot[prev_slot];
       ZCRC_HIP_TRY(hipMemcpyAsync(d_seeds, reinterpret_cast<uint32_t *>(p.d_meta + kMetaRes) + prev_item, 4,
                                   hipMemcpyDeviceToDevice, s.stream));
     }
@@ -552,16 +673,18 @@ int batch_host(const void *const *ptrs, const size_t *lens, const uint32_t *seed
     s.busy = true;
     prev_slot = cur;
     prev_item = (uint32_t)(items - 1);
-    cur ^= 1;
+    cur = (cur + 1) % lease.count;
   }
-  rc = slot_finish(t_host.slot[cur], out);
-  if (rc) return rc;
-  return slot_finish(t_host.slot[cur ^ 1], out);
+  for (int k = 0; k < lease.count; k++) {
+    rc = slot_finish(*lease.slot[k], out);
+    if (rc) return rc;
+  }
+  return ZCRC_OK;
 }
 
 // ------------------------------------------------------------- streaming
 
-constexpr size_t kStreamChunk = 16ull << 20;  // ZIPsFS PRELOADRAM_READ_BYTES_NUM
+constexpr size_t kStreamChunk = kStageBytes;  // ZIPsFS PRELOADRAM_READ_BYTES_NUM
 
 }  // namespace
 
@@ -569,49 +692,58 @@ int set_error(int code, const char *msg) { return fail(code, msg); }
 
 }  // namespace zcrc
 
+// A stream object owns a HIP stream, two events and a 2-word device CRC cell;
+// closed streams go back to a free list (no allocation per ZIP entry).  Its
+// pinned/HBM staging is leased from the SlotPool by the first update() and
+// returned by final() and close(), so an open but idle stream holds none.
 struct zcrc32_stream {
   int dev = -1;
   hipStream_t stream = nullptr;
-  uint8_t *h_stage[2] = {nullptr, nullptr};
-  uint8_t *d_stage[2] = {nullptr, nullptr};
-  hipEvent_t staged[2] = {nullptr, nullptr};  // H2D from h_stage[b] finished
+  zcrc::StageSlot *slot[2] = {nullptr, nullptr};
+  int nslot = 0;
+  hipEvent_t staged[2] = {nullptr, nullptr};  // H2D from slot[b]'s pinned area finished
   uint32_t *d_crc = nullptr;                  // [2] ping-pong running CRC
   uint64_t parts = 0;                         // chunk launches so far
   uint32_t seed = 0;
-  bool dirty = false;                         // any update since open/final
 };
 
 namespace zcrc {
 namespace {
 
-void stream_free(zcrc32_stream *s) {
+constexpr size_t kStreamFreeMax = 64;  // idle stream objects kept per process
+std::mutex g_streams_mu;
+std::vector<zcrc32_stream *> g_streams_free;
+
+void stream_release_slots(zcrc32_stream *s) {
+  for (int b = 0; b < 2; b++) SlotPool::get().release(s->slot[b]), s->slot[b] = nullptr;
+  s->nslot = 0;
+}
+
+void stream_destroy(zcrc32_stream *s) {
   if (!s) return;
   if (s->stream) (void)hipStreamSynchronize(s->stream);
-  for (int b = 0; b < 2; b++) {
-    if (s->h_stage[b]) (void)hipHostFree(s->h_stage[b]);
-    if (s->d_stage[b]) (void)hipFree(s->d_stage[b]);
+  stream_release_slots(s);
+  for (int b = 0; b < 2; b++)
     if (s->staged[b]) (void)hipEventDestroy(s->staged[b]);
-  }
   if (s->d_crc) (void)hipFree(s->d_crc);
   if (s->stream) (void)hipStreamDestroy(s->stream);
   delete s;
 }
 
-int stream_init(zcrc32_stream *s, uint32_t seed) {
-  DeviceCtx *dc = nullptr;
-  int rc = device_ctx(&dc);
-  if (rc) return rc;
+int stream_create(zcrc32_stream *s) {
   ZCRC_HIP_TRY(hipGetDevice(&s->dev));
   ZCRC_HIP_TRY(hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking));
-  for (int b = 0; b < 2; b++) {
-    ZCRC_HIP_TRY(hipHostMalloc(reinterpret_cast<void **>(&s->h_stage[b]), kStreamChunk, hipHostMallocDefault));
-    ZCRC_HIP_TRY(hipMalloc(reinterpret_cast<void **>(&s->d_stage[b]), kStreamChunk));
-    ZCRC_HIP_TRY(hipEventCreateWithFlags(&s->staged[b], hipEventDisableTiming));
-  }
+  for (int b = 0; b < 2; b++) ZCRC_HIP_TRY(hipEventCreateWithFlags(&s->staged[b], hipEventDisableTiming));
   ZCRC_HIP_TRY(hipMalloc(reinterpret_cast<void **>(&s->d_crc), 2 * sizeof(uint32_t)));
+  return ZCRC_OK;
+}
+
+// (re)start: running CRC = seed
+int stream_reset(zcrc32_stream *s, uint32_t seed) {
   s->seed = seed;
+  s->parts = 0;
   ZCRC_HIP_TRY(hipMemcpyAsync(s->d_crc, &s->seed, 4, hipMemcpyHostToDevice, s->stream));
-  ZCRC_HIP_TRY(hipStreamSynchronize(s->stream));
+  ZCRC_HIP_TRY(hipStreamSynchronize(s->stream));  // s->seed is a host source
   return ZCRC_OK;
 }
 
@@ -621,18 +753,24 @@ int stream_update(zcrc32_stream *s, const uint8_t *data, size_t n) {
   if (rc) return rc;
   while (n > 0) {
     const size_t take = std::min(n, kStreamChunk);
-    const int b = (int)(s->parts & 1u);
-    // pinned slot b is free once its previous H2D finished
+    if (s->nslot < 2) {  // first slot: wait while none is free; second: only if free now
+      rc = SlotPool::get().acquire(s->dev, s->nslot == 0, &s->slot[s->nslot]);
+      if (rc && s->nslot == 0) return rc;
+      if (!rc && s->slot[s->nslot]) s->nslot++;
+    }
+    const int b = (int)(s->parts % (uint64_t)s->nslot);
+    StageSlot &st = *s->slot[b];
+    // pinned area b is free once its previous H2D finished
     ZCRC_HIP_TRY(hipEventSynchronize(s->staged[b]));
-    CopyPool::get().run({CopyJob{s->h_stage[b], data, take}});
-    ZCRC_HIP_TRY(hipMemcpyAsync(s->d_stage[b], s->h_stage[b], take, hipMemcpyHostToDevice, s->stream));
+    CopyPool::get().run({CopyJob{st.h_data, data, take}});
+    ZCRC_HIP_TRY(hipMemcpyAsync(st.d_data, st.h_data, take, hipMemcpyHostToDevice, s->stream));
     ZCRC_HIP_TRY(hipEventRecord(s->staged[b], s->stream));
     // running CRC: seed from d_crc[cur], result to d_crc[cur ^ 1] (zeroed:
-    // split pieces xor into it).  One stream => chunks chain in order.
+    // split pieces xor into it).  One HIP stream => chunks chain in order.
     uint32_t *cur = s->d_crc + (s->parts & 1u), *nxt = s->d_crc + ((s->parts + 1) & 1u);
     ZCRC_HIP_TRY(hipMemsetAsync(nxt, 0, 4, s->stream));
     BatchArgs a{};
-    a.base = s->d_stage[b];
+    a.base = st.d_data;
     a.stride = take;
     a.len = take;
     a.n = 1;
@@ -645,7 +783,6 @@ int stream_update(zcrc32_stream *s, const uint8_t *data, size_t n) {
     data += take;
     n -= take;
   }
-  s->dirty = true;
   return ZCRC_OK;
 }
 
@@ -707,10 +844,19 @@ uint32_t zcrc32(const void *data, size_t n_bytes, uint32_t crc) {
     return host_crc32(data, n_bytes, crc);
   }
   uint32_t r = 0;
-  const int rc = zcrc32_checked(data, n_bytes, crc, &r);
+  const void *ptrs[1] = {data};
+  const size_t lens[1] = {n_bytes};
+  const uint32_t seeds[1] = {crc};
+  // no waiting for staging under the caller's mutex_fhandle: with every slot
+  // of the pool busy, the host CRC answers (counted as a host call)
+  const int rc = batch_host(ptrs, lens, seeds, &r, 1, false);
   if (rc == ZCRC_OK) {
     g_dropin_gpu.fetch_add(1, std::memory_order_relaxed);
     return r;
+  }
+  if (rc == kBusy) {
+    g_dropin_host.fetch_add(1, std::memory_order_relaxed);
+    return host_crc32(data, n_bytes, crc);
   }
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) g_no_device.store(1);
@@ -964,10 +1110,10 @@ int zcrc_inflate_batch(const void *const *src, const size_t *src_len, void *cons
   DeviceCtx *dc = nullptr;
   int rc = device_ctx(&dc);
   if (rc) return rc;
-  rc = host_ctx_init();
+  Lease lease;  // for its HIP stream; the inflate staging is its own
+  rc = lease.take(true, false);
   if (rc) return rc;
-  StageSlot &slot = t_host.slot[0];
-  ZCRC_HIP_TRY(hipStreamSynchronize(slot.stream));
+  StageSlot &slot = *lease.slot[0];
   for (size_t a = 0; a < n;) {
     size_t b = a, bytes = 0;
     while (b < n && (b == a || bytes + src_len[b] + cap[b] <= kInflateGroupBytes)) bytes += src_len[b] + cap[b], b++;
@@ -979,14 +1125,39 @@ int zcrc_inflate_batch(const void *const *src, const size_t *src_len, void *cons
 }
 
 zcrc32_stream *zcrc32_stream_open(uint32_t seed) {
-  zcrc32_stream *s = new (std::nothrow) zcrc32_stream();
-  if (!s) {
-    fail(ZCRC_ERR_HIP, "out of host memory");
+  DeviceCtx *dc = nullptr;
+  if (device_ctx(&dc) != ZCRC_OK) return nullptr;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) {
+    fail(ZCRC_ERR_HIP, "hipGetDevice failed");
     return nullptr;
   }
-  if (stream_init(s, seed) != ZCRC_OK) {
+  zcrc32_stream *s = nullptr;
+  {
+    std::lock_guard<std::mutex> lk(g_streams_mu);
+    for (size_t k = 0; k < g_streams_free.size(); k++)
+      if (g_streams_free[k]->dev == dev) {
+        s = g_streams_free[k];
+        g_streams_free.erase(g_streams_free.begin() + (long)k);
+        break;
+      }
+  }
+  if (!s) {
+    s = new (std::nothrow) zcrc32_stream();
+    if (!s) {
+      fail(ZCRC_ERR_HIP, "out of host memory");
+      return nullptr;
+    }
+    if (stream_create(s) != ZCRC_OK) {
+      const std::string err = t_last_error;
+      stream_destroy(s);
+      t_last_error = err;
+      return nullptr;
+    }
+  }
+  if (stream_reset(s, seed) != ZCRC_OK) {
     const std::string err = t_last_error;
-    stream_free(s);
+    stream_destroy(s);
     t_last_error = err;
     return nullptr;
   }
@@ -1007,11 +1178,30 @@ int zcrc32_stream_final(zcrc32_stream *s, uint32_t *crc) {
   uint32_t v = 0;
   ZCRC_HIP_TRY(hipMemcpyAsync(&v, s->d_crc + (s->parts & 1u), 4, hipMemcpyDeviceToHost, s->stream));
   ZCRC_HIP_TRY(hipStreamSynchronize(s->stream));
+  stream_release_slots(s);  // an idle stream holds no staging
   *crc = v;
   return ZCRC_OK;
 }
 
-void zcrc32_stream_close(zcrc32_stream *s) { stream_free(s); }
+void zcrc32_stream_close(zcrc32_stream *s) {
+  if (!s) return;
+  if (hipStreamSynchronize(s->stream) != hipSuccess) {  // a broken stream is not reused
+    stream_destroy(s);
+    return;
+  }
+  stream_release_slots(s);
+  std::lock_guard<std::mutex> lk(g_streams_mu);
+  if (g_streams_free.size() < kStreamFreeMax) {
+    g_streams_free.push_back(s);
+    return;
+  }
+  stream_destroy(s);
+}
+
+int zcrc_staging_info(uint64_t *pinned_bytes, uint64_t *slots_in_use, uint64_t *slots_peak, uint64_t *slots_budget) {
+  SlotPool::get().info(pinned_bytes, slots_in_use, slots_peak, slots_budget);
+  return ZCRC_OK;
+}
 
 uint32_t zcrc32_combine(uint32_t crc_a, uint32_t crc_b, uint64_t len_b) {
   return gf2_crc_combine(host_xpow(), crc_a, crc_b, len_b);

@@ -10,6 +10,14 @@
 // inflated on the GPU into an HBM arena (zcrc_inflate_batch_device) and the
 // outputs checksummed by the same batched CRC kernel.  The scan is bounds
 // checked against the image; it never reads outside [archive, archive+len).
+//
+// Stored-entry extraction replaces the zip_fread() of a
+// method-0 entry in preloadram_now (src/ZIPsFS_preloadfileram.c:286-288,
+// src/ZIPsFS.c:2014-2019) and the CRC that follows it (:243): the entry's
+// bytes are copied into the caller's buffer and the CRC of the copy -- the
+// bytes fhandle_check_crc32 would check -- is compared with the central
+// directory's, for a whole batch of entries in one copy launch and one CRC
+// launch.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <string.h>
@@ -205,7 +213,148 @@ int verify_deflated_chunk(const uint8_t *d_archive, zcrc_zip_entry *entries, con
   return ZCRC_OK;
 }
 
+// ---------------------------------------------------------- stored entries
+
+// Batched byte-range copy, any alignment.  Range j: len[j] bytes from src[j]
+// to dst[j], cut into tiles of kCopyTileChunks destination-aligned 16-B
+// chunks; workgroup b copies tile b (tile_range[b] = j, tile_first[b] = first
+// chunk).  Interior chunks are one 16-B store whose bytes come from five
+// aligned source dwords funnelled by v_alignbyte; a chunk whose five dwords
+// do not all lie inside the source range (the range's edges -- a buffer load
+// returns zero for a whole dword that straddles the range end) goes
+// bytewise, like the partial destination chunks at both ends.
+constexpr uint32_t kCopyThreads = 256, kCopyTileChunks = 4096;  // 64 KiB per tile
+
+__global__ __launch_bounds__(kCopyThreads) void copy_ranges_kernel(const uint64_t *src, const uint64_t *dst,
+                                                                   const uint64_t *len, const uint32_t *tile_range,
+                                                                   const uint64_t *tile_first) {
+  const uint32_t j = tile_range[blockIdx.x];
+  const uint64_t s = src[j], d = dst[j], n = len[j];
+  const uint64_t d_al = d & ~(uint64_t)15, d_end = d + n;
+  const uint64_t nchunks = (((d_end + 15) & ~(uint64_t)15) - d_al) >> 4;
+  const uint64_t c0 = tile_first[blockIdx.x];
+  const uint64_t c1 = c0 + kCopyTileChunks < nchunks ? c0 + kCopyTileChunks : nchunks;
+  // source window of this tile: [w0, w1), dword aligned at w0
+  const uint64_t first_a = d_al + 16 * c0 > d ? d_al + 16 * c0 : d;
+  const uint64_t w0 = (s + (first_a - d)) & ~(uint64_t)3;
+  const uint64_t w1 = s + ((d_al + 16 * c1 < d_end ? d_al + 16 * c1 : d_end) - d);
+  __amdgpu_buffer_rsrc_t rs =
+      __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void *>(w0), (short)0, (int)(w1 - w0), 0x00020000);
+  for (uint64_t c = c0 + threadIdx.x; c < c1; c += kCopyThreads) {
+    const uint64_t a = d_al + 16 * c;  // destination chunk
+    const uint64_t sa = s + (a - d);   // its source (>= w0 when a >= d)
+    if (a >= d && a + 16 <= d_end && (sa & ~(uint64_t)3) + 20 <= w1) {
+      const uint32_t q = (uint32_t)((sa & ~(uint64_t)3) - w0), sh = (uint32_t)(sa & 3);
+      uint32_t w[5];
+#pragma unroll
+      for (int k = 0; k < 5; k++) w[k] = __builtin_amdgcn_raw_buffer_load_b32(rs, q + 4u * k, 0, 0);
+      uint4 v;
+      v.x = __builtin_amdgcn_alignbyte(w[1], w[0], sh);
+      v.y = __builtin_amdgcn_alignbyte(w[2], w[1], sh);
+      v.z = __builtin_amdgcn_alignbyte(w[3], w[2], sh);
+      v.w = __builtin_amdgcn_alignbyte(w[4], w[3], sh);
+      *reinterpret_cast<uint4 *>(a) = v;
+    } else {
+      for (uint32_t b = 0; b < 16; b++)
+        if (a + b >= d && a + b < d_end)
+          *reinterpret_cast<uint8_t *>(a + b) = *reinterpret_cast<const uint8_t *>(s + (a + b - d));
+    }
+  }
+}
+
+// Entries eligible for extraction: stored, unencrypted, consistent sizes, in
+// range, and a destination of at least comp_size bytes (none needed for an
+// empty entry).
+bool extractable(const zcrc_zip_entry &E, size_t archive_len, const void *dst, size_t cap) {
+  return verifiable(E) && (dst || !E.comp_size) && cap >= E.comp_size && E.data_offset <= archive_len &&
+         E.comp_size <= archive_len - E.data_offset;
+}
+
 }  // namespace
+
+extern "C" int zcrc_zip_extract_stored_device(const void *d_archive, size_t archive_len, zcrc_zip_entry *entries,
+                                              void *const *d_dst, const size_t *cap, size_t n, void *stream) {
+  if (!d_archive || (n && (!entries || !d_dst || !cap))) return zfail("null argument");
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  std::vector<size_t> idx;
+  std::vector<uint64_t> hs, hd, hl;  // src | dst | len
+  std::vector<uint32_t> t_range;
+  std::vector<uint64_t> t_first;
+  for (size_t i = 0; i < n; i++) {
+    zcrc_zip_entry &E = entries[i];
+    if (E.status == ZCRC_ZIP_BAD) continue;
+    E.status = ZCRC_ZIP_UNVERIFIED;
+    E.crc_computed = 0;
+    if (!extractable(E, archive_len, d_dst[i], cap[i])) continue;
+    const uint64_t d = reinterpret_cast<uint64_t>(d_dst[i]);
+    const uint64_t nchunks = E.comp_size ? (((d + E.comp_size + 15) & ~(uint64_t)15) - (d & ~(uint64_t)15)) >> 4 : 0;
+    for (uint64_t c = 0; c < nchunks; c += kCopyTileChunks) {
+      t_range.push_back((uint32_t)idx.size());
+      t_first.push_back(c);
+    }
+    idx.push_back(i);
+    hs.push_back(reinterpret_cast<uint64_t>(d_archive) + E.data_offset);
+    hd.push_back(d);
+    hl.push_back(E.comp_size);
+  }
+  const size_t m = idx.size(), tiles = t_range.size();
+  if (!m) return ZCRC_OK;
+  if (m > 0xFFFFFFFFu || tiles > 0x7FFFFFFFu) return zfail("too many entries for one extraction");
+  void *dv = nullptr;
+  const size_t bytes = 8 * 3 * m + 4 * m + 8 * tiles + 4 * tiles;
+  if (hipMallocAsync(&dv, bytes, st) != hipSuccess) return zfail("hipMallocAsync failed");
+  uint64_t *d_src = static_cast<uint64_t *>(dv), *d_dstp = d_src + m, *d_len = d_dstp + m;
+  uint64_t *d_tfirst = d_len + m;
+  uint32_t *d_crc = reinterpret_cast<uint32_t *>(d_tfirst + tiles), *d_trange = d_crc + m;
+  std::vector<uint32_t> crc(m);
+  int rc = ZCRC_OK;
+  if (hipMemcpyAsync(d_src, hs.data(), 8 * m, hipMemcpyHostToDevice, st) != hipSuccess ||
+      hipMemcpyAsync(d_dstp, hd.data(), 8 * m, hipMemcpyHostToDevice, st) != hipSuccess ||
+      hipMemcpyAsync(d_len, hl.data(), 8 * m, hipMemcpyHostToDevice, st) != hipSuccess ||
+      (tiles && (hipMemcpyAsync(d_tfirst, t_first.data(), 8 * tiles, hipMemcpyHostToDevice, st) != hipSuccess ||
+                 hipMemcpyAsync(d_trange, t_range.data(), 4 * tiles, hipMemcpyHostToDevice, st) != hipSuccess)))
+    rc = zfail("descriptor upload failed");
+  if (!rc && tiles) {
+    hipLaunchKernelGGL(copy_ranges_kernel, dim3((unsigned)tiles), dim3(kCopyThreads), 0, st, d_src, d_dstp, d_len,
+                       d_trange, d_tfirst);
+    if (hipGetLastError() != hipSuccess) rc = zfail("copy launch failed");
+  }
+  // the CRC of the copies, as fhandle_check_crc32 checks the preload buffer
+  if (!rc) rc = zcrc32_batch_device(reinterpret_cast<const void *const *>(d_dstp), d_len, nullptr, d_crc, m, stream);
+  if (!rc && hipMemcpyAsync(crc.data(), d_crc, 4 * m, hipMemcpyDeviceToHost, st) != hipSuccess)
+    rc = zfail("result download failed");
+  (void)hipFreeAsync(dv, st);
+  if (!rc && hipStreamSynchronize(st) != hipSuccess) rc = zfail("stream synchronize failed");
+  if (rc) return rc;
+  finish(entries, idx, crc);
+  return ZCRC_OK;
+}
+
+extern "C" int zcrc_zip_extract_stored_host(const void *archive, size_t archive_len, zcrc_zip_entry *entries,
+                                            void *const *dst, const size_t *cap, size_t n) {
+  if (!archive || (n && (!entries || !dst || !cap))) return zfail("null argument");
+  const uint8_t *a = static_cast<const uint8_t *>(archive);
+  std::vector<size_t> idx;
+  std::vector<const void *> ptrs;
+  std::vector<size_t> lens;
+  for (size_t i = 0; i < n; i++) {
+    zcrc_zip_entry &E = entries[i];
+    if (E.status == ZCRC_ZIP_BAD) continue;
+    E.status = ZCRC_ZIP_UNVERIFIED;
+    E.crc_computed = 0;
+    if (!extractable(E, archive_len, dst[i], cap[i])) continue;
+    if (E.comp_size) memcpy(dst[i], a + E.data_offset, E.comp_size);  // what zip_fread delivers for a stored entry
+    idx.push_back(i);
+    ptrs.push_back(dst[i]);
+    lens.push_back(E.comp_size);
+  }
+  if (idx.empty()) return ZCRC_OK;
+  std::vector<uint32_t> crc(idx.size());
+  const int rc = zcrc32_batch(ptrs.data(), lens.data(), nullptr, crc.data(), idx.size(), 0);
+  if (rc) return rc;
+  finish(entries, idx, crc);
+  return ZCRC_OK;
+}
 
 extern "C" int zcrc_zip_verify_device(const void *d_archive, size_t archive_len, zcrc_zip_entry *entries, size_t n,
                                       void *stream) {

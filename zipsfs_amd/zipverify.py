@@ -47,6 +47,12 @@ def _setup():
     l.zcrc_zip_verify_device.restype = ctypes.c_int
     l.zcrc_zip_verify_device.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_size_t,
                                          ctypes.c_void_p]
+    for f in (l.zcrc_zip_extract_stored_host, l.zcrc_zip_extract_stored_device):
+        f.restype = ctypes.c_int
+    l.zcrc_zip_extract_stored_host.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_void_p,
+                                               ctypes.c_void_p, ctypes.c_size_t]
+    l.zcrc_zip_extract_stored_device.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p,
+                                                 ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p]
     _SIGS = True
     return l
 
@@ -124,3 +130,47 @@ def verify(archive, device: bool = True) -> List[ZipEntryCheck]:
     else:
         check(l.zcrc_zip_verify_host(a.ctypes.data, a.size, arr, len(entries)), "zcrc_zip_verify_host")
     return [_to_check(a, e) for e in arr[: len(entries)]]
+
+
+def extract_stored(archive, device: bool = True):
+    """Stored-entry extraction: the bytes zip_fread()
+    would deliver for every stored entry (src/ZIPsFS_preloadfileram.c:286-288)
+    plus fhandle_check_crc32's verdict on them (:237-250), in one call.
+
+    Returns a list of (ZipEntryCheck, data) in central-directory order; data
+    is a uint8 torch tensor in HBM (device=True: zcrc_zip_extract_stored_device,
+    one copy launch + one CRC launch) or a numpy array (device=False:
+    zcrc_zip_extract_stored_host, host memcpy + one zcrc32_batch), or None for
+    entries that are not extracted (not stored, encrypted, out of range:
+    status ZIP_UNVERIFIED or ZIP_BAD)."""
+    a = _as_array(archive)
+    l = _setup()
+    entries = _scan_raw(a)
+    n = len(entries)
+    arr = (_Entry * max(n, 1))(*entries)
+    want = [e.status != ZIP_BAD and e.method == 0 and not (e.flags & 1) and e.comp_size == e.uncomp_size
+            and e.data_offset + e.comp_size <= a.size for e in entries]
+    cap = np.array([e.comp_size if w else 0 for e, w in zip(entries, want)], dtype=np.uint64)
+    bufs = [None] * n
+    if device:
+        import torch
+        from .crc32 import _stream_ptr
+        d = torch.from_numpy(a if a.flags.writeable else a.copy()).to("cuda")
+        for i in range(n):
+            if want[i]:
+                bufs[i] = torch.empty(int(cap[i]), dtype=torch.uint8, device="cuda")
+        ptrs = np.array([b.data_ptr() if b is not None else 0 for b in bufs], dtype=np.uint64)
+        check(l.zcrc_zip_extract_stored_device(d.data_ptr(), a.size, arr, ptrs.ctypes.data, cap.ctypes.data, n,
+                                               _stream_ptr(None)), "zcrc_zip_extract_stored_device")
+    else:
+        for i in range(n):
+            if want[i]:
+                bufs[i] = np.empty(int(cap[i]), dtype=np.uint8)
+        ptrs = np.array([b.ctypes.data if b is not None else 0 for b in bufs], dtype=np.uint64)
+        check(l.zcrc_zip_extract_stored_host(a.ctypes.data, a.size, arr, ptrs.ctypes.data, cap.ctypes.data, n),
+              "zcrc_zip_extract_stored_host")
+    out = []
+    for i, e in enumerate(arr[:n]):
+        c = _to_check(a, e)
+        out.append((c, bufs[i] if c.status in (ZIP_OK, ZIP_MISMATCH) else None))
+    return out
