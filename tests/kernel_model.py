@@ -145,6 +145,45 @@ class Batch:
         return b0 + q
 
 
+def device_lower_bound(prefix, n: int, t: int):
+    """BatchView::lower_bound_ex (zcrc_batch_kernel.h): the wave-wide 64-ary
+    search whose last level loads prefix(lo-1 .. lo+62) -> (i, prefix(i),
+    prefix(i-1))."""
+    lo, hi = 0, n
+    while hi - lo > 62:
+        step = (hi - lo + 63) // 64
+        f = next(l for l in range(64) if int(prefix[min(lo + (l + 1) * step, hi)]) >= t)
+        nhi = min(lo + (f + 1) * step, hi)
+        lo, hi = (lo if f == 0 else lo + f * step + 1), nhi
+    v = [int(prefix[lo + l - 1]) if (lo + l >= 1 and lo + l - 1 <= hi) else None for l in range(64)]
+    f = next(l for l in range(1, 64) if v[l] is not None and v[l] >= t)
+    r = lo - 1 + f
+    return r, v[f], (v[f - 1] if r else 0)
+
+
+def device_snap(batch: "Batch", t: int):
+    """BatchView::snap_at on the device search: (S, lb = lower_bound(S),
+    first = the first buffer overlapping [S, ...))."""
+    tot, n = batch.total, batch.n
+    if t == 0:
+        return 0, 0, 0
+    if t >= tot:
+        x = device_lower_bound(batch.prefix, n, tot)[0]
+        return tot, x, x
+    i, pi, pim1 = device_lower_bound(batch.prefix, n, t)
+    if pi == t:
+        return t, i, i
+    b0 = pim1
+    m, p = pi - b0, t - b0
+    if m < K_SPLIT_MIN:
+        return pi, i, i
+    q = m - K_SPLIT_GRAIN * ((m - p) // K_SPLIT_GRAIN)
+    if q < K_MIN_PIECE:
+        x = device_lower_bound(batch.prefix, n, b0)[0]
+        return b0, x, x
+    return b0 + q, i, (i - 1 if q < m else i)
+
+
 def wave_ranges(batch: Batch, num_cus: int, dyn_shift: int = K_DYN_SHIFT, unit: int = K_DYN_UNIT):
     """Every (s0, s1, last) range the kernel processes: W static wave ranges
     over the first Ts bytes, then the dynamic units of `unit` nominal bytes

@@ -118,3 +118,38 @@ def test_model_dynamic_tail_matches_oracle(dyn_shift, unit):
     got = km.run_batch(b, num_cus=1, dyn_shift=dyn_shift, unit=unit)
     exp = [o.cg_crc32(mem[a:a + L], s) for a, L, s in zip(addrs, lens, seeds)]
     assert list(got) == exp
+
+
+@pytest.mark.parametrize("shape", ["ragged_with_empties", "config4", "grid_edges"])
+def test_device_search_and_first_buffer(shape):
+    """The device's range search (BatchView::lower_bound_ex + snap_at) returns
+    the snapped boundary, lower_bound of it and the first buffer overlapping
+    it -- the values the piece walk starts from without another read.  Checked
+    against the definitions (np.searchsorted, Batch.snap, the walk's own
+    decrement).  grid_edges aims targets where the end-relative split grid
+    puts the snap exactly on a buffer's end (q == n: its end, not inside it;
+    a round-2 kernel bug complemented such buffers)."""
+    M = km
+    rnd = random.Random({"ragged_with_empties": 1, "config4": 2, "grid_edges": 3}[shape])
+    if shape == "config4":
+        lens = [M.config4_len(i) for i in range(20000)] if hasattr(M, "config4_len") else \
+            [int(1024 / (1 - rnd.random() * 127 / 128) ** 2) for _ in range(20000)]
+    elif shape == "grid_edges":
+        lens = [rnd.choice([3 * (64 << 10) + rnd.randint(1, 5000), 1 << 20, 200_000]) for _ in range(3000)]
+    else:
+        lens = [rnd.choice([0, 0, 7, 4096, 130_000, 1 << 20, rnd.randint(0, 3 << 20)]) for _ in range(5000)]
+    b = M.Batch(np.zeros(1, dtype=np.uint8), [0] * len(lens), lens)
+    targets = [rnd.randrange(0, b.total + 1) for _ in range(600)] + [0, b.total, b.total - 1]
+    if shape == "grid_edges":  # just past the last full grid cell of a buffer
+        for i in rnd.sample(range(len(lens)), 300):
+            b0, b1 = int(b.prefix[i]), int(b.prefix[i + 1])
+            targets += [b1 - (64 << 10) + 1, b1 - 1, b0 + 1, b0 + (b1 - b0) % (64 << 10) + 1]
+    for t in targets:
+        t = min(max(t, 0), b.total)
+        S, lb, first = M.device_snap(b, t)
+        assert S == b.snap(t), t
+        assert lb == b.lower_bound(S), t
+        f = lb
+        if 0 < f <= b.n and int(b.prefix[f]) > S:
+            f -= 1
+        assert first == f, (t, S, lb, first)

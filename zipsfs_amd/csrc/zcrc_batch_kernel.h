@@ -41,6 +41,12 @@ namespace zcrc {
 
 // ----------------------------------------------------------------- helpers
 
+// kAux: cache-policy bits of the payload loads.  The product streams with
+// nt (2): every payload byte is read once, and non-temporal loads lift the
+// sustained HBM read rate by ~12% over the default policy on gfx950
+// (tools/hbm_probe, tools/crc_variants; DESIGN.md section 4).
+constexpr int kLoadNt = 2;
+
 __device__ __forceinline__ uint32_t lds_u32(const uint32_t *lds, uint32_t byte_addr) {
   return *reinterpret_cast<const uint32_t *>(reinterpret_cast<const char *>(lds) + byte_addr);
 }
@@ -126,6 +132,12 @@ __device__ __forceinline__ uint64_t uni64(uint64_t v) {
   return (uint64_t)uni32((uint32_t)v) | ((uint64_t)uni32((uint32_t)(v >> 32)) << 32);
 }
 
+// lane k's value of a 64-bit register (k wave-uniform)
+__device__ __forceinline__ uint64_t rdlane64(uint64_t v, uint32_t k) {
+  return (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, (int)k) |
+         ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), (int)k) << 32);
+}
+
 __device__ __forceinline__ uint32_t hash32(uint32_t x) {
   x ^= x >> 16;
   x *= 0x7FEB352Du;
@@ -153,17 +165,27 @@ struct BatchView {
   __device__ uint32_t seed(uint64_t i) const { return a.seeds ? a.seeds[i] : 0u; }
   __device__ uint64_t total() const { return tot_; }
 
-  // First i in [0, n] with prefix(i) >= t (prefix(n) = total >= t).  Wave-wide
-  // 64-ary search; every lane returns the same value.
-  __device__ uint64_t lower_bound(uint64_t t) const {
+  // First i in [0, n] with prefix(i) >= t (prefix(n) = total >= t), plus
+  // p_i = prefix(i) and p_im1 = prefix(i-1) (0 for i = 0).  Wave-wide 64-ary
+  // search; its last level loads prefix(lo-1 .. lo+62), so the two values the
+  // snap needs come from lanes of that level instead of another dependent
+  // round trip (each costs ~1-2 us at kernel start: tools/c2_probe timeline).
+  // Every lane returns the same values.  (An interpolation window loaded with
+  // the first level -- one round trip for equal-size buffers -- measured
+  // +4-5% on 4 and 16 KiB batches and nothing on config 2, whose search waits
+  // behind the table loads anyway: dropped.)
+  __device__ uint64_t lower_bound_ex(uint64_t t, uint64_t &p_i, uint64_t &p_im1) const {
     if (kStrided) {
-      if (a.len == 0) return t == 0 ? 0 : a.n;
-      const uint64_t i = (t + a.len - 1) / a.len;
-      return i < a.n ? i : a.n;
+      uint64_t i;
+      if (a.len == 0) i = t == 0 ? 0 : a.n;
+      else i = (t + a.len - 1) / a.len < a.n ? (t + a.len - 1) / a.len : a.n;
+      p_i = i * a.len;
+      p_im1 = i ? (i - 1) * a.len : 0;
+      return i;
     }
     const uint32_t lane = threadIdx.x & 63u;
     uint64_t lo = 0, hi = a.n;
-    while (hi - lo > 63) {
+    while (hi - lo > 62) {
       const uint64_t step = (hi - lo + 63) / 64;
       uint64_t idx = lo + (uint64_t)(lane + 1) * step;
       if (idx > hi) idx = hi;
@@ -174,62 +196,71 @@ struct BatchView {
       lo = uni64(nlo);
       hi = uni64(nhi);
     }
-    const uint64_t idx = lo + lane;
-    const bool ok = idx <= hi && pre(idx <= hi ? idx : hi) >= t;
-    const uint64_t m = __ballot(ok);
-    return uni64(lo + (uint64_t)__builtin_ctzll(m));
+    // lane j holds prefix(lo - 1 + j); lanes 1..63 cover lo .. lo + 62 >= hi
+    const uint64_t idx = lo + lane - 1;
+    const bool in = lo + lane >= 1 && idx <= hi;
+    const uint64_t v = pre(in ? idx : hi);
+    const uint64_t m = __ballot(in && lane >= 1 && v >= t);
+    const uint32_t f = (uint32_t)__builtin_ctzll(m);  // >= 1
+    const uint64_t r = uni64(lo - 1 + f);
+    p_i = rdlane64(v, f);
+    p_im1 = r ? rdlane64(v, f - 1) : 0;
+    return r;
+  }
+  __device__ uint64_t lower_bound(uint64_t t) const {
+    uint64_t p, q;
+    return lower_bound_ex(t, p, q);
   }
 
   // Snap a nominal wave boundary t so that buffers shorter than kSplitMin are
   // never split and split points sit at end-relative multiples of kSplitGrain.
   // Monotone non-decreasing in t, so snapped ranges stay ordered.
-  __device__ uint64_t snap(uint64_t t) const {
-    uint64_t lb;
-    return snap_at(t, lower_bound(t), lb);
-  }
-
-  // snap() given i = lower_bound(t); also returns lb = lower_bound(result),
-  // which process_range needs, without a second search in the common cases.
-  __device__ uint64_t snap_at(uint64_t t, uint64_t i, uint64_t &lb) const {
+  // Given i = lower_bound(t), pi = prefix(i), pim1 = prefix(i-1); returns the
+  // snapped S and lb = lower_bound(S), first = the first buffer overlapping
+  // [S, ...) (lb - 1 when S is strictly inside buffer lb - 1, else lb) --
+  // process_range's piece walk starts there, without reading prefix(lb).
+  __device__ uint64_t snap_at(uint64_t t, uint64_t i, uint64_t pi, uint64_t pim1, uint64_t &lb,
+                              uint64_t &first) const {
     const uint64_t tot = total();
-    if (t == 0) return lb = 0, 0;
-    if (t >= tot) return lb = lower_bound(tot), tot;
-    const uint64_t pi = prefix(i);
-    lb = i;
+    if (t == 0) return lb = first = 0, 0;
+    if (t >= tot) return lb = first = lower_bound(tot), tot;
+    lb = first = i;
     if (pi == t) return t;
-    const uint64_t b0 = prefix(i - 1);
+    const uint64_t b0 = pim1;
     const uint64_t n = pi - b0, p = t - b0;
     if (n < kSplitMin) return pi;  // prefix(i-1) < pi: lower_bound(pi) = i
     const uint64_t q = n - kSplitGrain * ((n - p) / kSplitGrain);
-    if (q < kMinPiece) return lb = lower_bound(b0), b0;  // empty buffers may precede i-1
-    return b0 + q;  // strictly inside buffer i-1
+    if (q < kMinPiece) return lb = first = lower_bound(b0), b0;  // empty buffers may precede i-1
+    if (q < n) first = i - 1;  // strictly inside buffer i-1 (q == n: its end, = pi)
+    return b0 + q;
   }
 
-  // lower_bound of two targets in one 64-ary pass (two independent loads per
-  // level instead of two dependent searches).
-  __device__ void lower_bound2(uint64_t t0, uint64_t t1, uint64_t &r0, uint64_t &r1) const {
+  // lower_bound_ex of two targets in one 64-ary pass (two independent loads
+  // per level instead of two dependent searches).
+  __device__ void lower_bound2(uint64_t t0, uint64_t t1, uint64_t &r0, uint64_t &r1, uint64_t &p0, uint64_t &q0,
+                               uint64_t &p1, uint64_t &q1) const {
     if (kStrided) {
-      r0 = lower_bound(t0);
-      r1 = lower_bound(t1);
+      r0 = lower_bound_ex(t0, p0, q0);
+      r1 = lower_bound_ex(t1, p1, q1);
       return;
     }
     const uint32_t lane = threadIdx.x & 63u;
     uint64_t lo0 = 0, hi0 = a.n, lo1 = 0, hi1 = a.n;
-    while (hi0 - lo0 > 63 || hi1 - lo1 > 63) {
+    while (hi0 - lo0 > 62 || hi1 - lo1 > 62) {
       const uint64_t st0 = (hi0 - lo0 + 63) / 64, st1 = (hi1 - lo1 + 63) / 64;
       uint64_t x0 = lo0 + (uint64_t)(lane + 1) * st0, x1 = lo1 + (uint64_t)(lane + 1) * st1;
       if (x0 > hi0) x0 = hi0;
       if (x1 > hi1) x1 = hi1;
       const uint64_t v0 = pre(x0), v1 = pre(x1);
       const uint64_t m0 = __ballot(v0 >= t0), m1 = __ballot(v1 >= t1);
-      if (hi0 - lo0 > 63) {
+      if (hi0 - lo0 > 62) {
         const uint32_t f = (uint32_t)__builtin_ctzll(m0);
         const uint64_t nh = lo0 + (uint64_t)(f + 1) * st0;
         const uint64_t nl = f == 0 ? lo0 : lo0 + (uint64_t)f * st0 + 1;
         hi0 = uni64(nh < hi0 ? nh : hi0);
         lo0 = uni64(nl);
       }
-      if (hi1 - lo1 > 63) {
+      if (hi1 - lo1 > 62) {
         const uint32_t f = (uint32_t)__builtin_ctzll(m1);
         const uint64_t nh = lo1 + (uint64_t)(f + 1) * st1;
         const uint64_t nl = f == 0 ? lo1 : lo1 + (uint64_t)f * st1 + 1;
@@ -237,30 +268,36 @@ struct BatchView {
         lo1 = uni64(nl);
       }
     }
-    const uint64_t x0 = lo0 + lane, x1 = lo1 + lane;
-    const uint64_t v0 = pre(x0 <= hi0 ? x0 : hi0), v1 = pre(x1 <= hi1 ? x1 : hi1);
-    const uint64_t m0 = __ballot(x0 <= hi0 && v0 >= t0), m1 = __ballot(x1 <= hi1 && v1 >= t1);
-    r0 = uni64(lo0 + (uint64_t)__builtin_ctzll(m0));
-    r1 = uni64(lo1 + (uint64_t)__builtin_ctzll(m1));
+    const uint64_t x0 = lo0 + lane - 1, x1 = lo1 + lane - 1;
+    const bool in0 = lo0 + lane >= 1 && x0 <= hi0, in1 = lo1 + lane >= 1 && x1 <= hi1;
+    const uint64_t v0 = pre(in0 ? x0 : hi0), v1 = pre(in1 ? x1 : hi1);
+    const uint64_t m0 = __ballot(in0 && lane >= 1 && v0 >= t0), m1 = __ballot(in1 && lane >= 1 && v1 >= t1);
+    const uint32_t f0 = (uint32_t)__builtin_ctzll(m0), f1 = (uint32_t)__builtin_ctzll(m1);
+    r0 = uni64(lo0 - 1 + f0);
+    r1 = uni64(lo1 - 1 + f1);
+    p0 = rdlane64(v0, f0);
+    q0 = r0 ? rdlane64(v0, f0 - 1) : 0;
+    p1 = rdlane64(v1, f1);
+    q1 = r1 ? rdlane64(v1, f1 - 1) : 0;
   }
 
-  // Snapped range [S0, S1) for nominal [t0, t1) plus the lower bounds of the
-  // snapped ends (process_range's piece walk), with one dual search.
-  // `last`: S1 = total (the caller's final range).
-  __device__ void range(uint64_t t0, uint64_t t1, bool last, uint64_t &S0, uint64_t &S1, uint64_t &lb0,
+  // Snapped range [S0, S1) for nominal [t0, t1), the first buffer overlapping
+  // it (first0) and lb1 = lower_bound(S1) -- process_range's piece walk --
+  // with one dual search.  `last`: S1 = total (the caller's final range).
+  __device__ void range(uint64_t t0, uint64_t t1, bool last, uint64_t &S0, uint64_t &S1, uint64_t &first0,
                         uint64_t &lb1) const {
     const uint64_t tot = total();
     const uint64_t c0 = t0 < tot ? t0 : tot, c1 = t1 < tot ? t1 : tot;
-    uint64_t i0, i1;
-    lower_bound2(c0, c1, i0, i1);
-    S0 = uni64(snap_at(c0, i0, lb0));
+    uint64_t i0, i1, p0, q0, p1, q1, lb0, first1;
+    lower_bound2(c0, c1, i0, i1, p0, q0, p1, q1);
+    S0 = uni64(snap_at(c0, i0, p0, q0, lb0, first0));
     if (last) {
       S1 = tot;
       lb1 = a.n;
     } else {
-      S1 = uni64(snap_at(c1, i1, lb1));
+      S1 = uni64(snap_at(c1, i1, p1, q1, lb1, first1));
     }
-    lb0 = uni64(lb0);
+    first0 = uni64(first0);
     lb1 = uni64(lb1);
   }
 };
@@ -335,28 +372,53 @@ __device__ void split_accumulate(const BatchArgs &a, uint64_t i, uint64_t n, uin
 // Process every piece of the byte range [S0, S1) of the concatenated batch
 // (S0, S1 snapped; `last_range` also takes the trailing empty buffers).
 // Returns the number of pieces.  Wave-uniform; no barriers.
+// Descriptors of up to 64 pieces of a range walk (kWin), lane k = piece k of
+// the window that starts at walk position k0.
+struct PieceWindow {
+  uint64_t i, b0, b1, p;
+  uint32_t s;
+};
+
+template <bool kStrided>
+__device__ __forceinline__ void load_window(const BatchView<kStrided> &bv, uint64_t i_first, uint64_t npieces,
+                                            uint64_t rot, uint64_t k0, uint32_t lane, PieceWindow &w) {
+  uint64_t x = k0 + lane + rot;  // rotated position of this lane's piece
+  if (x >= npieces) x -= npieces;
+  w.i = i_first + (k0 + lane < npieces ? x : 0);
+  w.b0 = bv.prefix(w.i);
+  w.b1 = bv.prefix(w.i + 1);
+  w.p = reinterpret_cast<uint64_t>(bv.ptr(w.i));
+  w.s = bv.seed(w.i);
+}
+
+// Per-wave rotated visiting order.  Pieces are independent, and the rotation
+// de-phases waves whose ranges start on large power-of-two boundaries
+// (uniform batches), which otherwise walk the HBM channel interleave in
+// lockstep ("partition camping", tools/hbm_probe: up to -13%).
+template <bool kRotate>
+__device__ __forceinline__ uint64_t walk_rotation(uint32_t salt, uint64_t npieces) {
+  return (kRotate && npieces > 1) ? (uint64_t)(hash32(salt) % (uint32_t)npieces) : 0;
+}
+
+// kWin: piece descriptors are fetched 64 pieces at a time with one vector
+// load per field (lane k: the window's piece k) and read back with
+// v_readlane, instead of a dependent scalar round trip per piece.
 template <bool kStrided, uint32_t kD, int kAblate, bool kRotate, int kPrio = 0, int kAux = 0, bool kStamp = false,
-          bool kFused = false>
+          bool kFused = false, bool kWin = false>
 __device__ __forceinline__ uint64_t process_range(const BatchArgs &args, const BatchView<kStrided> &bv,
                                                   const uint32_t *s_lds, const TableBlob *tab, uint64_t S0,
                                                   uint64_t S1, bool last_wave, uint32_t salt, uint32_t lane,
-                                                  bool band, uint64_t lb0, uint64_t lb1, uint64_t *t_tail = nullptr) {
+                                                  bool band, uint64_t first0, uint64_t lb1, uint64_t *t_tail = nullptr) {
   // lane constants for the braided lookups
   const uint32_t lo0 = (lane & 31u) * 4u;
   const uint32_t o0 = lo0, o1 = lo0 + 128u, o2 = lo0 + 65536u, o3 = lo0 + 65536u + 128u;
 
   // Buffers [i_first, i_end) overlap this wave's range [S0, S1).
-  // lb0 = lower_bound(S0), lb1 = lower_bound(S1) (BatchView::range)
-  uint64_t i_first = lb0;
-  if (i_first > 0 && i_first <= args.n && bv.prefix(i_first) > S0) i_first--;  // S0 inside buffer i-1
-  i_first = uni64(i_first);
+  // first0: the first buffer overlapping it, lb1 = lower_bound(S1) (BatchView::range)
+  const uint64_t i_first = uni64(first0);
   const uint64_t i_end = last_wave ? args.n : lb1;
   const uint64_t npieces = i_end > i_first ? i_end - i_first : 0;
-  // Visit the pieces in a per-wave rotated order.  Pieces are independent,
-  // and the rotation de-phases waves whose ranges start on large power-of-two
-  // boundaries (uniform batches), which otherwise walk the HBM channel
-  // interleave in lockstep ("partition camping", tools/hbm_probe: up to -13%).
-  const uint64_t rot = (kRotate && npieces > 1) ? (uint64_t)(hash32(salt) % (uint32_t)npieces) : 0;
+  const uint64_t rot = walk_rotation<kRotate>(salt, npieces);
 
   // kPrio: least-progress-first issue priority.  Waves of a CU are otherwise
   // served oldest-first, so with equal byte ranges slot 0-3 finish at ~50% of
@@ -365,11 +427,21 @@ __device__ __forceinline__ uint64_t process_range(const BatchArgs &args, const B
   uint64_t done = 0;
   if (kPrio && band) __builtin_amdgcn_s_setprio(3);
 
+  PieceWindow win{0, 0, 0, 0, 0};  // kWin: the current window
   for (uint64_t k = 0; k < npieces; k++) {
-    uint64_t i = i_first + k + rot;
-    if (i >= i_end) i -= npieces;
-    i = uni64(i);
-    const uint64_t b0 = uni64(bv.prefix(i)), b1 = uni64(bv.prefix(i + 1));
+    uint64_t i, b0, b1;
+    if (kWin && !kStrided) {
+      const uint32_t kk = (uint32_t)(k & 63u);
+      if (kk == 0) load_window(bv, i_first, npieces, rot, k, lane, win);
+      i = rdlane64(win.i, kk);
+      b0 = rdlane64(win.b0, kk);
+      b1 = rdlane64(win.b1, kk);
+    } else {
+      i = i_first + k + rot;
+      if (i >= i_end) i -= npieces;
+      i = uni64(i);
+      b0 = uni64(bv.prefix(i)), b1 = uni64(bv.prefix(i + 1));
+    }
     const uint64_t n = b1 - b0;
     const uint64_t rel_lo = (S0 > b0 ? S0 - b0 : 0);
     const uint64_t rel_hi = (b1 < S1 || last_wave) ? n : S1 - b0;
@@ -381,8 +453,15 @@ __device__ __forceinline__ uint64_t process_range(const BatchArgs &args, const B
       else if (lvl >= 3) __builtin_amdgcn_s_setprio(0);
       done += rel_hi - rel_lo;
     }
-    const uint32_t seed = uni32(bv.seed(i));
-    const uint8_t *bptr = reinterpret_cast<const uint8_t *>(uni64(reinterpret_cast<uint64_t>(bv.ptr(i))));
+    uint32_t seed;
+    const uint8_t *bptr;
+    if (kWin && !kStrided) {
+      seed = (uint32_t)__builtin_amdgcn_readlane((int)win.s, (int)(k & 63u));
+      bptr = reinterpret_cast<const uint8_t *>(rdlane64(win.p, (uint32_t)(k & 63u)));
+    } else {
+      seed = uni32(bv.seed(i));
+      bptr = reinterpret_cast<const uint8_t *>(uni64(reinterpret_cast<uint64_t>(bv.ptr(i))));
+    }
 
     if (n < 4) {  // tiny buffer: bytewise with the standard table (never split)
       uint32_t r = ~seed;
@@ -512,13 +591,8 @@ __device__ __forceinline__ uint64_t process_range(const BatchArgs &args, const B
   return npieces;
 }
 
-// kAux: cache-policy bits of the payload loads.  The product streams with
-// nt (2): every payload byte is read once, and non-temporal loads lift the
-// sustained HBM read rate by ~12% over the default policy on gfx950
-// (tools/hbm_probe, tools/crc_variants; DESIGN.md section 4).
-constexpr int kLoadNt = 2;
 template <bool kStrided, uint32_t kD = kDepth, int kAblate = 0, bool kRotate = true, bool kStamp = false,
-          int kPrio = 1, int kAux = kLoadNt, bool kFused = false>
+          int kPrio = 1, int kAux = kLoadNt, bool kFused = false, bool kWin = kWindowed>
 __global__ __launch_bounds__(kThreads) void crc32_batch_kernel(BatchArgs args) {
   __shared__ __attribute__((aligned(16))) uint32_t s_lds[kLdsBytes / 4];
   const TableBlob *tab = args.tab;
@@ -609,16 +683,15 @@ __global__ __launch_bounds__(kThreads) void crc32_batch_kernel(BatchArgs args) {
   // nominal boundary of wave k: floor(k * Ts / W), without 128-bit math
   const uint64_t q_tot = Ts / W, r_tot = Ts % W;
   bool last = (w + 1 == W) && !Td;
-  uint64_t S0 = 0, S1 = 0, lb0 = 0, lb1 = 0;
+  uint64_t S0 = 0, S1 = 0, f0 = 0, lb1 = 0;  // f0: first buffer overlapping [S0, S1)
   if (w < W)
     bv.range(q_tot * w + (r_tot * w) / W, (w + 1 == W) ? Ts : q_tot * (w + 1) + (r_tot * (w + 1)) / W, last, S0,
-             S1, lb0, lb1);
+             S1, f0, lb1);
   const uint64_t t_search = kStamp ? __builtin_amdgcn_s_memrealtime() : 0;
   if (kFused) {
     __syncthreads();  // every wave's search is done with the LDS prefix
     bv.lpre = nullptr;
   }
-
   // ---- LDS: braided table x32 replicas + 8 combine tables ---------------
   {
     uint4 *dst = reinterpret_cast<uint4 *>(s_lds);
@@ -659,8 +732,8 @@ __global__ __launch_bounds__(kThreads) void crc32_batch_kernel(BatchArgs args) {
       have_next = true;
     }
     if (S0 < S1 || last)
-      npieces += process_range<kStrided, kD, kAblate, kRotate, kPrio, kAux, kStamp, kFused>(
-          args, bv, s_lds, tab, S0, S1, last, salt, lane, band, lb0, lb1, &t_tail);
+      npieces += process_range<kStrided, kD, kAblate, kRotate, kPrio, kAux, kStamp, kFused, kWin>(
+          args, bv, s_lds, tab, S0, S1, last, salt, lane, band, f0, lb1, &t_tail);
     if (!units) break;
     if (first_claim) {
       nx = (uint32_t)w;  // units >= W whenever the dynamic part is on
@@ -682,7 +755,7 @@ __global__ __launch_bounds__(kThreads) void crc32_batch_kernel(BatchArgs args) {
       ts0 = __builtin_amdgcn_s_memrealtime();
       t_unit_drain += ts0 - tw;
     }
-    bv.range(t0, t0 + unit, last, S0, S1, lb0, lb1);
+    bv.range(t0, t0 + unit, last, S0, S1, f0, lb1);
     if (kStamp) t_unit_search += __builtin_amdgcn_s_memrealtime() - ts0;
     salt = u ^ 0x9E3779B9u;
     if (kPrio && band) __builtin_amdgcn_s_setprio(0);

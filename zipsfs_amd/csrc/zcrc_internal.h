@@ -20,6 +20,7 @@ constexpr size_t kCtrBytes = 256;              // work counter, own cache lines
 constexpr uint32_t kLdsBytes = 163840;         // all 160 KiB of the CU's LDS
 constexpr uint32_t kLdsCombDword = 32768;      // combine tables start at 128 KiB
 constexpr uint32_t kPlanPerThread = 8;
+constexpr bool kWindowed = true;       // piece descriptors fetched 64 at a time
 constexpr uint64_t kFusedMaxN = 8192;  // one-launch small batches: the kernel scans the lengths itself
 constexpr uint64_t kPlanTile = 1024 * kPlanPerThread;
 // one launch covers at most this many bytes (keeps every piece < 2 GiB)
