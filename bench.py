@@ -407,8 +407,11 @@ def main() -> None:
     if traffic is None and os.path.exists(pmc_path):
         # PMC traffic per config, collected by tools/collect_profiles.sh for
         # the kernel this build launches (same workload bytes)
+        # only for the same workload and the same kernel sources: a traffic
+        # figure measured for another kernel build is not reported
         pm = json.load(open(pmc_path)).get(str(args.config))
-        if pm and pm.get("bytes_per_gpu_per_step") == wl.bytes_local:
+        if (pm and pm.get("bytes_per_gpu_per_step") == wl.bytes_local
+                and pm.get("kernel_source_hash") == z.kernel_source_hash()):
             traffic = pm["traffic_bytes_per_launch"]
             traffic_src = pm["source"]
     cpu = None
@@ -449,7 +452,8 @@ def main() -> None:
                 "traffic_unit": "bytes per launch (HBM read+write, PMC)",
                 "traffic_source": traffic_src,
                 "algorithmic_bytes_per_launch": wl.bytes_local,
-                "kernel": "zcrc::crc32_batch_kernel<false, 4u, 0, true, false, 1, 2>",
+                "kernel": z.kernel_name(),
+                "kernel_source_hash": z.kernel_source_hash(),
                 "avg_kernel_ms": round(avg_kernel_ms, 4),
                 "launches_timed": prof.launches,
             },

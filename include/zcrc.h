@@ -219,6 +219,8 @@ int zcrc_fill_synthetic(const uint64_t *d_ptrs, const uint64_t *d_lens, size_t n
 int zcrc_staging_info(uint64_t *pinned_bytes, uint64_t *slots_in_use, uint64_t *slots_peak, uint64_t *slots_budget);
 const char *zcrc_last_error(void);
 const char *zcrc_version(void);
+/* The batched CRC kernel the device entry points launch, as rocprofv3 names it. */
+const char *zcrc_kernel_name(void);
 int zcrc_device_info(int *num_cus, int *arch_major, int *arch_minor);
 /* When enabled, each device launch of the main CRC kernel is bracketed by
  * HIP events recorded on the launch stream; zcrc_profile_read returns the

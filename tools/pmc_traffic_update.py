@@ -9,6 +9,9 @@ import json
 import os
 import sys
 
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from zipsfs_amd.crc32 import kernel_source_hash  # noqa: E402
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 BYTES = {2: 4096 * 65536, 3: 65536 << 20, 4: 13123505587, 5: 131072 << 20}
 
@@ -27,6 +30,7 @@ def main():
         "write_bytes": s["hbm_write_bytes_per_launch"],
         "kernel": kern[0].replace("void ", "").split("(")[0] if kern else "crc32_batch_kernel",
         "rocprof_avg_kernel_ms": s["kernel_trace"]["avg_ms"],
+        "kernel_source_hash": kernel_source_hash(),
         "source": f"{rel}: tools/collect_profiles.sh (rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate "
                   f"passes of python3 bench.py --config {cfg} --steps 5 --warmup 1 --no-cpu-baseline); "
                   f"{s['correction']}",

@@ -382,3 +382,20 @@ def staging_info() -> dict:
 
 def version() -> str:
     return lib().zcrc_version().decode()
+
+
+def kernel_name() -> str:
+    """The batched CRC kernel the device entry points launch (rocprofv3 name)."""
+    return lib().zcrc_kernel_name().decode()
+
+
+def kernel_source_hash() -> str:
+    """sha256 (16 hex) of the kernel's sources: PMC traffic recorded for one
+    kernel build is reported only for the same sources (bench.py)."""
+    import hashlib
+    import os
+    h = hashlib.sha256()
+    d = os.path.join(os.path.dirname(os.path.abspath(__file__)), "csrc")
+    for f in ("zcrc_batch_kernel.h", "zcrc_internal.h", "zcrc_gf2.h", "zcrc_kernels.hip"):
+        h.update(open(os.path.join(d, f), "rb").read())
+    return h.hexdigest()[:16]

@@ -88,6 +88,7 @@ hipError_t launch_inflate(const InflateArgs &args, int num_cus, hipStream_t stre
 enum ScratchUse { kScratchBatch = 0, kScratchInflateOrder = 1, kScratchFused = 2 };
 
 inline uint64_t plan_tiles(uint64_t n) { return n == 0 ? 1 : (n + kPlanTile - 1) / kPlanTile; }
+const char *product_kernel_name();
 hipError_t launch_plan(const uint64_t *d_lens, uint64_t n, uint64_t *d_prefix, uint64_t *d_tile_sum,
                        uint32_t *d_out, uint32_t *d_ctr, hipStream_t stream);
 

@@ -826,7 +826,9 @@ extern "C" {
 
 const char *zcrc_last_error(void) { return t_last_error.c_str(); }
 
-const char *zcrc_version(void) { return "zcrc 0.1 (gfx950, braided slice-by-4, LDS x32)"; }
+const char *zcrc_version(void) { return "zcrc 0.2 (gfx950, braided slice-by-4, LDS x32)"; }
+
+const char *zcrc_kernel_name(void) { return product_kernel_name(); }
 
 int zcrc32_checked(const void *data, size_t n_bytes, uint32_t crc, uint32_t *out_crc) {
   if (!out_crc) return fail(ZCRC_ERR_ARG, "null out_crc");
