@@ -53,9 +53,11 @@ static int cmp_d(const void *a, const void *b) {
   return x < y ? -1 : x > y;
 }
 
-static double median(double *v, int n) {
-  qsort(v, n, sizeof(double), cmp_d);
-  return v[n / 2];
+static double median(const double *v, int n) {
+  double t[1000];
+  memcpy(t, v, sizeof(double) * (size_t)n);
+  qsort(t, n, sizeof(double), cmp_d);
+  return t[n / 2];
 }
 
 typedef struct {
@@ -153,10 +155,14 @@ int main(int argc, char **argv) {
     }
     if (!ok) fprintf(stderr, "crc32-mismatch!  ZIP: %x != computed: %x (%s)\n", expected, crc, argv[a]);
     bad += !ok;
+    char holds[8192];
+    size_t hl = 0;
+    for (int k = 0; k < reps && hl + 32 < sizeof holds; k++)
+      hl += (size_t)snprintf(holds + hl, sizeof holds - hl, "%s%.1f", k ? ", " : "", hold[k]);
     printf("{\"mode\": \"%s\", \"crc\": \"%08x\", \"ok\": %s, \"reps\": %d, \"loop_ms\": %.3f, \"hold_us\": %.1f, "
-           "\"open_us\": %.1f, \"close_us\": %.1f}\n",
+           "\"open_us\": %.1f, \"close_us\": %.1f, \"hold_all_us\": [%s]}\n",
            argv[a], crc, ok ? "true" : "false", reps, median(loop, reps), median(hold, reps), median(op, reps),
-           median(cl, reps));
+           median(cl, reps), holds);
   }
   uint64_t gpu = 0, host = 0, fallback = 0;
   zcrc32_dropin_stats(&gpu, &host, &fallback);

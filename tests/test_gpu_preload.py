@@ -28,7 +28,7 @@ def test_preload_loop_modes(tmp_path, size):
     path = tmp_path / "entry.bin"
     o.payload(size, 41).tofile(path)
     exp = o.payload_crc(size, 41)
-    reps = 5 if size <= (16 << 20) else 3
+    reps = 7 if size <= (16 << 20) else 5
     modes = ["dropin", "stream"] + (["ref"] if os.path.exists(du.REF_O0) else [])
     rc, rows, stats, err = du.run_preload(exe, path, exp, reps, modes)
     assert rc == 0, err

@@ -155,10 +155,21 @@ struct BatchView {
   // read by the prologue's range search (nullptr afterwards: global copy)
   const uint64_t *lpre;
   const uint64_t tot_;
+  // the first 64-ary search level over [0, n] (lane l: prefix(min((l+1) step0,
+  // n))) is the same for every target: loaded once, with prefix[n], so every
+  // search -- the wave's range and each dynamic unit -- starts one dependent
+  // round trip later in the tree
+  uint64_t l1_;
   __device__ BatchView(const BatchArgs &args, const uint64_t *lds_prefix = nullptr)
       : a(args), lpre(lds_prefix),
         // read once per wave: prefix[n] would otherwise be re-read by every snap
-        tot_(kStrided ? args.n * args.len : uni64(lds_prefix ? lds_prefix[args.n] : args.prefix[args.n])) {}
+        tot_(kStrided ? args.n * args.len : uni64(lds_prefix ? lds_prefix[args.n] : args.prefix[args.n])) {
+    l1_ = 0;
+    if (!kStrided && args.n > 62) {
+      const uint64_t step = (args.n + 63) / 64, idx = (uint64_t)((threadIdx.x & 63u) + 1) * step;
+      l1_ = pre(idx < args.n ? idx : args.n);
+    }
+  }
   __device__ uint64_t pre(uint64_t i) const { return lpre ? lpre[i] : a.prefix[i]; }
   __device__ uint64_t prefix(uint64_t i) const { return kStrided ? i * a.len : pre(i); }
   __device__ const uint8_t *ptr(uint64_t i) const { return kStrided ? a.base + i * a.stride : a.ptrs[i]; }
@@ -189,7 +200,7 @@ struct BatchView {
       const uint64_t step = (hi - lo + 63) / 64;
       uint64_t idx = lo + (uint64_t)(lane + 1) * step;
       if (idx > hi) idx = hi;
-      const uint64_t m = __ballot(pre(idx) >= t);
+      const uint64_t m = __ballot((lo == 0 && hi == a.n ? l1_ : pre(idx)) >= t);
       const uint32_t f = (uint32_t)__builtin_ctzll(m);
       const uint64_t nhi = (lo + (uint64_t)(f + 1) * step) < hi ? (lo + (uint64_t)(f + 1) * step) : hi;
       const uint64_t nlo = f == 0 ? lo : lo + (uint64_t)f * step + 1;
@@ -251,7 +262,8 @@ struct BatchView {
       uint64_t x0 = lo0 + (uint64_t)(lane + 1) * st0, x1 = lo1 + (uint64_t)(lane + 1) * st1;
       if (x0 > hi0) x0 = hi0;
       if (x1 > hi1) x1 = hi1;
-      const uint64_t v0 = pre(x0), v1 = pre(x1);
+      const bool top0 = lo0 == 0 && hi0 == a.n, top1 = lo1 == 0 && hi1 == a.n;
+      const uint64_t v0 = top0 ? l1_ : pre(x0), v1 = top1 ? l1_ : pre(x1);
       const uint64_t m0 = __ballot(v0 >= t0), m1 = __ballot(v1 >= t1);
       if (hi0 - lo0 > 62) {
         const uint32_t f = (uint32_t)__builtin_ctzll(m0);
