@@ -182,6 +182,16 @@ int stream_scratch(hipStream_t st, int use, size_t bytes, void **out, size_t *ha
   return ZCRC_OK;
 }
 
+// Measurement knob: ZCRC_DYN_UNIT overrides the
+// dynamic part's unit size in bytes (0 = kDynUnit).
+uint64_t dyn_unit_override() {
+  static const uint64_t v = [] {
+    const char *e = getenv("ZCRC_DYN_UNIT");
+    return e ? (uint64_t)strtoull(e, nullptr, 0) : 0ull;
+  }();
+  return v;
+}
+
 int batch_device_ws(const void *const *d_ptrs, const uint64_t *d_lens, const uint32_t *d_seeds,
                     uint32_t *d_out, size_t n, void *scratch, size_t scratch_bytes, hipStream_t stream) {
   if (n == 0) return ZCRC_OK;
@@ -206,6 +216,7 @@ int batch_device_ws(const void *const *d_ptrs, const uint64_t *d_lens, const uin
   a.tab = dc->d_tab;
   a.ctr = d_ctr;
   a.dyn_shift = kDynShift;
+  a.dyn_unit = dyn_unit_override();
   return launch_main(a, false, *dc, stream);
 }
 
