@@ -1,7 +1,8 @@
 set -o pipefail
-O=gpurun_out/r2aa
+O=gpurun_out/r2ac
 mkdir -p $O
-export TMPDIR=/tmp
-for u in 65536 131072 262144 1048576; do
-  ZCRC_DYN_UNIT=$u timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/fetch_$u -o b -- python3 bench.py --config 4 --steps 3 --warmup 1 --no-cpu-baseline > $O/fetch_$u.log 2>&1 || exit 1
+for shape in "4096 65536 40" "100000 0 20" "16384 1048576 10" "1048576 1024 20" "262144 4096 20"; do
+  timeout -k 10 200 tools/crc_ab $shape >> $O/crc_ab.txt 2>&1 || exit 1
 done
+timeout -k 10 200 tools/small_probe 10 > $O/small_probe.txt 2>&1 || exit 2
+timeout -k 10 400 python -u -m pytest tests/test_gpu_parity.py -x -q --timeout 120 --timeout-method thread > $O/parity.log 2>&1 || exit 3
