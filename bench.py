@@ -313,6 +313,8 @@ def main() -> None:
     ap.add_argument("--buffers-per-gpu", type=int, default=None,
                     help="configs 3/5: override the per-GPU buffer count (rehearsals with ranks sharing a GPU)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-secondary", action="store_true",
+                    help="N=1 config 3: skip the configs 2 and 4 timed after the headline")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="nccl = RCCL over xGMI (default); gloo only to rehearse ranks sharing one GPU")
     ap.add_argument("--cpu-budget-s", type=float, default=12.0)
@@ -356,64 +358,99 @@ def main() -> None:
             else:
                 dist.barrier()
 
-    wl = Workload(args.config, rank, world, dev, args.buffers_per_gpu)
-    out = torch.empty(wl.n_local, dtype=torch.int32, device=dev)
-    result = {"global": out}
+    def measure(cfg: int, steps: int, warmup: int, n_override=None) -> dict:
+        """Warmup, then exactly `steps` timed steps between barriers and
+        synchronizes (max over ranks), then a parity spot-check."""
+        wl = Workload(cfg, rank, world, dev, n_override)
+        out = torch.empty(wl.n_local, dtype=torch.int32, device=dev)
+        result = {"global": out}
 
-    def step(s: int) -> None:
-        ptrs, lens = wl.batches[s % len(wl.batches)]
-        z.crc32_batch_device(ptrs, lens, out=out)
-        if world > 1:  # the one exchange: all-gather of the 32-bit CRCs
-            result["global"] = shard.gather_crcs(out, wl.n_total)
+        def step(s: int) -> None:
+            ptrs, lens = wl.batches[s % len(wl.batches)]
+            z.crc32_batch_device(ptrs, lens, out=out)
+            if world > 1:  # the one exchange: all-gather of the 32-bit CRCs
+                result["global"] = shard.gather_crcs(out, wl.n_total)
 
-    for s in range(args.warmup):
-        step(s)
-    torch.cuda.synchronize()
-    barrier()
-    torch.cuda.synchronize()
-    with z.profile() as prof:
-        t0 = time.perf_counter()
-        for s in range(args.steps):
-            step(args.warmup + s)
+        for s in range(warmup):
+            step(s)
         torch.cuda.synchronize()
-        t1 = time.perf_counter()
-    barrier()
-    elapsed = t1 - t0
-    if world > 1:
-        rdev = dev if args.dist_backend == "nccl" else torch.device("cpu")
-        et = torch.tensor([elapsed], dtype=torch.float64, device=rdev)
-        dist.all_reduce(et, op=dist.ReduceOp.MAX)
-        elapsed = float(et.item())
-        bt = torch.tensor([wl.bytes_local], dtype=torch.int64, device=rdev)
-        dist.all_reduce(bt, op=dist.ReduceOp.SUM)
-        bytes_all = int(bt.item())
-    else:
-        bytes_all = wl.bytes_local
+        barrier()
+        torch.cuda.synchronize()
+        with z.profile() as prof:
+            t0 = time.perf_counter()
+            for s in range(steps):
+                step(warmup + s)
+            torch.cuda.synchronize()
+            t1 = time.perf_counter()
+        barrier()
+        elapsed = t1 - t0
+        if world > 1:
+            rdev = dev if args.dist_backend == "nccl" else torch.device("cpu")
+            et = torch.tensor([elapsed], dtype=torch.float64, device=rdev)
+            dist.all_reduce(et, op=dist.ReduceOp.MAX)
+            elapsed = float(et.item())
+            bt = torch.tensor([wl.bytes_local], dtype=torch.int64, device=rdev)
+            dist.all_reduce(bt, op=dist.ReduceOp.SUM)
+            bytes_all = int(bt.item())
+        else:
+            bytes_all = wl.bytes_local
+        # parity spot-check: run batch 0 once more (collective at N>1) and compare
+        # sampled CRCs with the reference-generated golden vectors (data only)
+        step(0)
+        torch.cuda.synchronize()
+        glob = result["global"].cpu().numpy().view(np.uint32)
+        parity = golden_check(cfg, glob) if rank == 0 else None
+        res = {"wl_desc": wl.desc, "n_local": wl.n_local, "bytes_local": wl.bytes_local, "elapsed": elapsed,
+               "bytes_all": bytes_all, "avg_kernel_ms": prof.total_ms / max(prof.launches, 1),
+               "launches": prof.launches, "parity": parity}
+        del wl, out, result
+        torch.cuda.empty_cache()
+        return res
 
-    # parity spot-check: run batch 0 once more (collective at N>1) and compare
-    # sampled CRCs with the reference-generated golden vectors (data only)
-    step(0)
-    torch.cuda.synchronize()
-    glob = result["global"].cpu().numpy().view(np.uint32)
-    parity = golden_check(args.config, glob) if rank == 0 else None
+    def pmc_traffic(cfg: int, bytes_local: int):
+        """PMC traffic per launch recorded for this workload AND these kernel
+        sources (tools/collect_profiles.sh -> profiles/pmc_traffic.json)."""
+        path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+        if not os.path.exists(path):
+            return None, None
+        pm = json.load(open(path)).get(str(cfg))
+        if (pm and pm.get("bytes_per_gpu_per_step") == bytes_local
+                and pm.get("kernel_source_hash") == z.kernel_source_hash()):
+            return pm["traffic_bytes_per_launch"], pm["source"]
+        return None, None
+
+    m = measure(args.config, args.steps, args.warmup, args.buffers_per_gpu)
+    elapsed, bytes_all = m["elapsed"], m["bytes_all"]
+
+    class _WL:  # the headline workload's figures, for the line below
+        desc, n_local, bytes_local = m["wl_desc"], m["n_local"], m["bytes_local"]
+    wl = _WL()
+    parity = m["parity"]
+
+    # Secondary configs (N = 1 only): SURVEY 8(d) configs 2 and 4, timed the
+    # same way in the same run, so that they too carry the driver's clock.
+    secondary = None
+    if world == 1 and args.config == 3 and not args.no_secondary:
+        secondary = {}
+        for c in (2, 4):
+            r = measure(c, max(args.steps, 20), max(args.warmup, 3))
+            ach = r["bytes_local"] / (r["avg_kernel_ms"] * 1e-3) / 1e9
+            tr, _ = pmc_traffic(c, r["bytes_local"])
+            secondary[f"config{c}"] = {
+                "workload": r["wl_desc"], "value": round(r["bytes_all"] * max(args.steps, 20) / r["elapsed"] / GiB, 2),
+                "unit": "GiB/s", "ms_per_step": round(r["elapsed"] / max(args.steps, 20) * 1e3, 4),
+                "avg_kernel_ms": round(r["avg_kernel_ms"], 4), "achieved": round(ach, 1),
+                "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None if tr is None else int(tr),
+                "parity": r["parity"]}
 
     ms_per_step = elapsed / args.steps * 1e3
     value = bytes_all * args.steps / elapsed / GiB
-    avg_kernel_ms = prof.total_ms / max(prof.launches, 1)
+    avg_kernel_ms = m["avg_kernel_ms"]
     achieved = wl.bytes_local / (avg_kernel_ms * 1e-3) / 1e9
     traffic = args.pmc_traffic_bytes
     traffic_src = "--pmc-traffic-bytes" if traffic is not None else None
-    pmc_path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-    if traffic is None and os.path.exists(pmc_path):
-        # PMC traffic per config, collected by tools/collect_profiles.sh for
-        # the kernel this build launches (same workload bytes)
-        # only for the same workload and the same kernel sources: a traffic
-        # figure measured for another kernel build is not reported
-        pm = json.load(open(pmc_path)).get(str(args.config))
-        if (pm and pm.get("bytes_per_gpu_per_step") == wl.bytes_local
-                and pm.get("kernel_source_hash") == z.kernel_source_hash()):
-            traffic = pm["traffic_bytes_per_launch"]
-            traffic_src = pm["source"]
+    if traffic is None:
+        traffic, traffic_src = pmc_traffic(args.config, wl.bytes_local)
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(args.config, args.cpu_budget_s, args.cpu_sample_gib)
@@ -455,10 +492,11 @@ def main() -> None:
                 "kernel": z.kernel_name(),
                 "kernel_source_hash": z.kernel_source_hash(),
                 "avg_kernel_ms": round(avg_kernel_ms, 4),
-                "launches_timed": prof.launches,
+                "launches_timed": m["launches"],
             },
             "cpu_baseline": cpu,
             "parity": parity,
+            "secondary": secondary,
             "device": torch.cuda.get_device_name(dev),
         }
         print(json.dumps(line), flush=True)
