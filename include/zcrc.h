@@ -71,9 +71,9 @@ int zcrc32_checked(const void *data, size_t n_bytes, uint32_t crc, uint32_t *out
  * as few launches as fit the staging area.  flags: reserved, pass 0.
  * Staging: a process-wide pool of 16 MiB pinned + 16 MiB HBM slots, at most
  * ZCRC_STAGING_MIB (env, default 256) of each per device.  A call leases one
- * slot (waiting while none is free) plus a second if one is free, and
- * returns them before it returns; streams hold theirs from the first
- * update() to final(). */
+ * slot (waiting while none is free, at most 10 s: then ZCRC_ERR_HIP) plus a
+ * second if one is free, and returns them before it returns; streams hold
+ * theirs from the first update() to final(). */
 int zcrc32_batch(const void *const *ptrs, const size_t *lens, const uint32_t *seeds_or_null,
                  uint32_t *out, size_t n, unsigned flags);
 

@@ -72,3 +72,51 @@ def test_stream_objects_are_reused():
             s.update(np.full(100, k, dtype=np.uint8))
             assert s.final() == zlib.crc32(bytes([k]) * 100, k)
     assert z.staging_info()["slots_in_use"] == 0
+
+
+_ONE_SLOT = r"""
+import ctypes, sys, threading, zlib
+import numpy as np
+sys.path.insert(0, ".")
+import zipsfs_amd as z
+from zipsfs_amd import _lib
+from oracle import oracle as o
+lib = _lib.lib()
+big = [o.payload(L, 50 + i) for i, L in enumerate([40 << 20, (16 << 20) + 5, 33 << 20])]
+exp = [zlib.crc32(b.tobytes()) for b in big]
+# one slot: every launch of a > 16 MiB buffer chains through the same slot
+assert list(z.crc32_batch(big)) == exp, "batch through one slot"
+assert [z.cg_crc32(b) for b in big] == exp, "checked path through one slot"
+# a stream holds the only slot: the drop-in does not wait, answers on the host
+s = z.Crc32Stream()
+s.update(big[0][: 1 << 20])
+before = ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_uint64()
+lib.zcrc32_dropin_stats(*[ctypes.byref(x) for x in before])
+got = lib.zcrc32(big[1].ctypes.data, big[1].size, 0)
+after = ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_uint64()
+lib.zcrc32_dropin_stats(*[ctypes.byref(x) for x in after])
+assert got == exp[1]
+assert after[1].value == before[1].value + 1 and after[0].value == before[0].value, "busy pool -> host answer"
+assert s.final() == zlib.crc32(big[0][: 1 << 20].tobytes())
+s.close()
+info = z.staging_info()
+assert info["slots_budget"] == 1 and info["slots_peak"] == 1 and info["slots_in_use"] == 0, info
+print("one-slot pool ok", info)
+"""
+
+
+def test_staging_pool_with_one_slot(tmp_path):
+    """ZCRC_STAGING_MIB=16 (one slot): buffers larger than a slot chain their
+    launches through it, the waiting GPU path works, and a drop-in call made
+    while a stream holds the only slot is answered by the host CRC instead of
+    waiting (it runs under mutex_fhandle)."""
+    import os
+    import subprocess
+    import sys
+    script = tmp_path / "one_slot.py"
+    script.write_text(_ONE_SLOT)
+    env = dict(os.environ, ZCRC_STAGING_MIB="16", ZCRC_GPU_MIN_BYTES="0")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    p = subprocess.run([sys.executable, str(script)], cwd=root, env=env, capture_output=True, text=True, timeout=300)
+    assert p.returncode == 0, p.stdout + p.stderr
+    print(p.stdout.strip())

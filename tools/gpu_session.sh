@@ -1,5 +1,4 @@
 set -o pipefail
-O=gpurun_out/r2ad
+O=gpurun_out/r2ae
 mkdir -p $O
-timeout -k 10 400 python -u bench.py > $O/bench_default.jsonl 2> $O/bench_default.err || exit 1
-timeout -k 10 300 python -u bench.py --gpus 2 --dist-backend gloo --buffers-per-gpu 32768 --steps 5 --warmup 2 > $O/spawn2_gloo.jsonl 2> $O/spawn2_gloo.err || exit 2
+timeout -k 10 400 python -u -m pytest tests/test_gpu_host_pool.py tests/test_gpu_dropin.py -x -v -s --timeout 300 --timeout-method thread > $O/pool_tests.log 2>&1 || exit 1

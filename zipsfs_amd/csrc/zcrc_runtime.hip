@@ -16,6 +16,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <condition_variable>
 #include <map>
 #include <mutex>
@@ -274,6 +275,7 @@ int batch_device_fused(const void *const *d_ptrs, const uint64_t *d_lens, const 
 constexpr size_t kStageBytes = 16ull << 20;  // = ZIPsFS PRELOADRAM_READ_BYTES_NUM
 constexpr size_t kStageItems = 1u << 14;
 constexpr size_t kDefaultStagingMiB = 256;
+constexpr int kSlotWaitSeconds = 10;
 
 struct StageSlot {
   int dev = -1;
@@ -358,7 +360,12 @@ class SlotPool {
         return ZCRC_OK;
       }
       if (!wait) return ZCRC_OK;
-      cv_.wait(lk);
+      // bounded: a caller that itself holds the budget's slots (e.g. through
+      // open streams) would otherwise wait forever
+      if (cv_.wait_for(lk, std::chrono::seconds(kSlotWaitSeconds)) == std::cv_status::timeout && d.free.empty() &&
+          d.created >= budget_slots_)
+        return fail(ZCRC_ERR_HIP, "host staging pool exhausted: no slot freed within " +
+                                      std::to_string(kSlotWaitSeconds) + " s (ZCRC_STAGING_MIB)");
     }
   }
   void release(StageSlot *s) {
