@@ -1,8 +1,5 @@
 set -o pipefail
-O=gpurun_out/r2af
+O=gpurun_out/r2ag
 mkdir -p $O
-for shape in "4096 65536 40" "100000 0 20" "16384 1048576 10" "1048576 1024 20" "262144 4096 20"; do
-  timeout -k 10 200 tools/crc_ab $shape >> $O/crc_ab.txt 2>&1 || exit 1
-done
-timeout -k 10 200 tools/c2_probe 48 > $O/c2_probe.txt 2>&1 || exit 2
-timeout -k 10 400 python -u -m pytest tests/test_gpu_parity.py -x -q --timeout 120 --timeout-method thread > $O/parity.log 2>&1 || exit 3
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $O/gpu_tests.log 2>&1 || exit 1
+timeout -k 10 200 python -u -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > $O/smoke.log 2>&1 || exit 2
