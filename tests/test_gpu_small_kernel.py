@@ -1,0 +1,115 @@
+"""GPU parity of the small-buffer kernel (zipsfs_amd/csrc/zcrc_small_kernel.h).
+
+Whole buffers of at most kSmallMax = 8192 bytes go to the small kernel from
+the strided API, the host batch API (zcrc32_batch: direct and staged paths,
+where a mixed launch is partitioned into batch-kernel and small-kernel lists)
+and the device API's split plan.  Every result is compared bit-exactly with
+the CPU oracle (oracle/) or zlib on the same bytes, and with the batch kernel
+alone (ZCRC_SMALL=0).
+"""
+import random
+import zlib
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+import zipsfs_amd as z  # noqa: E402
+from oracle import oracle as o  # noqa: E402
+
+DEV = "cuda:0"
+SMALL_MAX = 8192
+
+# every length 0..300, then the block (256 B), lane-group (2 KiB mean: 8 vs 16
+# lanes) and size-limit boundaries
+LENGTHS = list(range(0, 301)) + [
+    511, 512, 513, 1000, 1023, 1024, 1025, 2047, 2048, 2049, 3000, 3971, 4095, 4096, 4097,
+    6000, 8175, 8176, 8177, 8191, 8192, 8193, 12288, 16384]
+
+
+def u32(t):
+    return t.cpu().numpy().view(np.uint32)
+
+
+def _seeds(rnd, n):
+    s = np.array([rnd.getrandbits(32) for _ in range(n)], dtype=np.uint32)
+    s[::5] = 0
+    return s, torch.tensor(s.view(np.int32), device=DEV)
+
+
+def _oracle(host, base_addr_offsets, lens, seeds):
+    ap = np.array([host.ctypes.data + int(q) for q in base_addr_offsets], dtype=np.uint64)
+    return o.crc32_batch(ap, np.asarray(lens, dtype=np.uint64), seeds, nthreads=8)
+
+
+@pytest.mark.parametrize("small", ["1", "0"])
+def test_strided_every_small_length(small, monkeypatch):
+    """Strided batches of each length at a misaligned base and odd strides,
+    with seeds; n = 37 (not a multiple of the 4 or 8 buffers per wave)."""
+    monkeypatch.setenv("ZCRC_SMALL", small)
+    rnd = random.Random(11)
+    n = 37
+    for L in LENGTHS:
+        lead, stride = rnd.randrange(16), L + rnd.choice([0, 1, 3, 16, 29])
+        total = lead + n * stride + 64
+        mem = torch.randint(0, 256, (total,), dtype=torch.uint8, device=DEV)
+        seeds_np, seeds = _seeds(rnd, n)
+        got = u32(z.crc32_batch_strided(mem[lead:], stride, L, n, seeds=seeds))
+        host = mem.cpu().numpy()
+        exp = _oracle(host, [lead + i * stride for i in range(n)], [L] * n, seeds_np)
+        np.testing.assert_array_equal(got, exp, err_msg=f"len {L}")
+
+
+def test_strided_large_uniform_batches():
+    """Whole-chip uniform batches (1 KiB and 4 KiB, 64 MiB each): every CRC
+    against the oracle on the generator's bytes, with and without seeds."""
+    for L in (1024, 4096, 3000):
+        n = (64 << 20) // L
+        mem = torch.empty(n * L + 64, dtype=torch.uint8, device=DEV)
+        ptrs = mem.data_ptr() + torch.arange(n, dtype=torch.int64, device=DEV) * L
+        lens = torch.full((n,), L, dtype=torch.int64, device=DEV)
+        z.fill_synthetic(ptrs, lens, index0=5, seed=o.PAYLOAD_SEED)
+        got = u32(z.crc32_batch_strided(mem, L, L, n))
+        host = mem.cpu().numpy()
+        exp = _oracle(host, [i * L for i in range(n)], [L] * n, np.zeros(n, np.uint32))
+        np.testing.assert_array_equal(got, exp, err_msg=f"len {L}")
+        seeds_np = (np.arange(n, dtype=np.uint64) * 2654435761 % (1 << 32)).astype(np.uint32)
+        seeds = torch.tensor(seeds_np.view(np.int32), device=DEV)
+        got = u32(z.crc32_batch_strided(mem, L, L, n, seeds=seeds))
+        exp = _oracle(host, [i * L for i in range(n)], [L] * n, seeds_np)
+        np.testing.assert_array_equal(got, exp, err_msg=f"len {L} seeded")
+
+
+@pytest.mark.parametrize("small", ["1", "0"])
+def test_host_batch_direct_and_partitioned(small, monkeypatch):
+    """zcrc32_batch: all-small direct calls, mixed direct calls, and staged
+    launches that mix continuation parts, large and small buffers."""
+    monkeypatch.setenv("ZCRC_SMALL", small)
+    rnd = random.Random(5)
+    cases = [
+        [rnd.choice(LENGTHS) for _ in range(300)],                            # direct, all small
+        [rnd.choice(LENGTHS + [20_000, 65_536]) for _ in range(200)],         # direct, mixed
+        [rnd.choice(LENGTHS + [100_000, 3_000_000]) for _ in range(3000)],    # staged, mixed
+        [5, 17 << 20, 4096, 0, 3, (40 << 20) + 7, 8192, 1, 8193, 100],        # continuation parts
+    ]
+    for k, lens in enumerate(cases):
+        bufs = [o.payload(L, 900 + k * 10_000 + i) for i, L in enumerate(lens)]
+        seeds = [rnd.getrandbits(32) if i % 3 else 0 for i in range(len(bufs))]
+        got = z.crc32_batch(bufs, seeds=seeds)
+        exp = [zlib.crc32(b.tobytes(), s) for b, s in zip(bufs, seeds)]
+        assert list(got) == exp, f"case {k}"
+
+
+def test_config4_golden_through_host_batch(golden):
+    """The config-4 golden sample (reference CRCs) through the host batch API,
+    whose staged launches split it between the two kernels."""
+    cfg = golden["cfg"]
+    idx = cfg["cfg4_idx"].astype(np.int64)
+    L = cfg["cfg4_len"].astype(np.int64)
+    bufs = [o.payload(int(n), int(i)) for n, i in zip(L, idx)]
+    got = z.crc32_batch(bufs)
+    np.testing.assert_array_equal(np.asarray(got, dtype=np.uint32), cfg["cfg4"])
+    assert int((L <= SMALL_MAX).sum()) > 0 and int((L > SMALL_MAX).sum()) > 0

@@ -396,6 +396,6 @@ def kernel_source_hash() -> str:
     import os
     h = hashlib.sha256()
     d = os.path.join(os.path.dirname(os.path.abspath(__file__)), "csrc")
-    for f in ("zcrc_batch_kernel.h", "zcrc_internal.h", "zcrc_gf2.h", "zcrc_kernels.hip"):
+    for f in ("zcrc_batch_kernel.h", "zcrc_small_kernel.h", "zcrc_internal.h", "zcrc_gf2.h", "zcrc_kernels.hip"):
         h.update(open(os.path.join(d, f), "rb").read())
     return h.hexdigest()[:16]

@@ -33,6 +33,7 @@ struct TableBlob {
   uint32_t tshift[16 * 4 * 256]; // x^(-8t), t = 0..15 (16-B alignment padding)
   uint32_t stdtab[256];          // standard byte table (buffers < 4 bytes)
   uint32_t x8pow[64];            // x^(8 * 2^k)
+  uint32_t braid256[4 * 256];    // MCT(x^(8*256)): the small-buffer kernel's table
 };
 
 struct BatchArgs {
@@ -63,6 +64,32 @@ struct BatchArgs {
   uint64_t *acc;
   uint32_t *done;
 };
+
+// Small-buffer kernel (zcrc_small_kernel.h): whole buffers of at most
+// kSmallMax bytes, kSmallLanes lanes per buffer.  General form: entry k of
+// the list is buffer j = sidx ? sidx[k] : k with ptrs[j], length lens[j] (or
+// prefix[j+1] - prefix[j] when lens is null), seeds[j], out[j]; the count is
+// *n_dev when n_dev is set (written by the split plan), else n.  Strided
+// form: buffer k = base + k*stride of length len.
+constexpr uint64_t kSmallMax = 8192;
+struct SmallArgs {
+  const uint8_t *const *ptrs;
+  const uint64_t *lens;
+  const uint64_t *prefix;
+  const uint32_t *sidx;
+  const uint8_t *base;
+  uint64_t stride;
+  uint64_t len;
+  const uint32_t *seeds;
+  uint32_t *out;
+  uint64_t n;
+  const uint64_t *n_dev;
+  const TableBlob *tab;
+};
+// lanes: 16 or 8 lanes per buffer (8 pays below ~2 KiB: more buffers in flight)
+hipError_t launch_small(const SmallArgs &args, bool strided, int lanes, int num_cus, hipStream_t stream,
+                        hipEvent_t t0 = nullptr, hipEvent_t t1 = nullptr);
+const char *small_kernel_name(int lanes);
 
 // t0/t1: optional events stamped with the kernel's own start and end
 hipError_t launch_batch(const BatchArgs &args, bool strided, int num_cus, hipStream_t stream,

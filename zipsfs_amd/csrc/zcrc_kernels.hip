@@ -9,6 +9,7 @@
 #include <mutex>
 
 #include "zcrc_batch_kernel.h"
+#include "zcrc_small_kernel.h"
 
 namespace zcrc {
 
@@ -142,6 +143,30 @@ const char *product_kernel_name() {
              kLoadNt, kWindowed ? "true" : "false");
   });
   return name;
+}
+
+// Small whole buffers: 16 lanes per buffer with 8 blocks in flight, or 8
+// lanes with 4 (same 32 VGPRs of loads, twice the buffers: pays below ~2 KiB).
+hipError_t launch_small(const SmallArgs &args, bool strided, int lanes, int num_cus, hipStream_t stream,
+                        hipEvent_t t0, hipEvent_t t1) {
+  const dim3 grid((unsigned)num_cus), block(kThreads);
+  if (strided) {
+    if (lanes == 8)
+      hipExtLaunchKernelGGL((crc32_small_kernel<true, 8, 4>), grid, block, 0, stream, t0, t1, 0, args);
+    else
+      hipExtLaunchKernelGGL((crc32_small_kernel<true, 16, 8>), grid, block, 0, stream, t0, t1, 0, args);
+  } else {
+    if (lanes == 8)
+      hipExtLaunchKernelGGL((crc32_small_kernel<false, 8, 4>), grid, block, 0, stream, t0, t1, 0, args);
+    else
+      hipExtLaunchKernelGGL((crc32_small_kernel<false, 16, 8>), grid, block, 0, stream, t0, t1, 0, args);
+  }
+  return hipGetLastError();
+}
+
+// the general-form small kernel as rocprofv3 names it
+const char *small_kernel_name(int lanes) {
+  return lanes == 8 ? "zcrc::crc32_small_kernel<false, 8, 4>" : "zcrc::crc32_small_kernel<false, 16, 8>";
 }
 
 hipError_t launch_plan(const uint64_t *d_lens, uint64_t n, uint64_t *d_prefix, uint64_t *d_tile_sum,

@@ -121,7 +121,9 @@ std::vector<hipEvent_t> g_prof_free;  // recycled: no hipEventCreate per launch
 double g_prof_ms = 0.0;
 int g_prof_count = 0;
 
-int launch_main(const BatchArgs &args, bool strided, const DeviceCtx &dc, hipStream_t stream, bool fused = false) {
+// Launch through `fn(t0, t1)`, with dispatch-packet timestamps when profiling.
+template <class F>
+int launch_timed(F fn) {
   hipEvent_t e0 = nullptr, e1 = nullptr;
   const bool prof = g_prof_on.load(std::memory_order_relaxed) != 0;
   if (prof) {
@@ -133,12 +135,33 @@ int launch_main(const BatchArgs &args, bool strided, const DeviceCtx &dc, hipStr
     if (!e0) ZCRC_HIP_TRY(hipEventCreate(&e0));
     if (!e1) ZCRC_HIP_TRY(hipEventCreate(&e1));
   }
-  ZCRC_HIP_TRY(launch_batch(args, strided, dc.num_cus, stream, e0, e1, fused));
+  ZCRC_HIP_TRY(fn(e0, e1));
   if (prof) {
     std::lock_guard<std::mutex> lk(g_prof_mu);
     g_prof_pending.emplace_back(e0, e1);
   }
   return ZCRC_OK;
+}
+
+int launch_main(const BatchArgs &args, bool strided, const DeviceCtx &dc, hipStream_t stream, bool fused = false) {
+  return launch_timed(
+      [&](hipEvent_t t0, hipEvent_t t1) { return launch_batch(args, strided, dc.num_cus, stream, t0, t1, fused); });
+}
+
+// The small-buffer kernel (zcrc_small_kernel.h) takes whole buffers of at
+// most kSmallMax bytes.  ZCRC_SMALL=0 routes everything through the batch
+// kernel (A/B measurement; read per call so that tests can switch it).
+bool small_enabled() {
+  const char *e = getenv("ZCRC_SMALL");
+  return !(e && e[0] == '0');
+}
+
+// 8 lanes per buffer below ~2 KiB mean (more buffers in flight), else 16
+int small_lanes(uint64_t mean_len) { return mean_len <= 2048 ? 8 : 16; }
+
+int launch_small_timed(const SmallArgs &args, bool strided, int lanes, const DeviceCtx &dc, hipStream_t stream) {
+  return launch_timed(
+      [&](hipEvent_t t0, hipEvent_t t1) { return launch_small(args, strided, lanes, dc.num_cus, stream, t0, t1); });
 }
 
 // ------------------------------------------------------------- device batch
@@ -572,14 +595,28 @@ int batch_host_direct(const DeviceCtx &dc, StageSlot &s, const void *const *ptrs
   }
   h_prefix[n] = pos;
   CopyPool::get().run(jobs);
-  BatchArgs a{};
-  a.ptrs = reinterpret_cast<const uint8_t *const *>(s.h_meta_dev);
-  a.prefix = reinterpret_cast<const uint64_t *>(s.h_meta_dev + off_prefix);
-  a.seeds = reinterpret_cast<const uint32_t *>(s.h_meta_dev + off_seeds);
-  a.out = reinterpret_cast<uint32_t *>(s.h_meta_dev + kMetaRes);
-  a.n = n;
-  a.tab = dc.d_tab;
-  int rc = launch_main(a, false, dc, s.stream);
+  bool all_small = small_enabled();
+  for (size_t i = 0; i < n && all_small; i++) all_small = lens[i] <= kSmallMax;
+  int rc;
+  if (all_small) {  // several buffers per wave: more PCIe reads in flight
+    SmallArgs a{};
+    a.ptrs = reinterpret_cast<const uint8_t *const *>(s.h_meta_dev);
+    a.prefix = reinterpret_cast<const uint64_t *>(s.h_meta_dev + off_prefix);
+    a.seeds = reinterpret_cast<const uint32_t *>(s.h_meta_dev + off_seeds);
+    a.out = reinterpret_cast<uint32_t *>(s.h_meta_dev + kMetaRes);
+    a.n = n;
+    a.tab = dc.d_tab;
+    rc = launch_small_timed(a, false, small_lanes(pos / n), dc, s.stream);
+  } else {
+    BatchArgs a{};
+    a.ptrs = reinterpret_cast<const uint8_t *const *>(s.h_meta_dev);
+    a.prefix = reinterpret_cast<const uint64_t *>(s.h_meta_dev + off_prefix);
+    a.seeds = reinterpret_cast<const uint32_t *>(s.h_meta_dev + off_seeds);
+    a.out = reinterpret_cast<uint32_t *>(s.h_meta_dev + kMetaRes);
+    a.n = n;
+    a.tab = dc.d_tab;
+    rc = launch_main(a, false, dc, s.stream);
+  }
   if (rc) return rc;
   ZCRC_HIP_TRY(hipEventRecord(s.done, s.stream));
   ZCRC_HIP_TRY(hipEventSynchronize(s.done));
@@ -621,8 +658,10 @@ int batch_host(const void *const *ptrs, const size_t *lens, const uint32_t *seed
     uint64_t *h_ptrs = reinterpret_cast<uint64_t *>(s.h_meta + kMetaPtrs);
     uint64_t *h_prefix = reinterpret_cast<uint64_t *>(s.h_meta + kMetaPrefix);
     uint32_t *h_seeds = reinterpret_cast<uint32_t *>(s.h_meta + kMetaSeeds);
-    size_t used = 0, items = 0;
+    size_t used = 0, items = 0, n_small = 0;
     std::vector<CopyJob> jobs;
+    std::vector<uint8_t> is_small;  // item is a whole buffer of <= kSmallMax bytes
+    const bool small_on = small_enabled();
     bool continuation = false;  // item 0 continues the previous launch's last item
     uint64_t pos = 0;
     while (i < n && items < kStageItems) {
@@ -641,6 +680,9 @@ int batch_host(const void *const *ptrs, const size_t *lens, const uint32_t *seed
       pos += take;
       used = (used + take + 15) & ~size_t(15);
       const bool done_buf = (take == remaining);
+      const bool small = small_on && part_off == 0 && done_buf && len <= kSmallMax;
+      is_small.push_back(small);
+      n_small += small;
       if (done_buf) {
         s.scatter.emplace_back(i, (uint32_t)items);
         i++;
@@ -653,6 +695,33 @@ int batch_host(const void *const *ptrs, const size_t *lens, const uint32_t *seed
     }
     h_prefix[items] = pos;
     CopyPool::get().run(jobs);
+    // small whole buffers go last, to the small-buffer kernel; the rest keep
+    // their order (a continuation stays item 0) for the batch kernel
+    uint32_t last_item = (uint32_t)(items - 1);
+    if (n_small && n_small < items) {
+      std::vector<uint64_t> p2(items), l2(items);
+      std::vector<uint32_t> s2(items), newpos(items);
+      size_t kl = 0, ks = items - n_small;
+      for (size_t k = 0; k < items; k++) {
+        const size_t d = is_small[k] ? ks++ : kl++;
+        newpos[k] = (uint32_t)d;
+        p2[d] = h_ptrs[k];
+        l2[d] = h_prefix[k + 1] - h_prefix[k];
+        s2[d] = h_seeds[k];
+      }
+      uint64_t run = 0;
+      for (size_t d = 0; d < items; d++) {
+        h_ptrs[d] = p2[d];
+        h_seeds[d] = s2[d];
+        h_prefix[d] = run;
+        run += l2[d];
+      }
+      h_prefix[items] = run;
+      for (auto &e : s.scatter) e.second = newpos[e.second];
+      last_item = newpos[items - 1];
+    }
+    const size_t n_large = items - n_small;
+    const uint64_t small_mean = n_small ? (h_prefix[items] - h_prefix[n_large]) / n_small : 0;
     // compact the metadata to [ptrs | prefix | seeds] for `items` entries so a
     // one-entry call moves ~20 bytes, not the whole 1.3 MB area
     const size_t off_prefix = 8 * items, off_seeds = off_prefix + 8 * (items + 1);
@@ -674,23 +743,38 @@ int batch_host(const void *const *ptrs, const size_t *lens, const uint32_t *seed
       ZCRC_HIP_TRY(hipMemcpyAsync(d_seeds, reinterpret_cast<uint32_t *>(p.d_meta + kMetaRes) + prev_item, 4,
                                   hipMemcpyDeviceToDevice, s.stream));
     }
-    BatchArgs a{};
-    a.ptrs = reinterpret_cast<const uint8_t *const *>(s.d_meta + kMetaPtrs);
-    a.prefix = reinterpret_cast<const uint64_t *>(s.d_meta + off_prefix);
-    a.seeds = d_seeds;
-    a.out = d_res;
-    a.n = items;
-    a.tab = dc->d_tab;
-    // split pieces xor into d_res: zero it first
-    ZCRC_HIP_TRY(hipMemsetAsync(d_res, 0, 4 * items, s.stream));
-    rc = launch_main(a, false, *dc, s.stream);
-    if (rc) return rc;
+    const uint8_t *const *d_ptrs = reinterpret_cast<const uint8_t *const *>(s.d_meta + kMetaPtrs);
+    const uint64_t *d_prefix = reinterpret_cast<const uint64_t *>(s.d_meta + off_prefix);
+    if (n_large) {
+      BatchArgs a{};
+      a.ptrs = d_ptrs;
+      a.prefix = d_prefix;
+      a.seeds = d_seeds;
+      a.out = d_res;
+      a.n = n_large;
+      a.tab = dc->d_tab;
+      // split pieces xor into d_res: zero it first
+      ZCRC_HIP_TRY(hipMemsetAsync(d_res, 0, 4 * n_large, s.stream));
+      rc = launch_main(a, false, *dc, s.stream);
+      if (rc) return rc;
+    }
+    if (n_small) {
+      SmallArgs a{};
+      a.ptrs = d_ptrs + n_large;
+      a.prefix = d_prefix + n_large;
+      a.seeds = d_seeds + n_large;
+      a.out = d_res + n_large;
+      a.n = n_small;
+      a.tab = dc->d_tab;
+      rc = launch_small_timed(a, false, small_lanes(small_mean), *dc, s.stream);
+      if (rc) return rc;
+    }
     ZCRC_HIP_TRY(hipEventRecord(s.kernel, s.stream));
     ZCRC_HIP_TRY(hipMemcpyAsync(s.h_meta + kMetaRes, d_res, 4 * items, hipMemcpyDeviceToHost, s.stream));
     ZCRC_HIP_TRY(hipEventRecord(s.done, s.stream));
     s.busy = true;
     prev_slot = cur;
-    prev_item = (uint32_t)(items - 1);
+    prev_item = last_item;
     cur = (cur + 1) % lease.count;
   }
   for (int k = 0; k < lease.count; k++) {
@@ -962,6 +1046,17 @@ int zcrc32_batch_device_strided(const void *d_base, uint64_t stride, uint64_t le
   int rc = device_ctx(&dc);
   if (rc) return rc;
   hipStream_t st = static_cast<hipStream_t>(stream);
+  if (len <= kSmallMax && small_enabled()) {  // whole small buffers: one small-kernel launch
+    SmallArgs a{};
+    a.base = static_cast<const uint8_t *>(d_base);
+    a.stride = stride;
+    a.len = len;
+    a.seeds = d_seeds_or_null;
+    a.out = d_out;
+    a.n = n;
+    a.tab = dc->d_tab;
+    return launch_small_timed(a, true, small_lanes(len), *dc, st);
+  }
   // keep every launch under kMaxLaunchBytes of payload
   const size_t per = len ? (size_t)std::max<uint64_t>(1, kMaxLaunchBytes / len) : n;
   // work counter for the kernel's dynamic half, only when it can engage
