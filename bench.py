@@ -32,6 +32,7 @@ sys.path.insert(0, ROOT)
 
 GiB = float(1 << 30)
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec, /opt/skills/guides/MI355X_MICROARCH.md
+SMALL_MAX = 8192  # zcrc_internal.h kSmallMax: the split plan's small-buffer bound
 PAYLOAD_SEED = 0xC0FFEE
 METRIC = "CRC32 GiB/s device-resident (batched chunks) and % of HBM3E read peak"
 
@@ -400,9 +401,25 @@ def main() -> None:
         torch.cuda.synchronize()
         glob = result["global"].cpu().numpy().view(np.uint32)
         parity = golden_check(cfg, glob) if rank == 0 else None
+        # bytes per step each CRC kernel reads: above kFusedMaxN buffers the
+        # split plan gives those of <= SMALL_MAX bytes to the small kernel
+        # when they carry >= 1/8 of the bytes (zcrc_kernels.hip, kSplitShare;
+        # ZCRC_SMALL=2: whenever there is one, 0: never)
+        lens0 = wl.batches[0][1]
+        small = lens0[lens0 <= SMALL_MAX]
+        small_b = int(small.sum().item())
+        mode = os.environ.get("ZCRC_SMALL", "1")
+        split = (prof.small_launches > 0 and len(small) > 0 and mode != "0"
+                 and (mode == "2" or small_b * 8 >= wl.bytes_local))
+        small_b = small_b if split else 0
         res = {"wl_desc": wl.desc, "n_local": wl.n_local, "bytes_local": wl.bytes_local, "elapsed": elapsed,
                "bytes_all": bytes_all, "avg_kernel_ms": prof.total_ms / max(prof.launches, 1),
-               "launches": prof.launches, "parity": parity}
+               "launches": prof.launches, "parity": parity, "bytes_main": wl.bytes_local - small_b,
+               "small": None if not prof.small_launches else {
+                   "kernel": z.small_kernel_name(), "launches_timed": prof.small_launches,
+                   "avg_kernel_ms": round(prof.small_ms / prof.small_launches, 4),
+                   "algorithmic_bytes_per_launch": small_b,
+                   "achieved": round(small_b / (prof.small_ms / prof.small_launches * 1e-3) / 1e9, 1)}}
         del wl, out, result
         torch.cuda.empty_cache()
         return res
@@ -434,19 +451,20 @@ def main() -> None:
         secondary = {}
         for c in (2, 4):
             r = measure(c, max(args.steps, 20), max(args.warmup, 3))
-            ach = r["bytes_local"] / (r["avg_kernel_ms"] * 1e-3) / 1e9
+            ach = r["bytes_main"] / (r["avg_kernel_ms"] * 1e-3) / 1e9
             tr, _ = pmc_traffic(c, r["bytes_local"])
             secondary[f"config{c}"] = {
                 "workload": r["wl_desc"], "value": round(r["bytes_all"] * max(args.steps, 20) / r["elapsed"] / GiB, 2),
                 "unit": "GiB/s", "ms_per_step": round(r["elapsed"] / max(args.steps, 20) * 1e3, 4),
                 "avg_kernel_ms": round(r["avg_kernel_ms"], 4), "achieved": round(ach, 1),
                 "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None if tr is None else int(tr),
+                "algorithmic_bytes_per_launch": r["bytes_main"], "small_kernel": r["small"],
                 "parity": r["parity"]}
 
     ms_per_step = elapsed / args.steps * 1e3
     value = bytes_all * args.steps / elapsed / GiB
     avg_kernel_ms = m["avg_kernel_ms"]
-    achieved = wl.bytes_local / (avg_kernel_ms * 1e-3) / 1e9
+    achieved = m["bytes_main"] / (avg_kernel_ms * 1e-3) / 1e9
     traffic = args.pmc_traffic_bytes
     traffic_src = "--pmc-traffic-bytes" if traffic is not None else None
     if traffic is None:
@@ -488,11 +506,12 @@ def main() -> None:
                 "traffic": None if traffic is None else int(traffic),
                 "traffic_unit": "bytes per launch (HBM read+write, PMC)",
                 "traffic_source": traffic_src,
-                "algorithmic_bytes_per_launch": wl.bytes_local,
+                "algorithmic_bytes_per_launch": m["bytes_main"],
                 "kernel": z.kernel_name(),
                 "kernel_source_hash": z.kernel_source_hash(),
                 "avg_kernel_ms": round(avg_kernel_ms, 4),
                 "launches_timed": m["launches"],
+                "small_kernel": m["small"],
             },
             "cpu_baseline": cpu,
             "parity": parity,

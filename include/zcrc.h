@@ -81,8 +81,13 @@ int zcrc32_batch(const void *const *ptrs, const size_t *lens, const uint32_t *se
  * d_lens: device array of n byte counts; d_seeds_or_null: device array or
  * NULL; d_out: device array of n results.  Asynchronous on `stream`; its
  * scratch (work counter, length prefix, plan tile sums: 256 + 8*(n+1) +
- * 8*ceil(n/8192) bytes) is a grow-only buffer cached per stream (stream-
- * ordered allocations under graph capture). */
+ * 8*ceil(n/8192) bytes; above 8192 buffers also the split lists, 20*n +
+ * 16*ceil(n/8192) more) is a grow-only buffer cached per stream (stream-
+ * ordered allocations under graph capture).  Above 8192 buffers the plan may
+ * split the batch on the device: when buffers of at most 8 KiB carry at
+ * least 1/8 of the bytes they go to the small-buffer kernel, on a stream
+ * forked from and joined back to `stream` (ZCRC_SMALL=0 in the environment:
+ * never; =2: whenever there is one). */
 int zcrc32_batch_device(const void *const *d_ptrs, const uint64_t *d_lens,
                         const uint32_t *d_seeds_or_null, uint32_t *d_out, size_t n, void *stream);
 
@@ -221,12 +226,17 @@ const char *zcrc_last_error(void);
 const char *zcrc_version(void);
 /* The batched CRC kernel the device entry points launch, as rocprofv3 names it. */
 const char *zcrc_kernel_name(void);
+/* The small-buffer kernel the general-form device entry points launch. */
+const char *zcrc_small_kernel_name(void);
 int zcrc_device_info(int *num_cus, int *arch_major, int *arch_minor);
-/* When enabled, each device launch of the main CRC kernel is bracketed by
- * HIP events recorded on the launch stream; zcrc_profile_read returns the
- * summed kernel milliseconds and launch count since the last reset. */
+/* When enabled, each device launch of the CRC kernels is timed by
+ * timestamps of its own dispatch packet; zcrc_profile_read returns the
+ * summed milliseconds and launch count of the batch kernel since the last
+ * reset, zcrc_profile_read_kind the same for kind 0 (batch kernel) or 1
+ * (small-buffer kernel, zcrc_small_kernel_name()). */
 void zcrc_profile_enable(int on);
 int zcrc_profile_read(double *total_ms, int *launches);
+int zcrc_profile_read_kind(int kind, double *total_ms, int *launches);
 void zcrc_profile_reset(void);
 
 #ifdef __cplusplus

@@ -40,7 +40,7 @@ def _seeds(rnd, n):
     return s, torch.tensor(s.view(np.int32), device=DEV)
 
 
-def _oracle(host, base_addr_offsets, lens, seeds):
+def _oracle(host, base_addr_offsets, lens, seeds):  # noqa: D103
     ap = np.array([host.ctypes.data + int(q) for q in base_addr_offsets], dtype=np.uint64)
     return o.crc32_batch(ap, np.asarray(lens, dtype=np.uint64), seeds, nthreads=8)
 
@@ -113,3 +113,117 @@ def test_config4_golden_through_host_batch(golden):
     got = z.crc32_batch(bufs)
     np.testing.assert_array_equal(np.asarray(got, dtype=np.uint32), cfg["cfg4"])
     assert int((L <= SMALL_MAX).sum()) > 0 and int((L > SMALL_MAX).sum()) > 0
+
+
+def _device_batch(rnd, lens, max_gap=40):
+    offs, pos = [], rnd.randrange(16)
+    for L in lens:
+        offs.append(pos)
+        pos += L + rnd.randrange(max_gap)
+    mem = torch.randint(0, 256, (pos + 64,), dtype=torch.uint8, device=DEV)
+    ptrs = torch.tensor([mem.data_ptr() + q for q in offs], dtype=torch.int64, device=DEV)
+    return mem, offs, ptrs, torch.tensor(lens, dtype=torch.int64, device=DEV)
+
+
+@pytest.mark.parametrize("small", ["1", "0", "2"])
+@pytest.mark.parametrize("shape", ["mixed", "all_small", "all_large", "sorted"])
+def test_device_split_plan(shape, small, monkeypatch):
+    """zcrc32_batch_device above kFusedMaxN buffers: the split plan sends the
+    small ones to the small kernel and the rest, compacted, to the batch
+    kernel (results written back through the original index), with and
+    without seeds.  ZCRC_SMALL=1: split only when small buffers carry >= 1/8
+    of the bytes (all_small); 2: whenever there is one; 0: never."""
+    monkeypatch.setenv("ZCRC_SMALL", small)
+    rnd = random.Random(zlib.crc32(shape.encode()))
+    n = {"mixed": 20_000, "all_small": 50_000, "all_large": 9_000, "sorted": 12_000}[shape]
+    if shape == "all_large":
+        lens = [rnd.randint(SMALL_MAX + 1, 200_000) for _ in range(n)]
+    elif shape == "all_small":
+        lens = [rnd.choice(LENGTHS[:-2]) for _ in range(n)]
+    else:
+        lens = [rnd.choice([rnd.choice(LENGTHS), rnd.randint(0, SMALL_MAX), rnd.randint(SMALL_MAX, 400_000)])
+                for _ in range(n)]
+        if shape == "sorted":  # long runs of small buffers, then the large ones
+            lens.sort()
+    mem, offs, ptrs, lt = _device_batch(rnd, lens)
+    host = mem.cpu().numpy()
+    seeds_np, seeds = _seeds(rnd, n)
+    got = u32(z.crc32_batch_device(ptrs, lt, seeds=seeds))
+    np.testing.assert_array_equal(got, _oracle(host, offs, lens, seeds_np))
+    got = u32(z.crc32_batch_device(ptrs, lt))
+    np.testing.assert_array_equal(got, _oracle(host, offs, lens, np.zeros(n, np.uint32)))
+    # caller-owned scratch (graph-capturable entry point), same results
+    scratch = torch.empty(z.scratch_bytes(n), dtype=torch.uint8, device=DEV)
+    got = u32(z.crc32_batch_device_ws(ptrs, lt, scratch, seeds=seeds))
+    np.testing.assert_array_equal(got, _oracle(host, offs, lens, seeds_np))
+
+
+def test_config4_golden_replicated_through_split_plan(golden):
+    """The config-4 golden sample repeated 9 times (> kFusedMaxN buffers, so
+    the device split plan runs): every CRC equals the reference's."""
+    cfg = golden["cfg"]
+    idx = cfg["cfg4_idx"].astype(np.int64)
+    L = cfg["cfg4_len"].astype(np.int64)
+    offs = np.zeros(len(L), dtype=np.int64)
+    offs[1:] = np.cumsum(L + 3)[:-1]
+    size = int(offs[-1] + L[-1] + 16)
+    reps = 9
+    mem = torch.empty(size * reps, dtype=torch.uint8, device=DEV)
+    ptrs1 = mem.data_ptr() + 1 + torch.tensor(offs, device=DEV)
+    lens1 = torch.tensor(L, device=DEV)
+    for k in range(len(idx)):
+        z.fill_synthetic(ptrs1[k:k + 1], lens1[k:k + 1], index0=int(idx[k]), seed=o.PAYLOAD_SEED)
+    for r in range(1, reps):
+        mem[r * size:(r + 1) * size].copy_(mem[:size])
+    ptrs = torch.cat([ptrs1 + r * size for r in range(reps)])
+    lens = lens1.repeat(reps)
+    assert len(lens) > 8192
+    got = u32(z.crc32_batch_device(ptrs, lens))
+    np.testing.assert_array_equal(got, np.tile(cfg["cfg4"], reps))
+
+
+def test_split_plan_graph_capture_replays():
+    """The split path (plan, batch kernel, small kernel on the forked stream,
+    join) captured in a HIP graph and replayed after lengths and bytes change
+    in place, so the small/large partition differs on every replay."""
+    rnd = random.Random(17)
+    n, cap = 12_000, 20_000
+    mem = torch.zeros(n * cap, dtype=torch.uint8, device=DEV)
+    ptrs = mem.data_ptr() + torch.arange(n, dtype=torch.int64, device=DEV) * cap
+    lens = torch.zeros(n, dtype=torch.int64, device=DEV)
+    out_a = torch.empty(n, dtype=torch.int32, device=DEV)
+    out_b = torch.empty(n, dtype=torch.int32, device=DEV)
+    scratch = torch.empty(z.scratch_bytes(n), dtype=torch.uint8, device=DEV)
+    z.crc32_batch_device(ptrs, lens, out=out_a)  # warm-up outside capture
+    z.crc32_batch_device_ws(ptrs, lens, scratch, out=out_b)
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        z.crc32_batch_device(ptrs, lens, out=out_a)
+        z.crc32_batch_device_ws(ptrs, lens, scratch, out=out_b)
+    for rep in range(3):
+        ln = [rnd.choice([0, rnd.randint(1, SMALL_MAX), rnd.randint(SMALL_MAX, cap)]) for _ in range(n)]
+        lens.copy_(torch.tensor(ln, dtype=torch.int64))
+        mem.copy_(torch.randint(0, 256, (n * cap,), dtype=torch.uint8, device=DEV))
+        g.replay()
+        torch.cuda.synchronize()
+        host = mem.cpu().numpy()
+        exp = _oracle(host, np.arange(n, dtype=np.uint64) * cap, ln, np.zeros(n, dtype=np.uint32))
+        np.testing.assert_array_equal(u32(out_a), exp, err_msg=f"batch_device replay {rep}")
+        np.testing.assert_array_equal(u32(out_b), exp, err_msg=f"batch_device_ws replay {rep}")
+
+
+def test_split_plan_profiles_both_kernels():
+    """zcrc_profile separates the two kernels: a mixed device batch above
+    kFusedMaxN times one batch-kernel and one small-kernel launch."""
+    rnd = random.Random(3)
+    lens = [rnd.choice([100, 5000, 50_000]) for _ in range(10_000)]
+    mem, offs, ptrs, lt = _device_batch(rnd, lens)
+    z.crc32_batch_device(ptrs, lt)
+    torch.cuda.synchronize()
+    with z.profile() as prof:
+        z.crc32_batch_device(ptrs, lt)
+        torch.cuda.synchronize()
+    assert prof.launches == 1 and prof.small_launches == 1
+    assert prof.total_ms > 0 and prof.small_ms > 0
+    assert "crc32_small_kernel" in z.small_kernel_name()

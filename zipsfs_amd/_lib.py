@@ -48,9 +48,11 @@ _SIGNATURES = {
     "zcrc_last_error": (ctypes.c_char_p, []),
     "zcrc_version": (ctypes.c_char_p, []),
     "zcrc_kernel_name": (ctypes.c_char_p, []),
+    "zcrc_small_kernel_name": (ctypes.c_char_p, []),
     "zcrc_device_info": (_c_int, [ctypes.POINTER(_c_int)] * 3),
     "zcrc_profile_enable": (None, [_c_int]),
     "zcrc_profile_read": (_c_int, [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(_c_int)]),
+    "zcrc_profile_read_kind": (_c_int, [_c_int, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(_c_int)]),
     "zcrc_profile_reset": (None, []),
 }
 

@@ -349,7 +349,9 @@ def fill_synthetic(ptrs, lens, index0: int = 0, index_step: int = 1, seed: int =
 
 
 class profile:
-    """Context manager: HIP-event timing of the main CRC kernel launches."""
+    """Context manager: dispatch-packet timing of the CRC kernel launches
+    (total_ms/launches: batch kernel; small_ms/small_launches: small-buffer
+    kernel)."""
 
     def __enter__(self):
         lib().zcrc_profile_reset()
@@ -360,9 +362,12 @@ class profile:
         lib().zcrc_profile_enable(0)
         ms = ctypes.c_double(0)
         cnt = ctypes.c_int(0)
-        check(lib().zcrc_profile_read(ctypes.byref(ms), ctypes.byref(cnt)), "zcrc_profile_read")
-        self.total_ms = float(ms.value)
+        check(lib().zcrc_profile_read_kind(0, ctypes.byref(ms), ctypes.byref(cnt)), "zcrc_profile_read_kind")
+        self.total_ms = float(ms.value)  # batch kernel
         self.launches = int(cnt.value)
+        check(lib().zcrc_profile_read_kind(1, ctypes.byref(ms), ctypes.byref(cnt)), "zcrc_profile_read_kind")
+        self.small_ms = float(ms.value)  # small-buffer kernel
+        self.small_launches = int(cnt.value)
         return False
 
 
@@ -387,6 +392,11 @@ def version() -> str:
 def kernel_name() -> str:
     """The batched CRC kernel the device entry points launch (rocprofv3 name)."""
     return lib().zcrc_kernel_name().decode()
+
+
+def small_kernel_name() -> str:
+    """The small-buffer kernel as rocprofv3 names it (zcrc_small_kernel.h)."""
+    return lib().zcrc_small_kernel_name().decode()
 
 
 def kernel_source_hash() -> str:

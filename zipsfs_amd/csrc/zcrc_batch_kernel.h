@@ -388,7 +388,7 @@ __device__ void split_accumulate(const BatchArgs &a, uint64_t i, uint64_t n, uin
 // the window that starts at walk position k0.
 struct PieceWindow {
   uint64_t i, b0, b1, p;
-  uint32_t s;
+  uint32_t s, o;  // o: result index (split plan: oidx[i])
 };
 
 template <bool kStrided>
@@ -401,6 +401,7 @@ __device__ __forceinline__ void load_window(const BatchView<kStrided> &bv, uint6
   w.b1 = bv.prefix(w.i + 1);
   w.p = reinterpret_cast<uint64_t>(bv.ptr(w.i));
   w.s = bv.seed(w.i);
+  if (!kStrided && bv.a.oidx) w.o = bv.a.oidx[w.i];
 }
 
 // Per-wave rotated visiting order.  Pieces are independent, and the rotation
@@ -439,7 +440,7 @@ __device__ __forceinline__ uint64_t process_range(const BatchArgs &args, const B
   uint64_t done = 0;
   if (kPrio && band) __builtin_amdgcn_s_setprio(3);
 
-  PieceWindow win{0, 0, 0, 0, 0};  // kWin: the current window
+  PieceWindow win{0, 0, 0, 0, 0, 0};  // kWin: the current window
   for (uint64_t k = 0; k < npieces; k++) {
     uint64_t i, b0, b1;
     if (kWin && !kStrided) {
@@ -467,18 +468,21 @@ __device__ __forceinline__ uint64_t process_range(const BatchArgs &args, const B
     }
     uint32_t seed;
     const uint8_t *bptr;
+    uint64_t oi = i;  // result index: i, or the buffer's index before the split plan compacted the batch
     if (kWin && !kStrided) {
       seed = (uint32_t)__builtin_amdgcn_readlane((int)win.s, (int)(k & 63u));
       bptr = reinterpret_cast<const uint8_t *>(rdlane64(win.p, (uint32_t)(k & 63u)));
+      if (args.oidx) oi = (uint32_t)__builtin_amdgcn_readlane((int)win.o, (int)(k & 63u));
     } else {
       seed = uni32(bv.seed(i));
       bptr = reinterpret_cast<const uint8_t *>(uni64(reinterpret_cast<uint64_t>(bv.ptr(i))));
+      if (!kStrided && args.oidx) oi = uni32(args.oidx[i]);
     }
 
     if (n < 4) {  // tiny buffer: bytewise with the standard table (never split)
       uint32_t r = ~seed;
       for (uint32_t p = 0; p < (uint32_t)n; p++) r = (r >> 8) ^ tab->stdtab[(r ^ bptr[p]) & 0xFFu];
-      if (lane == 0) args.out[i] = ~r;
+      if (lane == 0) args.out[oi] = ~r;
       continue;
     }
 
@@ -589,14 +593,14 @@ __device__ __forceinline__ uint64_t process_range(const BatchArgs &args, const B
     if (kStamp) r = uni32(r), *t_tail += __builtin_amdgcn_s_memrealtime() - tt0;  // diagnostic: padding MCT
 
     if (whole) {
-      if (lane == 0) args.out[i] = ~r;
+      if (lane == 0) args.out[oi] = ~r;
     } else {
       const uint64_t d = n - rel_hi;  // bytes after this piece, multiple of kSplitGrain
       uint32_t contrib = d ? shift_bytes(tab, r, d) : (r ^ 0xFFFFFFFFu);
       if (kFused) {
         if (lane == 0) split_accumulate(args, i, n, rel_lo, rel_hi, contrib);
       } else if (lane == 0) {
-        atomicXor(args.out + i, contrib);
+        atomicXor(args.out + oi, contrib);
       }
     }
   }
@@ -607,6 +611,16 @@ template <bool kStrided, uint32_t kD = kDepth, int kAblate = 0, bool kRotate = t
           int kPrio = 1, int kAux = kLoadNt, bool kFused = false, bool kWin = kWindowed>
 __global__ __launch_bounds__(kThreads) void crc32_batch_kernel(BatchArgs args) {
   __shared__ __attribute__((aligned(16))) uint32_t s_lds[kLdsBytes / 4];
+  if (!kStrided && args.n_dev) {  // split plan: its count, and its compacted lists if it split
+    args.n = uni64(args.n_dev[0]);
+    if (uni64(args.n_dev[2])) {
+      args.ptrs = args.ptrs_split;
+      args.seeds = args.seeds_split;
+    } else {
+      args.oidx = nullptr;
+    }
+    if (args.n == 0) return;  // every workgroup: no barrier is skipped
+  }
   const TableBlob *tab = args.tab;
   const uint64_t t_entry = kStamp ? __builtin_amdgcn_s_memrealtime() : 0;
 

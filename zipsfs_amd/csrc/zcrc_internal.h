@@ -63,6 +63,14 @@ struct BatchArgs {
   const uint64_t *lens;
   uint64_t *acc;
   uint32_t *done;
+  // split plan (launch_plan_split): n_dev[0] is the batch's count (n is only
+  // an upper bound; nullptr -> n).  When the plan split the batch
+  // (n_dev[2] != 0) the kernel reads ptrs_split/seeds_split and writes buffer
+  // i's result to out[oidx[i]]; otherwise ptrs/seeds and out[i].
+  const uint64_t *n_dev;
+  const uint32_t *oidx;
+  const uint8_t *const *ptrs_split;
+  const uint32_t *seeds_split;
 };
 
 // Small-buffer kernel (zcrc_small_kernel.h): whole buffers of at most
@@ -118,6 +126,30 @@ inline uint64_t plan_tiles(uint64_t n) { return n == 0 ? 1 : (n + kPlanTile - 1)
 const char *product_kernel_name();
 hipError_t launch_plan(const uint64_t *d_lens, uint64_t n, uint64_t *d_prefix, uint64_t *d_tile_sum,
                        uint32_t *d_out, uint32_t *d_ctr, hipStream_t stream);
+
+// Split plan (device batches of more than kFusedMaxN buffers).  When buffers
+// of at most kSmallMax bytes carry enough of the bytes (zcrc_kernels.hip),
+// they are listed for the small-buffer kernel (sidx, count counts[1]) and the
+// others compacted, in order, into a batch for the batch kernel (ptrs_c,
+// seeds_c, prefix_c, original index oidx, count counts[0]); counts[2] = 1.
+// Otherwise prefix_c is the plain prefix of all n buffers, counts = {n, 0,
+// 0}.  out[] of the batch kernel's buffers is zeroed.  force: split whenever
+// there is a small buffer.  Scratch layout: SplitScratch (zcrc_runtime.hip).
+struct SplitPlan {
+  const uint8_t *const *ptrs;
+  const uint64_t *lens;
+  const uint32_t *seeds;  // nullable
+  uint64_t n;
+  uint64_t *tile_sum;     // 3 words per tile: large bytes, small bytes, packed counts
+  uint64_t *prefix_c;     // n + 1
+  const uint8_t **ptrs_c;
+  uint32_t *seeds_c;      // written when seeds != nullptr
+  uint32_t *oidx, *sidx, *out;
+  uint64_t *counts;       // [0] n_large, [1] n_small, [2] split
+  uint32_t force;
+  uint32_t *ctr;          // the batch kernel's work counter (zeroed)
+};
+hipError_t launch_plan_split(const SplitPlan &p, hipStream_t stream);
 
 }  // namespace zcrc
 

@@ -115,6 +115,142 @@ __global__ __launch_bounds__(1024) void plan_one_tile(const uint64_t *lens, uint
   if (threadIdx.x == 0) prefix[n] = tot;
 }
 
+// ------------------------------------------------------------ split plan
+// Two passes like plan_tile_sums/plan_tile_scan.  Per tile: bytes of the
+// buffers above kSmallMax, bytes of those at or below it, and both counts
+// packed (low half: above, high half: at or below).  The scan decides for the
+// whole launch (every workgroup reads all tile sums, so all decide alike):
+// split when small buffers carry at least 1/kSplitShare of the bytes (or
+// p.force and there is any); otherwise it writes the plain prefix of all
+// buffers, as plan_tile_scan does, and an empty small list.  Order is kept in
+// both lists.
+
+constexpr uint64_t kSplitShare = 8;
+
+__global__ __launch_bounds__(1024) void plan_split_sums(SplitPlan p) {
+  __shared__ uint64_t s_w[16][3];
+  const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+  const uint64_t base = (uint64_t)blockIdx.x * kPlanTile;
+  uint64_t bl = 0, bs = 0, cnt = 0;
+#pragma unroll
+  for (uint32_t k = 0; k < kPlanPerThread; k++) {
+    const uint64_t idx = base + (uint64_t)k * blockDim.x + threadIdx.x;
+    if (idx < p.n) {
+      const uint64_t L = p.lens[idx];
+      if (L > kSmallMax) bl += L, cnt += 1;
+      else bs += L, cnt += 1ull << 32;
+    }
+  }
+  // sums only (no scan): one butterfly per wave, then the 16 wave totals
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1)
+    bl += __shfl_xor(bl, d, 64), bs += __shfl_xor(bs, d, 64), cnt += __shfl_xor(cnt, d, 64);
+  if (lane == 0) s_w[wv][0] = bl, s_w[wv][1] = bs, s_w[wv][2] = cnt;
+  __syncthreads();
+  if (threadIdx.x < 3) {
+    uint64_t t = 0;
+    for (uint32_t w = 0; w < 16; w++) t += s_w[w][threadIdx.x];
+    p.tile_sum[3 * blockIdx.x + threadIdx.x] = t;
+  }
+}
+
+// Thread t of a tile owns its buffers 8t .. 8t+7 (one block scan per
+// quantity: a lane-contiguous layout with a wave scan per k cost 16 dependent
+// 64-bit shuffle scans per thread and measured 30 us on config 4, against 12
+// for plan_tile_scan).  Without a split only the byte prefix is scanned.
+__global__ __launch_bounds__(1024) void plan_split_scan(SplitPlan p) {
+  __shared__ uint64_t s_b[16], s_c[16];
+  __shared__ uint64_t s_off[2];
+  __shared__ uint32_t s_mode;
+  if (blockIdx.x == 0 && threadIdx.x == 0) *p.ctr = 0u;  // the CRC kernel's work counter
+  if (threadIdx.x == 0) {
+    // one thread sums the tile words, 8 tiles' loads in flight at a time
+    const uint32_t tiles = gridDim.x;
+    uint64_t pl = 0, ps = 0, pc = 0, al = 0, as = 0, ac = 0;  // previous tiles, all tiles
+    for (uint32_t b0 = 0; b0 < tiles; b0 += 8) {
+      uint64_t w[8][3];
+#pragma unroll
+      for (uint32_t k = 0; k < 8; k++)
+#pragma unroll
+        for (uint32_t f = 0; f < 3; f++) w[k][f] = b0 + k < tiles ? p.tile_sum[3 * (b0 + k) + f] : 0;
+#pragma unroll
+      for (uint32_t k = 0; k < 8; k++) {
+        al += w[k][0], as += w[k][1], ac += w[k][2];
+        if (b0 + k < blockIdx.x) pl += w[k][0], ps += w[k][1], pc += w[k][2];
+      }
+    }
+    {
+      const bool any_small = (ac >> 32) != 0;
+      const uint32_t mode = any_small && (p.force || as * kSplitShare >= al + as);
+      s_mode = mode;
+      s_off[0] = mode ? pl : pl + ps;
+      s_off[1] = pc;
+    }
+  }
+  __syncthreads();
+  const bool split = s_mode != 0;
+  const uint64_t base = (uint64_t)blockIdx.x * kPlanTile + (uint64_t)threadIdx.x * kPlanPerThread;
+  uint64_t v[kPlanPerThread];
+  uint64_t bytes = 0, cnt = 0;
+#pragma unroll
+  for (uint32_t k = 0; k < kPlanPerThread; k++) {
+    const uint64_t idx = base + k;
+    v[k] = idx < p.n ? p.lens[idx] : 0;
+    if (idx < p.n) {
+      const bool large = !split || v[k] > kSmallMax;
+      bytes += large ? v[k] : 0;
+      cnt += large ? 1ull : 1ull << 32;
+    }
+  }
+  uint64_t tb;
+  uint64_t rb = s_off[0] + block_excl_scan(bytes, s_b, &tb);
+  if (!split) {  // the plain prefix (plan_tile_scan's), counts {n, 0, 0}
+#pragma unroll
+    for (uint32_t k = 0; k < kPlanPerThread; k++) {
+      const uint64_t idx = base + k;
+      if (idx >= p.n) break;
+      p.prefix_c[idx] = rb;
+      p.out[idx] = 0u;  // split pieces xor into it
+      rb += v[k];
+      if (idx + 1 == p.n) p.prefix_c[p.n] = rb, p.counts[0] = p.n, p.counts[1] = 0, p.counts[2] = 0;
+    }
+    return;
+  }
+  uint64_t tc;
+  uint64_t rc = s_off[1] + block_excl_scan(cnt, s_c, &tc);
+#pragma unroll
+  for (uint32_t k = 0; k < kPlanPerThread; k++) {
+    const uint64_t idx = base + k;
+    if (idx >= p.n) break;
+    if (v[k] > kSmallMax) {
+      const uint64_t j = rc & 0xFFFFFFFFull;
+      p.prefix_c[j] = rb;
+      p.ptrs_c[j] = p.ptrs[idx];
+      if (p.seeds) p.seeds_c[j] = p.seeds[idx];
+      p.oidx[j] = (uint32_t)idx;
+      p.out[idx] = 0u;
+      rb += v[k];
+      rc += 1;
+    } else {
+      p.sidx[rc >> 32] = (uint32_t)idx;
+      rc += 1ull << 32;
+    }
+    if (idx + 1 == p.n) {  // totals
+      p.prefix_c[rc & 0xFFFFFFFFull] = rb;
+      p.counts[0] = rc & 0xFFFFFFFFull;
+      p.counts[1] = rc >> 32;
+      p.counts[2] = 1;
+    }
+  }
+}
+
+hipError_t launch_plan_split(const SplitPlan &p, hipStream_t stream) {
+  const uint64_t tiles = plan_tiles(p.n);
+  hipLaunchKernelGGL(plan_split_sums, dim3((unsigned)tiles), dim3(1024), 0, stream, p);
+  hipLaunchKernelGGL(plan_split_scan, dim3((unsigned)tiles), dim3(1024), 0, stream, p);
+  return hipGetLastError();
+}
+
 // ------------------------------------------------------------ launchers
 
 hipError_t launch_batch(const BatchArgs &args, bool strided, int num_cus, hipStream_t stream, hipEvent_t t0,

@@ -116,14 +116,18 @@ int device_ctx(DeviceCtx **out) {
 
 std::atomic<int> g_prof_on{0};
 std::mutex g_prof_mu;
-std::vector<std::pair<hipEvent_t, hipEvent_t>> g_prof_pending;
+struct ProfLaunch {
+  hipEvent_t t0, t1;
+  int kind;  // 0: batch kernel, 1: small-buffer kernel
+};
+std::vector<ProfLaunch> g_prof_pending;
 std::vector<hipEvent_t> g_prof_free;  // recycled: no hipEventCreate per launch
-double g_prof_ms = 0.0;
-int g_prof_count = 0;
+double g_prof_ms[2] = {0.0, 0.0};
+int g_prof_count[2] = {0, 0};
 
 // Launch through `fn(t0, t1)`, with dispatch-packet timestamps when profiling.
 template <class F>
-int launch_timed(F fn) {
+int launch_timed(int kind, F fn) {
   hipEvent_t e0 = nullptr, e1 = nullptr;
   const bool prof = g_prof_on.load(std::memory_order_relaxed) != 0;
   if (prof) {
@@ -138,14 +142,14 @@ int launch_timed(F fn) {
   ZCRC_HIP_TRY(fn(e0, e1));
   if (prof) {
     std::lock_guard<std::mutex> lk(g_prof_mu);
-    g_prof_pending.emplace_back(e0, e1);
+    g_prof_pending.push_back({e0, e1, kind});
   }
   return ZCRC_OK;
 }
 
 int launch_main(const BatchArgs &args, bool strided, const DeviceCtx &dc, hipStream_t stream, bool fused = false) {
   return launch_timed(
-      [&](hipEvent_t t0, hipEvent_t t1) { return launch_batch(args, strided, dc.num_cus, stream, t0, t1, fused); });
+      0, [&](hipEvent_t t0, hipEvent_t t1) { return launch_batch(args, strided, dc.num_cus, stream, t0, t1, fused); });
 }
 
 // The small-buffer kernel (zcrc_small_kernel.h) takes whole buffers of at
@@ -161,7 +165,7 @@ int small_lanes(uint64_t mean_len) { return mean_len <= 2048 ? 8 : 16; }
 
 int launch_small_timed(const SmallArgs &args, bool strided, int lanes, const DeviceCtx &dc, hipStream_t stream) {
   return launch_timed(
-      [&](hipEvent_t t0, hipEvent_t t1) { return launch_small(args, strided, lanes, dc.num_cus, stream, t0, t1); });
+      1, [&](hipEvent_t t0, hipEvent_t t1) { return launch_small(args, strided, lanes, dc.num_cus, stream, t0, t1); });
 }
 
 // ------------------------------------------------------------- device batch
@@ -216,6 +220,85 @@ uint64_t dyn_unit_override() {
   return v;
 }
 
+// Device batches of more than kFusedMaxN buffers go through the split plan
+// (launch_plan_split): when buffers of at most kSmallMax bytes carry enough
+// of the bytes, they go to the small-buffer kernel and the rest --
+// compacted, results written back through oidx -- to the batch kernel --
+// queued after it on the same stream (an empty list costs one launch, ~5 us;
+// on a forked stream the small kernel did not overlap the batch kernel on
+// config 4 -- whose dynamic part leaves no tail to fill -- and the fork's
+// event cost ~8 us before the batch kernel: profiles/r02/small_kernel/).
+// Scratch, in bytes:
+struct SplitScratch {
+  size_t counts, prefix, tiles, ptrs, seeds, oidx, sidx, total;
+  explicit SplitScratch(size_t n) {
+    counts = 128;  // [n_large, n_small, split]: in the counter area, off the counter's cache line
+    prefix = kCtrBytes;
+    tiles = prefix + 8 * (n + 1);
+    ptrs = tiles + 24 * plan_tiles(n);
+    seeds = ptrs + 8 * n;
+    oidx = seeds + 4 * n;
+    sidx = oidx + 4 * n;
+    total = sidx + 4 * n;
+  }
+};
+static_assert(kCtrBytes >= 128 + 24, "split counts share the counter area");
+
+bool split_batch(size_t n) { return n > kFusedMaxN && n < (1ull << 31) && small_enabled(); }
+
+// ZCRC_SMALL=2: the split plan splits whenever there is a small buffer (tests)
+bool split_forced() {
+  const char *e = getenv("ZCRC_SMALL");
+  return e && e[0] == '2';
+}
+
+int batch_device_split(const DeviceCtx &dc, const void *const *d_ptrs, const uint64_t *d_lens,
+                       const uint32_t *d_seeds, uint32_t *d_out, size_t n, void *scratch, hipStream_t stream) {
+  uint8_t *b = static_cast<uint8_t *>(scratch);
+  const SplitScratch L(n);
+  SplitPlan p{};
+  p.ptrs = reinterpret_cast<const uint8_t *const *>(d_ptrs);
+  p.lens = d_lens;
+  p.seeds = d_seeds;
+  p.n = n;
+  p.tile_sum = reinterpret_cast<uint64_t *>(b + L.tiles);
+  p.prefix_c = reinterpret_cast<uint64_t *>(b + L.prefix);
+  p.ptrs_c = reinterpret_cast<const uint8_t **>(b + L.ptrs);
+  p.seeds_c = reinterpret_cast<uint32_t *>(b + L.seeds);
+  p.oidx = reinterpret_cast<uint32_t *>(b + L.oidx);
+  p.sidx = reinterpret_cast<uint32_t *>(b + L.sidx);
+  p.out = d_out;
+  p.counts = reinterpret_cast<uint64_t *>(b + L.counts);
+  p.ctr = reinterpret_cast<uint32_t *>(b);
+  p.force = split_forced();
+  BatchArgs a{};
+  a.ptrs = p.ptrs;
+  a.seeds = d_seeds;
+  a.ptrs_split = p.ptrs_c;
+  a.seeds_split = d_seeds ? p.seeds_c : nullptr;
+  a.prefix = p.prefix_c;
+  a.out = d_out;
+  a.n = n;
+  a.n_dev = p.counts;
+  a.oidx = p.oidx;
+  a.tab = dc.d_tab;
+  a.ctr = p.ctr;
+  a.dyn_shift = kDynShift;
+  a.dyn_unit = dyn_unit_override();
+  SmallArgs sa{};
+  sa.ptrs = p.ptrs;
+  sa.lens = d_lens;
+  sa.sidx = p.sidx;
+  sa.seeds = d_seeds;
+  sa.out = d_out;
+  sa.n = n;
+  sa.n_dev = p.counts + 1;
+  sa.tab = dc.d_tab;
+  ZCRC_HIP_TRY(launch_plan_split(p, stream));
+  const int rc = launch_main(a, false, dc, stream);
+  return rc ? rc : launch_small_timed(sa, false, 16, dc, stream);
+}
+
 int batch_device_ws(const void *const *d_ptrs, const uint64_t *d_lens, const uint32_t *d_seeds,
                     uint32_t *d_out, size_t n, void *scratch, size_t scratch_bytes, hipStream_t stream) {
   if (n == 0) return ZCRC_OK;
@@ -224,6 +307,7 @@ int batch_device_ws(const void *const *d_ptrs, const uint64_t *d_lens, const uin
   DeviceCtx *dc = nullptr;
   int rc = device_ctx(&dc);
   if (rc) return rc;
+  if (split_batch(n)) return batch_device_split(*dc, d_ptrs, d_lens, d_seeds, d_out, n, scratch, stream);
   // scratch: work counter (zeroed by the plan; own kCtrBytes area) |
   // prefix[n+1] | tile sums.  The counter must not share a cache line with
   // the prefix, which every wave reads while claims hammer the counter.
@@ -942,6 +1026,8 @@ const char *zcrc_version(void) { return "zcrc 0.2 (gfx950, braided slice-by-4, L
 
 const char *zcrc_kernel_name(void) { return product_kernel_name(); }
 
+const char *zcrc_small_kernel_name(void) { return small_kernel_name(16); }
+
 int zcrc32_checked(const void *data, size_t n_bytes, uint32_t crc, uint32_t *out_crc) {
   if (!out_crc) return fail(ZCRC_ERR_ARG, "null out_crc");
   if (n_bytes && !data) return fail(ZCRC_ERR_ARG, "null data");
@@ -997,7 +1083,10 @@ int zcrc32_batch(const void *const *ptrs, const size_t *lens, const uint32_t *se
   return batch_host(ptrs, lens, seeds_or_null, out, n);
 }
 
-size_t zcrc32_batch_device_scratch_bytes(size_t n) { return 8 * (n + 1) + 8 * zcrc::plan_tiles(n) + zcrc::kCtrBytes; }
+size_t zcrc32_batch_device_scratch_bytes(size_t n) {
+  const size_t plain = 8 * (n + 1) + 8 * zcrc::plan_tiles(n) + zcrc::kCtrBytes;
+  return n > zcrc::kFusedMaxN ? std::max(plain, zcrc::SplitScratch(n).total) : plain;
+}
 
 int zcrc32_batch_device_ws(const void *const *d_ptrs, const uint64_t *d_lens, const uint32_t *d_seeds_or_null,
                            uint32_t *d_out, size_t n, void *d_scratch, size_t scratch_bytes, void *stream) {
@@ -1350,32 +1439,35 @@ int zcrc_fill_synthetic(const uint64_t *d_ptrs, const uint64_t *d_lens, size_t n
 
 void zcrc_profile_enable(int on) { g_prof_on.store(on ? 1 : 0); }
 
-int zcrc_profile_read(double *total_ms, int *launches) {
+int zcrc_profile_read_kind(int kind, double *total_ms, int *launches) {
+  if (kind < 0 || kind > 1) return fail(ZCRC_ERR_ARG, "profile kind: 0 batch kernel, 1 small-buffer kernel");
   std::lock_guard<std::mutex> lk(g_prof_mu);
   for (auto &p : g_prof_pending) {
-    hipError_t e = hipEventSynchronize(p.second);
+    hipError_t e = hipEventSynchronize(p.t1);
     if (e != hipSuccess) return fail(ZCRC_ERR_HIP, std::string("profile sync: ") + hipGetErrorString(e));
     float ms = 0.f;
-    e = hipEventElapsedTime(&ms, p.first, p.second);
+    e = hipEventElapsedTime(&ms, p.t0, p.t1);
     if (e != hipSuccess) return fail(ZCRC_ERR_HIP, std::string("profile elapsed: ") + hipGetErrorString(e));
-    g_prof_ms += ms;
-    g_prof_count++;
-    g_prof_free.push_back(p.first);
-    g_prof_free.push_back(p.second);
+    g_prof_ms[p.kind] += ms;
+    g_prof_count[p.kind]++;
+    g_prof_free.push_back(p.t0);
+    g_prof_free.push_back(p.t1);
   }
   g_prof_pending.clear();
-  if (total_ms) *total_ms = g_prof_ms;
-  if (launches) *launches = g_prof_count;
+  if (total_ms) *total_ms = g_prof_ms[kind];
+  if (launches) *launches = g_prof_count[kind];
   return ZCRC_OK;
 }
+
+int zcrc_profile_read(double *total_ms, int *launches) { return zcrc_profile_read_kind(0, total_ms, launches); }
 
 void zcrc_profile_reset(void) {
   double ms;
   int c;
   (void)zcrc_profile_read(&ms, &c);
   std::lock_guard<std::mutex> lk(g_prof_mu);
-  g_prof_ms = 0.0;
-  g_prof_count = 0;
+  g_prof_ms[0] = g_prof_ms[1] = 0.0;
+  g_prof_count[0] = g_prof_count[1] = 0;
 }
 
 }  // extern "C"
