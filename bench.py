@@ -32,7 +32,6 @@ sys.path.insert(0, ROOT)
 
 GiB = float(1 << 30)
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec, /opt/skills/guides/MI355X_MICROARCH.md
-SMALL_MAX = 8192  # zcrc_internal.h kSmallMax: the split plan's small-buffer bound
 PAYLOAD_SEED = 0xC0FFEE
 METRIC = "CRC32 GiB/s device-resident (batched chunks) and % of HBM3E read peak"
 
@@ -401,17 +400,11 @@ def main() -> None:
         torch.cuda.synchronize()
         glob = result["global"].cpu().numpy().view(np.uint32)
         parity = golden_check(cfg, glob) if rank == 0 else None
-        # bytes per step each CRC kernel reads: above kFusedMaxN buffers the
-        # split plan gives those of <= SMALL_MAX bytes to the small kernel
-        # when they carry >= 1/8 of the bytes (zcrc_kernels.hip, kSplitShare;
-        # ZCRC_SMALL=2: whenever there is one, 0: never)
-        lens0 = wl.batches[0][1]
-        small = lens0[lens0 <= SMALL_MAX]
-        small_b = int(small.sum().item())
-        mode = os.environ.get("ZCRC_SMALL", "1")
-        split = (prof.small_launches > 0 and len(small) > 0 and mode != "0"
-                 and (mode == "2" or small_b * 8 >= wl.bytes_local))
-        small_b = small_b if split else 0
+        # the device path runs in one batch-kernel launch per step (the split
+        # plan's small list, when it splits, runs inside it: zcrc_kernels.hip);
+        # launches of the separate small kernel (strided/host paths) are
+        # reported beside it
+        small_b = 0
         res = {"wl_desc": wl.desc, "n_local": wl.n_local, "bytes_local": wl.bytes_local, "elapsed": elapsed,
                "bytes_all": bytes_all, "avg_kernel_ms": prof.total_ms / max(prof.launches, 1),
                "launches": prof.launches, "parity": parity, "bytes_main": wl.bytes_local - small_b,

@@ -213,17 +213,28 @@ def test_split_plan_graph_capture_replays():
         np.testing.assert_array_equal(u32(out_b), exp, err_msg=f"batch_device_ws replay {rep}")
 
 
-def test_split_plan_profiles_both_kernels():
-    """zcrc_profile separates the two kernels: a mixed device batch above
-    kFusedMaxN times one batch-kernel and one small-kernel launch."""
+def test_profile_kinds_and_one_launch_split():
+    """zcrc_profile separates the kernels: the strided path of small buffers
+    times one small-kernel launch; a split device batch (small list inside
+    the batch kernel's launch) times one batch-kernel launch and no other."""
     rnd = random.Random(3)
-    lens = [rnd.choice([100, 5000, 50_000]) for _ in range(10_000)]
-    mem, offs, ptrs, lt = _device_batch(rnd, lens)
+    mem = torch.randint(0, 256, (4096 * 1000,), dtype=torch.uint8, device=DEV)
+    lens = [rnd.choice([100, 3000, 50_000]) for _ in range(10_000)]
+    mem2, offs, ptrs, lt = _device_batch(rnd, lens)
+    z.crc32_batch_strided(mem, 4096, 4096, 1000)
     z.crc32_batch_device(ptrs, lt)
     torch.cuda.synchronize()
     with z.profile() as prof:
-        z.crc32_batch_device(ptrs, lt)
+        z.crc32_batch_strided(mem, 4096, 4096, 1000)
         torch.cuda.synchronize()
-    assert prof.launches == 1 and prof.small_launches == 1
-    assert prof.total_ms > 0 and prof.small_ms > 0
+    assert (prof.launches, prof.small_launches) == (0, 1) and prof.small_ms > 0
+    os_env = dict(ZCRC_SMALL="2")
+    with pytest.MonkeyPatch.context() as mp:
+        for k, v in os_env.items():
+            mp.setenv(k, v)
+        with z.profile() as prof:
+            got = z.crc32_batch_device(ptrs, lt)
+            torch.cuda.synchronize()
+    assert (prof.launches, prof.small_launches) == (1, 0)
+    np.testing.assert_array_equal(u32(got), _oracle(mem2.cpu().numpy(), offs, lens, np.zeros(len(lens), np.uint32)))
     assert "crc32_small_kernel" in z.small_kernel_name()

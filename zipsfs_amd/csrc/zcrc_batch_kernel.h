@@ -607,19 +607,44 @@ __device__ __forceinline__ uint64_t process_range(const BatchArgs &args, const B
   return npieces;
 }
 
+// zcrc_small_kernel.h (included at the end of this header)
+template <bool kStrided, int G, int kD>
+__device__ __forceinline__ void small_body(const SmallArgs &a, uint32_t *s_lds, uint64_t n, uint32_t blk,
+                                           uint32_t nblk);
+
 template <bool kStrided, uint32_t kD = kDepth, int kAblate = 0, bool kRotate = true, bool kStamp = false,
           int kPrio = 1, int kAux = kLoadNt, bool kFused = false, bool kWin = kWindowed>
 __global__ __launch_bounds__(kThreads) void crc32_batch_kernel(BatchArgs args) {
   __shared__ __attribute__((aligned(16))) uint32_t s_lds[kLdsBytes / 4];
-  if (!kStrided && args.n_dev) {  // split plan: its count, and its compacted lists if it split
-    args.n = uni64(args.n_dev[0]);
+  uint32_t grid = gridDim.x;  // the batch's workgroups
+  if (!kStrided && !kFused && args.n_dev) {
+    // split plan: its counts; when it split, the top n_dev[4] workgroups take
+    // the small list (zcrc_small_kernel.h, own LDS table) and the rest the
+    // compacted batch -- both in this one launch
     if (uni64(args.n_dev[2])) {
+      const uint32_t nsm = (uint32_t)uni64(args.n_dev[4]);
+      if (blockIdx.x + nsm >= gridDim.x) {
+        SmallArgs sa{};
+        sa.ptrs = args.ptrs;
+        sa.lens = args.lens;
+        sa.sidx = args.sidx;
+        sa.seeds = args.seeds;
+        sa.out = args.out;
+        sa.tab = args.tab;
+        const uint64_t ns = uni64(args.n_dev[1]);
+        const uint32_t blk = blockIdx.x - (gridDim.x - nsm);
+        if (uni64(args.n_dev[3]) == 8) small_body<false, 8, 4>(sa, s_lds, ns, blk, nsm);
+        else small_body<false, 16, 8>(sa, s_lds, ns, blk, nsm);
+        return;  // uniform per workgroup: no barrier is skipped
+      }
+      grid -= nsm;
       args.ptrs = args.ptrs_split;
       args.seeds = args.seeds_split;
     } else {
       args.oidx = nullptr;
     }
-    if (args.n == 0) return;  // every workgroup: no barrier is skipped
+    args.n = uni64(args.n_dev[0]);
+    if (args.n == 0) return;
   }
   const TableBlob *tab = args.tab;
   const uint64_t t_entry = kStamp ? __builtin_amdgcn_s_memrealtime() : 0;
@@ -674,7 +699,7 @@ __global__ __launch_bounds__(kThreads) void crc32_batch_kernel(BatchArgs args) {
   }
   BatchView<kStrided> bv(args, kFused ? lds_pre : nullptr);
   const uint64_t total = bv.total();
-  const uint64_t max_waves = (uint64_t)gridDim.x * kWaves;
+  const uint64_t max_waves = (uint64_t)grid * kWaves;
   const uint64_t min_range = args.min_range ? args.min_range : kMinRange;
   uint64_t want = (total + min_range - 1) / min_range;
   // many small buffers: at least a wave per buffer -- per-buffer latency,
@@ -810,3 +835,6 @@ __global__ __launch_bounds__(kThreads) void crc32_batch_kernel(BatchArgs args) {
 }
 
 }  // namespace zcrc
+
+// the small-buffer body the batch kernel runs for the split plan's small list
+#include "zcrc_small_kernel.h"

@@ -71,14 +71,16 @@ struct BatchArgs {
   const uint32_t *oidx;
   const uint8_t *const *ptrs_split;
   const uint32_t *seeds_split;
+  const uint32_t *sidx;  // the split plan's small list (with lens, ptrs, seeds)
 };
 
 // Small-buffer kernel (zcrc_small_kernel.h): whole buffers of at most
-// kSmallMax bytes, kSmallLanes lanes per buffer.  General form: entry k of
-// the list is buffer j = sidx ? sidx[k] : k with ptrs[j], length lens[j] (or
+// kSmallMax bytes, 8 or 16 lanes per buffer.  General form: entry k of the
+// list is buffer j = sidx ? sidx[k] : k with ptrs[j], length lens[j] (or
 // prefix[j+1] - prefix[j] when lens is null), seeds[j], out[j]; the count is
-// *n_dev when n_dev is set (written by the split plan), else n.  Strided
-// form: buffer k = base + k*stride of length len.
+// n.  Strided form: buffer k = base + k*stride of length len.  The split
+// plan's small list runs inside the batch kernel's launch instead
+// (crc32_batch_kernel, BatchArgs::sidx).
 constexpr uint64_t kSmallMax = 8192;
 struct SmallArgs {
   const uint8_t *const *ptrs;
@@ -134,7 +136,9 @@ hipError_t launch_plan(const uint64_t *d_lens, uint64_t n, uint64_t *d_prefix, u
 // seeds_c, prefix_c, original index oidx, count counts[0]); counts[2] = 1.
 // Otherwise prefix_c is the plain prefix of all n buffers, counts = {n, 0,
 // 0}.  out[] of the batch kernel's buffers is zeroed.  force: split whenever
-// there is a small buffer.  Scratch layout: SplitScratch (zcrc_runtime.hip).
+// there is a small buffer.  A split batch runs in one batch-kernel launch:
+// counts[4] of its `grid` workgroups take the small list.  Scratch layout:
+// SplitScratch (zcrc_runtime.hip).
 struct SplitPlan {
   const uint8_t *const *ptrs;
   const uint64_t *lens;
@@ -145,7 +149,8 @@ struct SplitPlan {
   const uint8_t **ptrs_c;
   uint32_t *seeds_c;      // written when seeds != nullptr
   uint32_t *oidx, *sidx, *out;
-  uint64_t *counts;       // [0] n_large, [1] n_small, [2] split
+  uint64_t *counts;       // [0] n_large, [1] n_small, [2] split, [3] small lanes per buffer, [4] small workgroups
+  uint32_t grid;          // the batch kernel's workgroups
   uint32_t force;
   uint32_t *ctr;          // the batch kernel's work counter (zeroed)
 };

@@ -126,6 +126,7 @@ __global__ __launch_bounds__(1024) void plan_one_tile(const uint64_t *lens, uint
 // both lists.
 
 constexpr uint64_t kSplitShare = 8;
+constexpr uint64_t kSmallCost = 5;  // a small-list byte costs ~2.5 batch-kernel bytes of CU time
 
 __global__ __launch_bounds__(1024) void plan_split_sums(SplitPlan p) {
   __shared__ uint64_t s_w[16][3];
@@ -162,6 +163,8 @@ __global__ __launch_bounds__(1024) void plan_split_scan(SplitPlan p) {
   __shared__ uint64_t s_b[16], s_c[16];
   __shared__ uint64_t s_off[2];
   __shared__ uint32_t s_mode;
+  __shared__ uint64_t s_small_bytes;
+  __shared__ uint32_t s_small_wgs;
   if (blockIdx.x == 0 && threadIdx.x == 0) *p.ctr = 0u;  // the CRC kernel's work counter
   if (threadIdx.x == 0) {
     // one thread sums the tile words, 8 tiles' loads in flight at a time
@@ -183,6 +186,18 @@ __global__ __launch_bounds__(1024) void plan_split_scan(SplitPlan p) {
       const bool any_small = (ac >> 32) != 0;
       const uint32_t mode = any_small && (p.force || as * kSplitShare >= al + as);
       s_mode = mode;
+      s_small_bytes = as;
+      // workgroups for the small list: its share of the bytes, a small-list
+      // byte weighted kSmallCost/2 against a batch-kernel byte (per-CU rates
+      // on config 4's mix: tools/small_batches.py, profiles/r02/small_kernel/)
+      const uint64_t n_large = ac & 0xFFFFFFFFull;
+      uint64_t wgs = p.grid;
+      if (mode && n_large) {
+        const uint64_t ws = kSmallCost * as, wl = 2 * al;
+        wgs = (p.grid * ws + ws + wl - 1) / (ws + wl);
+        wgs = wgs < 1 ? 1 : (wgs > p.grid - 1 ? p.grid - 1 : wgs);
+      }
+      s_small_wgs = (uint32_t)wgs;
       s_off[0] = mode ? pl : pl + ps;
       s_off[1] = pc;
     }
@@ -212,7 +227,7 @@ __global__ __launch_bounds__(1024) void plan_split_scan(SplitPlan p) {
       p.prefix_c[idx] = rb;
       p.out[idx] = 0u;  // split pieces xor into it
       rb += v[k];
-      if (idx + 1 == p.n) p.prefix_c[p.n] = rb, p.counts[0] = p.n, p.counts[1] = 0, p.counts[2] = 0;
+      if (idx + 1 == p.n) p.prefix_c[p.n] = rb, p.counts[0] = p.n, p.counts[1] = 0, p.counts[2] = 0, p.counts[3] = 16;
     }
     return;
   }
@@ -240,6 +255,8 @@ __global__ __launch_bounds__(1024) void plan_split_scan(SplitPlan p) {
       p.counts[0] = rc & 0xFFFFFFFFull;
       p.counts[1] = rc >> 32;
       p.counts[2] = 1;
+      p.counts[3] = s_small_bytes <= 2048 * (rc >> 32) ? 8 : 16;  // mean small length <= 2 KiB: 8 lanes
+      p.counts[4] = s_small_wgs;
     }
   }
 }
@@ -300,7 +317,7 @@ hipError_t launch_small(const SmallArgs &args, bool strided, int lanes, int num_
   return hipGetLastError();
 }
 
-// the general-form small kernel as rocprofv3 names it
+// the general-form small kernels as rocprofv3 names them
 const char *small_kernel_name(int lanes) {
   return lanes == 8 ? "zcrc::crc32_small_kernel<false, 8, 4>" : "zcrc::crc32_small_kernel<false, 16, 8>";
 }

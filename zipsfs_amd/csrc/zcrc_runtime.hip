@@ -222,17 +222,17 @@ uint64_t dyn_unit_override() {
 
 // Device batches of more than kFusedMaxN buffers go through the split plan
 // (launch_plan_split): when buffers of at most kSmallMax bytes carry enough
-// of the bytes, they go to the small-buffer kernel and the rest --
-// compacted, results written back through oidx -- to the batch kernel --
-// queued after it on the same stream (an empty list costs one launch, ~5 us;
-// on a forked stream the small kernel did not overlap the batch kernel on
-// config 4 -- whose dynamic part leaves no tail to fill -- and the fork's
-// event cost ~8 us before the batch kernel: profiles/r02/small_kernel/).
-// Scratch, in bytes:
+// of the bytes, some of the batch kernel's workgroups run the small-buffer
+// body on them and the rest the compacted batch (results written back
+// through oidx) -- one launch either way.  (A separate small-kernel launch
+// cost ~5 us even with an empty list; on a forked stream it did not overlap
+// the batch kernel on config 4, whose dynamic part leaves no tail to fill,
+// and the fork's event cost ~8 us before the batch kernel:
+// profiles/r02/small_kernel/.)  Scratch, in bytes:
 struct SplitScratch {
   size_t counts, prefix, tiles, ptrs, seeds, oidx, sidx, total;
   explicit SplitScratch(size_t n) {
-    counts = 128;  // [n_large, n_small, split]: in the counter area, off the counter's cache line
+    counts = 128;  // [n_large, n_small, split, lanes]: in the counter area, off the counter's cache line
     prefix = kCtrBytes;
     tiles = prefix + 8 * (n + 1);
     ptrs = tiles + 24 * plan_tiles(n);
@@ -242,7 +242,7 @@ struct SplitScratch {
     total = sidx + 4 * n;
   }
 };
-static_assert(kCtrBytes >= 128 + 24, "split counts share the counter area");
+static_assert(kCtrBytes >= 128 + 32, "split counts share the counter area");
 
 bool split_batch(size_t n) { return n > kFusedMaxN && n < (1ull << 31) && small_enabled(); }
 
@@ -271,6 +271,7 @@ int batch_device_split(const DeviceCtx &dc, const void *const *d_ptrs, const uin
   p.counts = reinterpret_cast<uint64_t *>(b + L.counts);
   p.ctr = reinterpret_cast<uint32_t *>(b);
   p.force = split_forced();
+  p.grid = (uint32_t)dc.num_cus;
   BatchArgs a{};
   a.ptrs = p.ptrs;
   a.seeds = d_seeds;
@@ -281,22 +282,14 @@ int batch_device_split(const DeviceCtx &dc, const void *const *d_ptrs, const uin
   a.n = n;
   a.n_dev = p.counts;
   a.oidx = p.oidx;
+  a.lens = d_lens;
+  a.sidx = p.sidx;
   a.tab = dc.d_tab;
   a.ctr = p.ctr;
   a.dyn_shift = kDynShift;
   a.dyn_unit = dyn_unit_override();
-  SmallArgs sa{};
-  sa.ptrs = p.ptrs;
-  sa.lens = d_lens;
-  sa.sidx = p.sidx;
-  sa.seeds = d_seeds;
-  sa.out = d_out;
-  sa.n = n;
-  sa.n_dev = p.counts + 1;
-  sa.tab = dc.d_tab;
   ZCRC_HIP_TRY(launch_plan_split(p, stream));
-  const int rc = launch_main(a, false, dc, stream);
-  return rc ? rc : launch_small_timed(sa, false, 16, dc, stream);
+  return launch_main(a, false, dc, stream);
 }
 
 int batch_device_ws(const void *const *d_ptrs, const uint64_t *d_lens, const uint32_t *d_seeds,

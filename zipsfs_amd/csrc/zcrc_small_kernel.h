@@ -33,19 +33,19 @@ namespace zcrc {
 
 typedef unsigned int small_v4u __attribute__((ext_vector_type(4)));
 
+// Workgroup blk of nblk (the persistent grid, or the batch kernel's
+// workgroups that the split plan gave to the small list).
 template <bool kStrided, int G, int kD>
-__global__ __launch_bounds__(1024) void crc32_small_kernel(SmallArgs a) {
+__device__ __forceinline__ void small_body(const SmallArgs &a, uint32_t *s_lds, uint64_t n, uint32_t blk,
+                                           uint32_t nblk) {
   static_assert(G == 8 || G == 16, "lanes per buffer");
   constexpr int C = 16 / G, NS = 4 * C, LOG_NS = NS == 4 ? 2 : 3, LOG_G = G == 8 ? 3 : 4;
   constexpr uint32_t BPW = 64 / G;  // buffers per wave
-  __shared__ __attribute__((aligned(16))) uint32_t s_lds[kLdsBytes / 4];
   const uint32_t tid = threadIdx.x, lane = tid & 63u, g = lane / G, lg = lane % G;
-  // the count: written by the split plan on the device, or the launch's own
-  const uint64_t n = a.n_dev ? uni64(*a.n_dev) : a.n;
-  const uint64_t waves = (uint64_t)gridDim.x * kWaves;
+  const uint64_t waves = (uint64_t)nblk * kWaves;
   const uint64_t nq = (n + BPW - 1) / BPW;
-  uint64_t q = (uint64_t)blockIdx.x * kWaves + (tid >> 6);
-  if ((uint64_t)blockIdx.x * kWaves >= nq) return;  // whole workgroup idle: skip the table fill
+  uint64_t q = (uint64_t)blk * kWaves + (tid >> 6);
+  if ((uint64_t)blk * kWaves >= nq) return;  // whole workgroup idle: skip the table fill
 
   // descriptor of list entry k (buffer index, start, length, seed)
   auto desc = [&](uint64_t k, uint64_t &j, uint64_t &p, uint64_t &l, uint32_t &sd) {
@@ -150,6 +150,12 @@ __global__ __launch_bounds__(1024) void crc32_small_kernel(SmallArgs a) {
       a.out[j] = ~r;
     }
   }
+}
+
+template <bool kStrided, int G, int kD>
+__global__ __launch_bounds__(1024) void crc32_small_kernel(SmallArgs a) {
+  __shared__ __attribute__((aligned(16))) uint32_t s_lds[kLdsBytes / 4];
+  small_body<kStrided, G, kD>(a, s_lds, a.n, blockIdx.x, gridDim.x);
 }
 
 }  // namespace zcrc
