@@ -82,11 +82,11 @@ int zcrc32_batch(const void *const *ptrs, const size_t *lens, const uint32_t *se
  * NULL; d_out: device array of n results.  Asynchronous on `stream`; its
  * scratch (work counter, length prefix, plan tile sums: 256 + 8*(n+1) +
  * 8*ceil(n/8192) bytes; above 8192 buffers also the split lists, 20*n +
- * 16*ceil(n/8192) more) is a grow-only buffer cached per stream (stream-
+ * 280*ceil(n/8192) more) is a grow-only buffer cached per stream (stream-
  * ordered allocations under graph capture).  Above 8192 buffers the plan may
- * split the batch on the device: when buffers of at most 8 KiB carry at
- * least 1/8 of the bytes they go to the small-buffer kernel, on a stream
- * forked from and joined back to `stream` (ZCRC_SMALL=0 in the environment:
+ * split the batch on the device: when buffers of at most 8 KiB are worth at
+ * least two of the CRC kernel's workgroups, some workgroups of the same
+ * launch run the small-buffer body on them (ZCRC_SMALL=0 in the environment:
  * never; =2: whenever there is one). */
 int zcrc32_batch_device(const void *const *d_ptrs, const uint64_t *d_lens,
                         const uint32_t *d_seeds_or_null, uint32_t *d_out, size_t n, void *stream);

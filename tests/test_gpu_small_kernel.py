@@ -131,8 +131,8 @@ def test_device_split_plan(shape, small, monkeypatch):
     """zcrc32_batch_device above kFusedMaxN buffers: the split plan sends the
     small ones to the small kernel and the rest, compacted, to the batch
     kernel (results written back through the original index), with and
-    without seeds.  ZCRC_SMALL=1: split only when small buffers carry >= 1/8
-    of the bytes (all_small); 2: whenever there is one; 0: never."""
+    without seeds.  ZCRC_SMALL=1: split when the small list is worth two
+    workgroups; 2: whenever there is a small buffer; 0: never."""
     monkeypatch.setenv("ZCRC_SMALL", small)
     rnd = random.Random(zlib.crc32(shape.encode()))
     n = {"mixed": 20_000, "all_small": 50_000, "all_large": 9_000, "sorted": 12_000}[shape]

@@ -130,8 +130,8 @@ hipError_t launch_plan(const uint64_t *d_lens, uint64_t n, uint64_t *d_prefix, u
                        uint32_t *d_out, uint32_t *d_ctr, hipStream_t stream);
 
 // Split plan (device batches of more than kFusedMaxN buffers).  When buffers
-// of at most kSmallMax bytes carry enough of the bytes (zcrc_kernels.hip),
-// they are listed for the small-buffer kernel (sidx, count counts[1]) and the
+// of at most kSmallMax bytes are worth at least two of the batch kernel's
+// workgroups (zcrc_kernels.hip), they are listed for the small-buffer kernel (sidx, count counts[1]) and the
 // others compacted, in order, into a batch for the batch kernel (ptrs_c,
 // seeds_c, prefix_c, original index oidx, count counts[0]); counts[2] = 1.
 // Otherwise prefix_c is the plain prefix of all n buffers, counts = {n, 0,
@@ -144,17 +144,21 @@ struct SplitPlan {
   const uint64_t *lens;
   const uint32_t *seeds;  // nullable
   uint64_t n;
-  uint64_t *tile_sum;     // 3 words per tile: large bytes, small bytes, packed counts
+  uint64_t *tile_sum;     // kTileWords per tile: large bytes, small bytes, packed counts, size-class counts
   uint64_t *prefix_c;     // n + 1
   const uint8_t **ptrs_c;
   uint32_t *seeds_c;      // written when seeds != nullptr
   uint32_t *oidx, *sidx, *out;
   uint64_t *counts;       // [0] n_large, [1] n_small, [2] split, [3] small lanes per buffer, [4] small workgroups
   uint32_t grid;          // the batch kernel's workgroups
+  uint32_t small_cost;    // CU time of a small-list byte, in quarters of a batch-kernel byte
   uint32_t force;
   uint32_t *ctr;          // the batch kernel's work counter (zeroed)
 };
 hipError_t launch_plan_split(const SplitPlan &p, hipStream_t stream);
+constexpr uint32_t kSizeClasses = kSmallMax / 256 + 1;  // small list order: 256-B block count
+constexpr uint32_t kTileWords = 3 + kSizeClasses;
+constexpr uint32_t kSmallCostDefault = 14;  // 3.5 batch-kernel bytes (zcrc_kernels.hip, plan_split_scan)
 
 }  // namespace zcrc
 

@@ -117,20 +117,23 @@ __global__ __launch_bounds__(1024) void plan_one_tile(const uint64_t *lens, uint
 
 // ------------------------------------------------------------ split plan
 // Two passes like plan_tile_sums/plan_tile_scan.  Per tile: bytes of the
-// buffers above kSmallMax, bytes of those at or below it, and both counts
-// packed (low half: above, high half: at or below).  The scan decides for the
-// whole launch (every workgroup reads all tile sums, so all decide alike):
-// split when small buffers carry at least 1/kSplitShare of the bytes (or
-// p.force and there is any); otherwise it writes the plain prefix of all
-// buffers, as plan_tile_scan does, and an empty small list.  Order is kept in
-// both lists.
+// buffers above kSmallMax, bytes of those at or below it, both counts packed
+// (low half: above, high half: at or below) and the small buffers' size-class
+// counts.  The scan decides for the whole launch (every workgroup reads all
+// tile sums, so all decide alike): split when the small list is worth at
+// least two of the batch kernel's workgroups (or p.force and there is any
+// small buffer); otherwise it writes the plain prefix of all buffers, as
+// plan_tile_scan does, and an empty small list.  The large buffers keep
+// their order; the small list is ordered by size class.
 
-constexpr uint64_t kSplitShare = 8;
-constexpr uint64_t kSmallCost = 5;  // a small-list byte costs ~2.5 batch-kernel bytes of CU time
+__device__ __forceinline__ uint32_t size_class(uint64_t len) { return (uint32_t)((len + 255) >> 8); }  // 256-B blocks
 
 __global__ __launch_bounds__(1024) void plan_split_sums(SplitPlan p) {
   __shared__ uint64_t s_w[16][3];
+  __shared__ uint32_t s_cls[kSizeClasses];
   const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+  if (threadIdx.x < kSizeClasses) s_cls[threadIdx.x] = 0;
+  __syncthreads();
   const uint64_t base = (uint64_t)blockIdx.x * kPlanTile;
   uint64_t bl = 0, bs = 0, cnt = 0;
 #pragma unroll
@@ -138,8 +141,12 @@ __global__ __launch_bounds__(1024) void plan_split_sums(SplitPlan p) {
     const uint64_t idx = base + (uint64_t)k * blockDim.x + threadIdx.x;
     if (idx < p.n) {
       const uint64_t L = p.lens[idx];
-      if (L > kSmallMax) bl += L, cnt += 1;
-      else bs += L, cnt += 1ull << 32;
+      if (L > kSmallMax) {
+        bl += L, cnt += 1;
+      } else {
+        bs += L, cnt += 1ull << 32;
+        atomicAdd(&s_cls[size_class(L)], 1u);
+      }
     }
   }
   // sums only (no scan): one butterfly per wave, then the 16 wave totals
@@ -148,10 +155,13 @@ __global__ __launch_bounds__(1024) void plan_split_sums(SplitPlan p) {
     bl += __shfl_xor(bl, d, 64), bs += __shfl_xor(bs, d, 64), cnt += __shfl_xor(cnt, d, 64);
   if (lane == 0) s_w[wv][0] = bl, s_w[wv][1] = bs, s_w[wv][2] = cnt;
   __syncthreads();
+  uint64_t *t = p.tile_sum + (uint64_t)kTileWords * blockIdx.x;
   if (threadIdx.x < 3) {
-    uint64_t t = 0;
-    for (uint32_t w = 0; w < 16; w++) t += s_w[w][threadIdx.x];
-    p.tile_sum[3 * blockIdx.x + threadIdx.x] = t;
+    uint64_t v = 0;
+    for (uint32_t w = 0; w < 16; w++) v += s_w[w][threadIdx.x];
+    t[threadIdx.x] = v;
+  } else if (threadIdx.x < 3 + kSizeClasses) {
+    t[threadIdx.x] = s_cls[threadIdx.x - 3];
   }
 }
 
@@ -165,7 +175,28 @@ __global__ __launch_bounds__(1024) void plan_split_scan(SplitPlan p) {
   __shared__ uint32_t s_mode;
   __shared__ uint64_t s_small_bytes;
   __shared__ uint32_t s_small_wgs;
+  // the small list is ordered by size class (256-B blocks), so that the
+  // buffers a wave of the small body takes together run equal block counts;
+  // within a class and tile the order is the LDS atomics' (any order is
+  // correct: results go out by index)
+  __shared__ uint64_t s_cls_prev[kSizeClasses], s_cls_all[kSizeClasses], s_cls_at[kSizeClasses];
+  __shared__ uint32_t s_cls_cur[kSizeClasses];
   if (blockIdx.x == 0 && threadIdx.x == 0) *p.ctr = 0u;  // the CRC kernel's work counter
+  if (threadIdx.x >= 64 && threadIdx.x < 64 + kSizeClasses) {  // wave 1: class counts
+    const uint32_t c = threadIdx.x - 64;
+    uint64_t prev = 0, all = 0;
+    for (uint32_t b0 = 0; b0 < gridDim.x; b0 += 8) {  // 8 tiles' loads in flight at a time
+      uint64_t v[8];
+#pragma unroll
+      for (uint32_t k = 0; k < 8; k++) v[k] = b0 + k < gridDim.x ? p.tile_sum[(uint64_t)kTileWords * (b0 + k) + 3 + c] : 0;
+#pragma unroll
+      for (uint32_t k = 0; k < 8; k++) {
+        all += v[k];
+        if (b0 + k < blockIdx.x) prev += v[k];
+      }
+    }
+    s_cls_prev[c] = prev, s_cls_all[c] = all, s_cls_cur[c] = 0;
+  }
   if (threadIdx.x == 0) {
     // one thread sums the tile words, 8 tiles' loads in flight at a time
     const uint32_t tiles = gridDim.x;
@@ -175,7 +206,7 @@ __global__ __launch_bounds__(1024) void plan_split_scan(SplitPlan p) {
 #pragma unroll
       for (uint32_t k = 0; k < 8; k++)
 #pragma unroll
-        for (uint32_t f = 0; f < 3; f++) w[k][f] = b0 + k < tiles ? p.tile_sum[3 * (b0 + k) + f] : 0;
+        for (uint32_t f = 0; f < 3; f++) w[k][f] = b0 + k < tiles ? p.tile_sum[kTileWords * (b0 + k) + f] : 0;
 #pragma unroll
       for (uint32_t k = 0; k < 8; k++) {
         al += w[k][0], as += w[k][1], ac += w[k][2];
@@ -183,20 +214,21 @@ __global__ __launch_bounds__(1024) void plan_split_scan(SplitPlan p) {
       }
     }
     {
-      const bool any_small = (ac >> 32) != 0;
-      const uint32_t mode = any_small && (p.force || as * kSplitShare >= al + as);
+      // workgroups for the small list: its share of the CU time, a
+      // small-list byte weighted small_cost/4 against a batch-kernel byte
+      // (config 4 forced to split, one box: weight 1 -> 2.90 ms per step,
+      // 1.5 -> 2.25, 2.5 -> 2.045, 3.5 -> 2.046, 5 -> 2.047, 7 -> 2.049,
+      // against 2.06-2.075 unsplit; profiles/r02/small_kernel/)
+      const uint64_t n_large = ac & 0xFFFFFFFFull, n_small = ac >> 32;
+      const uint64_t ws = p.small_cost * as, wl = 4 * al;
+      uint64_t wgs = p.grid;
+      if (n_large) wgs = ws ? (p.grid * ws + ws + wl - 1) / (ws + wl) : 0;
+      // split when the small list is worth at least two workgroups (a
+      // workgroup given to a handful of small buffers would idle a CU)
+      const uint32_t mode = n_small && (p.force || wgs >= 2);
+      if (n_large) wgs = wgs < 1 ? 1 : (wgs > p.grid - 1 ? p.grid - 1 : wgs);
       s_mode = mode;
       s_small_bytes = as;
-      // workgroups for the small list: its share of the bytes, a small-list
-      // byte weighted kSmallCost/2 against a batch-kernel byte (per-CU rates
-      // on config 4's mix: tools/small_batches.py, profiles/r02/small_kernel/)
-      const uint64_t n_large = ac & 0xFFFFFFFFull;
-      uint64_t wgs = p.grid;
-      if (mode && n_large) {
-        const uint64_t ws = kSmallCost * as, wl = 2 * al;
-        wgs = (p.grid * ws + ws + wl - 1) / (ws + wl);
-        wgs = wgs < 1 ? 1 : (wgs > p.grid - 1 ? p.grid - 1 : wgs);
-      }
       s_small_wgs = (uint32_t)wgs;
       s_off[0] = mode ? pl : pl + ps;
       s_off[1] = pc;
@@ -231,8 +263,12 @@ __global__ __launch_bounds__(1024) void plan_split_scan(SplitPlan p) {
     }
     return;
   }
+  if (threadIdx.x == 0) {  // where this tile's entries of each class start
+    uint64_t at = 0;
+    for (uint32_t c = 0; c < kSizeClasses; c++) s_cls_at[c] = at + s_cls_prev[c], at += s_cls_all[c];
+  }
   uint64_t tc;
-  uint64_t rc = s_off[1] + block_excl_scan(cnt, s_c, &tc);
+  uint64_t rc = s_off[1] + block_excl_scan(cnt, s_c, &tc);  // (its barriers order s_cls_at)
 #pragma unroll
   for (uint32_t k = 0; k < kPlanPerThread; k++) {
     const uint64_t idx = base + k;
@@ -247,7 +283,8 @@ __global__ __launch_bounds__(1024) void plan_split_scan(SplitPlan p) {
       rb += v[k];
       rc += 1;
     } else {
-      p.sidx[rc >> 32] = (uint32_t)idx;
+      const uint32_t c = size_class(v[k]);
+      p.sidx[s_cls_at[c] + atomicAdd(&s_cls_cur[c], 1u)] = (uint32_t)idx;
       rc += 1ull << 32;
     }
     if (idx + 1 == p.n) {  // totals

@@ -235,7 +235,7 @@ struct SplitScratch {
     counts = 128;  // [n_large, n_small, split, lanes]: in the counter area, off the counter's cache line
     prefix = kCtrBytes;
     tiles = prefix + 8 * (n + 1);
-    ptrs = tiles + 24 * plan_tiles(n);
+    ptrs = tiles + 8 * kTileWords * plan_tiles(n);
     seeds = ptrs + 8 * n;
     oidx = seeds + 4 * n;
     sidx = oidx + 4 * n;
@@ -245,6 +245,17 @@ struct SplitScratch {
 static_assert(kCtrBytes >= 128 + 32, "split counts share the counter area");
 
 bool split_batch(size_t n) { return n > kFusedMaxN && n < (1ull << 31) && small_enabled(); }
+
+// Measurement knob: ZCRC_SMALL_COST = CU time of a small-list byte in
+// quarters of a batch-kernel byte (sizes the split's small workgroups)
+uint32_t small_cost() {
+  static const uint32_t v = [] {
+    const char *e = getenv("ZCRC_SMALL_COST");
+    const unsigned long x = e ? strtoul(e, nullptr, 0) : 0;
+    return x ? (uint32_t)x : kSmallCostDefault;
+  }();
+  return v;
+}
 
 // ZCRC_SMALL=2: the split plan splits whenever there is a small buffer (tests)
 bool split_forced() {
@@ -272,6 +283,7 @@ int batch_device_split(const DeviceCtx &dc, const void *const *d_ptrs, const uin
   p.ctr = reinterpret_cast<uint32_t *>(b);
   p.force = split_forced();
   p.grid = (uint32_t)dc.num_cus;
+  p.small_cost = small_cost();
   BatchArgs a{};
   a.ptrs = p.ptrs;
   a.seeds = d_seeds;
