@@ -89,6 +89,7 @@ def mct_apply(t: np.ndarray, r):
 class Tables:
     def __init__(self):
         self.braid = mct(xpow8(1024))
+        self.braid256 = mct(xpow8(256))  # the small-buffer kernel's table
         self.comb = [mct(xinvpow8(b)) for b in (4, 8, 16, 32, 64, 128, 256, 512)]
         self.tshift = [mct(xinvpow8(t)) for t in range(16)]
         std = np.zeros(256, dtype=np.uint32)
@@ -320,3 +321,98 @@ def run_batch(batch: Batch, num_cus: int = 256, dyn_shift: int = K_DYN_SHIFT, un
                 contrib = gf2_mul(xpow8(d), r) if d else r ^ 0xFFFFFFFF
                 out[i] ^= np.uint32(contrib)
     return out
+
+
+# ------------------------------------------------------------ small-buffer kernel
+
+def crc_small_group(mem: np.ndarray, pstart: int, length: int, seed: int, G: int, T: Tables,
+                    extra_blocks: int = 0) -> int:
+    """zcrc_small_kernel.h small_body for one buffer: G lanes, 256-B blocks,
+    C = 16/G chunks per lane, end-aligned; `extra_blocks` leading blocks that
+    load nothing (the wave runs its largest buffer's block count)."""
+    if length < 4:
+        r = (~seed) & 0xFFFFFFFF
+        for p in range(length):
+            r = (r >> 8) ^ int(T.stdtab[(r ^ int(mem[pstart + p])) & 0xFF])
+        return (~r) & 0xFFFFFFFF
+    C = 16 // G
+    astart = pstart & ~15
+    rs = pstart - astart
+    re = rs + length
+    span = (re + 15) & ~15
+    K = (span + 255) >> 8
+    kmax = K + extra_blocks
+    inj = (~seed) & 0xFFFFFFFF
+    lanes = np.arange(G, dtype=np.int64)
+    s = np.zeros((G, 4 * C), dtype=np.uint32)
+    rel0 = span - 256 * kmax + 16 * C * lanes
+    for k in range(kmax):
+        for c in range(C):
+            rel = rel0 + 256 * k + 16 * c
+            data = np.zeros((G, 16), dtype=np.uint8)
+            for l in range(G):
+                if rel[l] >= 0:
+                    data[l] = mem[astart + rel[l]: astart + rel[l] + 16]
+            words = data.view("<u4").astype(np.uint64)
+            edge = (rel >= 0) & ((rel < rs + 4) | (rel + 16 > re))
+            lo = np.clip(rs - rel, -64, 64)
+            hi = np.clip(re - rel, -64, 64)
+            for q in range(4):
+                m = _lowmask(hi - 4 * q) & ~_lowmask(lo - 4 * q) & np.uint64(0xFFFFFFFF)
+                fixed = ((words[:, q] & m) ^ _inj_word(inj, lo - 4 * q)) & np.uint64(0xFFFFFFFF)
+                words[:, q] = np.where(edge, fixed, words[:, q])
+            x = (s[:, 4 * c:4 * c + 4].astype(np.uint64) ^ words).astype(np.uint32)
+            s[:, 4 * c:4 * c + 4] = mct_apply(T.braid256, x)
+    ns = 4 * C
+    v = [s[:, m].copy() for m in range(ns)]
+    t = 0
+    while (1 << t) < ns:  # in-lane tree: combine tables 0.. (4 B, 8 B, 16 B)
+        for m in range(0, ns, 2 << t):
+            v[m] = v[m] ^ mct_apply(T.comb[t], v[m + (1 << t)])
+        t += 1
+    r = v[0]
+    j = 0
+    while (1 << j) < G:  # cross-lane: 16 C B apart, doubling
+        moved = mct_apply(T.comb[t + j], r)
+        d = 1 << j
+        shifted = moved.copy()
+        shifted[:G - d] = moved[d:]
+        r = r ^ shifted
+        j += 1
+    r0 = int(r[0])
+    tpad = span - re
+    if tpad >> 2 & 2:
+        r0 = int(mct_apply(T.comb[1], np.array([r0], dtype=np.uint32))[0])
+    if tpad >> 2 & 1:
+        r0 = int(mct_apply(T.comb[0], np.array([r0], dtype=np.uint32))[0])
+    for _ in range(8 * (tpad & 3)):
+        r0 = times_xinv(r0)
+    return (~r0) & 0xFFFFFFFF
+
+
+K_SMALL_MAX = 8192
+K_SIZE_CLASSES = K_SMALL_MAX // 256 + 1
+K_SMALL_COST = 14  # zcrc_internal.h kSmallCostDefault (quarters of a batch-kernel byte)
+
+
+def split_plan(lens, grid: int = 256, force: bool = False, small_cost: int = K_SMALL_COST):
+    """zcrc_kernels.hip plan_split_scan's decisions and lists: (split,
+    large list in order with its prefix, small list by size class, small
+    workgroups, small lanes)."""
+    lens = [int(x) for x in lens]
+    small = [i for i, L in enumerate(lens) if L <= K_SMALL_MAX]
+    large = [i for i, L in enumerate(lens) if L > K_SMALL_MAX]
+    as_ = sum(lens[i] for i in small)
+    al = sum(lens[i] for i in large)
+    ws, wl = small_cost * as_, 4 * al
+    wgs = grid
+    if large:
+        wgs = (grid * ws + ws + wl - 1) // (ws + wl) if ws else 0
+    split = bool(small) and (force or wgs >= 2)
+    if large:
+        wgs = min(max(wgs, 1), grid - 1)
+    if not split:
+        return dict(split=False, large=list(range(len(lens))), small=[], wgs=wgs, lanes=16)
+    by_class = sorted(small, key=lambda i: (lens[i] + 255) >> 8)  # within a class: any order
+    lanes = 8 if as_ <= 2048 * len(small) else 16
+    return dict(split=True, large=large, small=by_class, wgs=wgs, lanes=lanes)

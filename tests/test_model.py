@@ -153,3 +153,45 @@ def test_device_search_and_first_buffer(shape):
         if 0 < f <= b.n and int(b.prefix[f]) > S:
             f -= 1
         assert first == f, (t, S, lb, first)
+
+
+# ------------------------------------------------------------ small-buffer kernel model
+
+@pytest.mark.parametrize("G", [16, 8])
+def test_small_group_model_matches_oracle(G):
+    """The small body's algebra (256-B blocks on MCT(x^2048), end alignment,
+    in-lane and cross-lane folds, padding undone) reproduces zlib's CRC for
+    every length 0..600 and the block boundaries, at every 16-B misalignment
+    of a sample, with seeds and with extra leading empty blocks."""
+    T = km.tables()
+    rng = np.random.default_rng(G)
+    mem = rng.integers(0, 256, 9000 + 64, dtype=np.uint8)
+    lengths = list(range(0, 601, 7)) + [255, 256, 257, 511, 512, 1023, 1024, 1025, 2048, 4095, 4096, 8191, 8192]
+    for L in lengths:
+        for off in (0, 3, 13):
+            seed = int(rng.integers(0, 2**32)) if L % 3 else 0
+            got = km.crc_small_group(mem, 16 + off, L, seed, G, T, extra_blocks=L % 2)
+            assert got == zlib.crc32(mem[16 + off:16 + off + L].tobytes(), seed), (L, off, G)
+
+
+def test_split_plan_model_lists():
+    """The split plan's lists: the large buffers keep their order, the small
+    list holds every buffer <= 8 KiB once, ordered by 256-B block count; the
+    split rule and the workgroup share follow zcrc_kernels.hip."""
+    rng = np.random.default_rng(5)
+    # config-4-like law: most buffers small, a few MiB-sized ones carry the bytes
+    u = rng.random(20000)
+    lens = np.clip(1024.0 / (1.0 - u * 127.0 / 128.0) ** 2, 1024, 16 << 20).astype(np.int64)
+    p = km.split_plan(lens)
+    assert p["split"] and 1 <= p["wgs"] <= 255
+    assert sorted(p["large"] + p["small"]) == list(range(len(lens)))
+    assert p["large"] == sorted(p["large"]) and all(lens[i] > 8192 for i in p["large"])
+    cls = [(int(lens[i]) + 255) >> 8 for i in p["small"]]
+    assert cls == sorted(cls)
+    # all large: nothing to split; all small: every workgroup takes the small list
+    assert not km.split_plan([70000] * 10000)["split"]
+    q = km.split_plan([1000] * 10000)
+    assert q["split"] and q["wgs"] == 256 and q["lanes"] == 8
+    # a handful of small buffers among large ones is not worth two workgroups
+    few = [1 << 20] * 9000 + [100] * 5
+    assert not km.split_plan(few)["split"] and km.split_plan(few, force=True)["split"]

@@ -784,15 +784,24 @@ int batch_host(const void *const *ptrs, const size_t *lens, const uint32_t *seed
     }
     h_prefix[items] = pos;
     CopyPool::get().run(jobs);
-    // small whole buffers go last, to the small-buffer kernel; the rest keep
-    // their order (a continuation stays item 0) for the batch kernel
+    // small whole buffers go last, to the small-buffer kernel, ordered by
+    // size class (as the device split plan orders them); the rest keep their
+    // order (a continuation stays item 0) for the batch kernel
     uint32_t last_item = (uint32_t)(items - 1);
-    if (n_small && n_small < items) {
+    if (n_small) {
       std::vector<uint64_t> p2(items), l2(items);
       std::vector<uint32_t> s2(items), newpos(items);
-      size_t kl = 0, ks = items - n_small;
+      size_t at[kSizeClasses];
+      {
+        size_t cnt[kSizeClasses] = {};
+        for (size_t k = 0; k < items; k++)
+          if (is_small[k]) cnt[(h_prefix[k + 1] - h_prefix[k] + 255) >> 8]++;
+        size_t run = items - n_small;
+        for (uint32_t c = 0; c < kSizeClasses; c++) at[c] = run, run += cnt[c];
+      }
+      size_t kl = 0;
       for (size_t k = 0; k < items; k++) {
-        const size_t d = is_small[k] ? ks++ : kl++;
+        const size_t d = is_small[k] ? at[(h_prefix[k + 1] - h_prefix[k] + 255) >> 8]++ : kl++;
         newpos[k] = (uint32_t)d;
         p2[d] = h_ptrs[k];
         l2[d] = h_prefix[k + 1] - h_prefix[k];
