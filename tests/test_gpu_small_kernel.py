@@ -238,3 +238,45 @@ def test_profile_kinds_and_one_launch_split():
     assert (prof.launches, prof.small_launches) == (1, 0)
     np.testing.assert_array_equal(u32(got), _oracle(mem2.cpu().numpy(), offs, lens, np.zeros(len(lens), np.uint32)))
     assert "crc32_small_kernel" in z.small_kernel_name()
+
+
+def test_split_batches_overlapping_on_four_streams():
+    """Split-plan launches (> 8192 buffers, small-list share varying from
+    none to all) from four host threads on four streams at once, each
+    queueing six launches without synchronising; per-stream scratch grows
+    under queued work.  Every result vs the oracle."""
+    from concurrent.futures import ThreadPoolExecutor
+    rnd = random.Random(321)
+    total = 64 << 20
+    mem = torch.randint(0, 256, (total,), dtype=torch.uint8, device=DEV)
+    host = mem.cpu().numpy()
+    streams = [torch.cuda.Stream(device=DEV) for _ in range(4)]
+    plans = []
+    for t in range(4):
+        jobs = []
+        for j in range(6):
+            n = rnd.randint(8193, 30000)
+            share = rnd.choice([0.0, 0.3, 0.9, 1.0])
+            ln = [rnd.randint(0, SMALL_MAX) if rnd.random() < share else rnd.randint(SMALL_MAX + 1, 60_000)
+                  for _ in range(n)]
+            offs = [rnd.randrange(0, total - L) for L in ln]
+            jobs.append((offs, ln))
+        plans.append(jobs)
+
+    def work(t):
+        st = streams[t]
+        outs = []
+        with torch.cuda.stream(st):
+            for offs, ln in plans[t]:
+                ptrs = torch.tensor([mem.data_ptr() + q for q in offs], dtype=torch.int64, device=DEV)
+                lt = torch.tensor(ln, dtype=torch.int64, device=DEV)
+                outs.append((z.crc32_batch_device(ptrs, lt), ptrs, lt))
+            st.synchronize()
+        return [u32(o) for o, _, _ in outs]
+
+    with ThreadPoolExecutor(4) as ex:
+        res = list(ex.map(work, range(4)))
+    for t in range(4):
+        for j, ((offs, ln), got) in enumerate(zip(plans[t], res[t])):
+            exp = _oracle(host, offs, ln, np.zeros(len(ln), dtype=np.uint32))
+            np.testing.assert_array_equal(got, exp, err_msg=f"thread {t} job {j}")
