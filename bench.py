@@ -405,7 +405,7 @@ def main() -> None:
         # launches of the separate small kernel (strided/host paths) are
         # reported beside it
         small_b = 0
-        res = {"wl_desc": wl.desc, "n_local": wl.n_local, "bytes_local": wl.bytes_local, "elapsed": elapsed,
+        res = {"wl_desc": wl.desc, "n_local": wl.n_local, "kernel": z.kernel_name_for(wl.n_local), "bytes_local": wl.bytes_local, "elapsed": elapsed,
                "bytes_all": bytes_all, "avg_kernel_ms": prof.total_ms / max(prof.launches, 1),
                "launches": prof.launches, "parity": parity, "bytes_main": wl.bytes_local - small_b,
                "small": None if not prof.small_launches else {
@@ -451,7 +451,7 @@ def main() -> None:
                 "unit": "GiB/s", "ms_per_step": round(r["elapsed"] / max(args.steps, 20) * 1e3, 4),
                 "avg_kernel_ms": round(r["avg_kernel_ms"], 4), "achieved": round(ach, 1),
                 "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None if tr is None else int(tr),
-                "algorithmic_bytes_per_launch": r["bytes_main"], "small_kernel": r["small"],
+                "algorithmic_bytes_per_launch": r["bytes_main"], "kernel": r["kernel"], "small_kernel": r["small"],
                 "parity": r["parity"]}
 
     ms_per_step = elapsed / args.steps * 1e3
@@ -485,7 +485,9 @@ def main() -> None:
                 "workload": wl.desc,
                 "buffers_per_gpu": wl.n_local,
                 "bytes_per_gpu_per_step": wl.bytes_local,
-                "api": "zcrc32_batch_device (plan scan + persistent CRC kernel)" +
+                "api": ("zcrc32_batch_device (one persistent CRC launch, lengths scanned in-kernel)"
+                        if m["kernel"] != z.kernel_name() else
+                        "zcrc32_batch_device (plan scan + persistent CRC kernel)") +
                        (f" + {'RCCL' if args.dist_backend == 'nccl' else 'gloo'} all_gather of uint32 CRCs"
                         if world > 1 else ""),
                 "parallelism": f"round-robin buffer sharding over {world} GPU(s)",
@@ -500,7 +502,7 @@ def main() -> None:
                 "traffic_unit": "bytes per launch (HBM read+write, PMC)",
                 "traffic_source": traffic_src,
                 "algorithmic_bytes_per_launch": m["bytes_main"],
-                "kernel": z.kernel_name(),
+                "kernel": m["kernel"],
                 "kernel_source_hash": z.kernel_source_hash(),
                 "avg_kernel_ms": round(avg_kernel_ms, 4),
                 "launches_timed": m["launches"],

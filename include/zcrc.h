@@ -226,6 +226,10 @@ const char *zcrc_last_error(void);
 const char *zcrc_version(void);
 /* The batched CRC kernel the device entry points launch, as rocprofv3 names it. */
 const char *zcrc_kernel_name(void);
+/* The batched CRC kernel zcrc32_batch_device launches for a batch of n
+ * buffers: the one-launch form for n <= 16 x CUs (ZCRC_FUSED), else the
+ * two-launch form above. */
+const char *zcrc_kernel_name_for(size_t n);
 /* The small-buffer kernel the general-form device entry points launch. */
 const char *zcrc_small_kernel_name(void);
 int zcrc_device_info(int *num_cus, int *arch_major, int *arch_minor);

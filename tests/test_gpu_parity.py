@@ -616,6 +616,37 @@ def test_fused_small_batch_vs_two_launch_path(shape, monkeypatch):
         assert int(ref[i]) == exp, (shape, i, lens_l[i])
 
 
+@pytest.mark.parametrize("n,longest", [(1, 65536), (5, 4), (255, 65536), (256, 65536), (257, 3000),
+                                       (1000, 65536), (4095, 65536), (4096, 65536), (4096, 65537),
+                                       (4097, 65536), (4096, 1 << 20)])
+def test_per_buffer_mode_vs_oracle(n, longest, monkeypatch):
+    """Default eager calls of at most 16 x CUs buffers run one launch; when no
+    buffer exceeds 64 KiB the kernel gives each wave one whole buffer (no
+    prefix scan, no search), otherwise it scans in-kernel (fused form).
+    Ragged lengths 0..longest (tiny ones included), odd addresses, random
+    seeds; vs the oracle and the two-launch path, repeated on one stream."""
+    monkeypatch.delenv("ZCRC_FUSED", raising=False)
+    rnd = random.Random(n * 7 + longest)
+    lens_l = [rnd.choice([0, 1, 2, 3, 4, 5, 17, rnd.randint(0, longest), rnd.randint(0, longest), longest])
+              for _ in range(n)]
+    lens_l[-1] = longest
+    offs = np.zeros(n, dtype=np.int64)
+    offs[1:] = np.cumsum(np.array(lens_l, dtype=np.int64) + 3)[:-1]
+    mem = torch.randint(0, 256, (int(offs[-1] + lens_l[-1] + 64),), dtype=torch.uint8, device=DEV)
+    ptrs = mem.data_ptr() + 1 + torch.tensor(offs, device=DEV)
+    lens = torch.tensor(lens_l, dtype=torch.int64, device=DEV)
+    seeds_np = np.array([rnd.getrandbits(32) for _ in range(n)], dtype=np.uint32)
+    seeds = torch.tensor(seeds_np.view(np.int32), device=DEV)
+    host = mem.cpu().numpy()
+    exp = o.crc32_batch(host.ctypes.data + 1 + offs.astype(np.uint64), np.array(lens_l, dtype=np.uint64),
+                        seeds_np, nthreads=8)
+    scratch = torch.empty(z.crc32.scratch_bytes(n), dtype=torch.uint8, device=DEV)
+    np.testing.assert_array_equal(u32(z.crc32_batch_device_ws(ptrs, lens, scratch, seeds=seeds)), exp)
+    for rep in range(3):
+        np.testing.assert_array_equal(u32(z.crc32_batch_device(ptrs, lens, seeds=seeds)), exp,
+                                      err_msg=f"n={n} launch {rep}")
+
+
 @pytest.mark.parametrize("fused", ["0", "1"])
 def test_fused_scratch_reuse_across_batch_sizes(fused, monkeypatch):
     """Fused launches of different n share one per-stream scratch slot.  A

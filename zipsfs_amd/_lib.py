@@ -48,6 +48,7 @@ _SIGNATURES = {
     "zcrc_last_error": (ctypes.c_char_p, []),
     "zcrc_version": (ctypes.c_char_p, []),
     "zcrc_kernel_name": (ctypes.c_char_p, []),
+    "zcrc_kernel_name_for": (ctypes.c_char_p, [ctypes.c_size_t]),
     "zcrc_small_kernel_name": (ctypes.c_char_p, []),
     "zcrc_device_info": (_c_int, [ctypes.POINTER(_c_int)] * 3),
     "zcrc_profile_enable": (None, [_c_int]),

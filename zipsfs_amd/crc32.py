@@ -394,6 +394,11 @@ def kernel_name() -> str:
     return lib().zcrc_kernel_name().decode()
 
 
+def kernel_name_for(n: int) -> str:
+    """The batched CRC kernel crc32_batch_device launches for n buffers."""
+    return lib().zcrc_kernel_name_for(n).decode()
+
+
 def small_kernel_name() -> str:
     """The small-buffer kernel as rocprofv3 names it (zcrc_small_kernel.h)."""
     return lib().zcrc_small_kernel_name().decode()

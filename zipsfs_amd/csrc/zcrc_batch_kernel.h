@@ -384,6 +384,11 @@ __device__ void split_accumulate(const BatchArgs &a, uint64_t i, uint64_t n, uin
 // Process every piece of the byte range [S0, S1) of the concatenated batch
 // (S0, S1 snapped; `last_range` also takes the trailing empty buffers).
 // Returns the number of pieces.  Wave-uniform; no barriers.
+template <uint32_t kD, int kAblate, int kAux, bool kStamp, bool kPre = false>
+__device__ __forceinline__ uint32_t piece_raw(const uint32_t *s_lds, const uint8_t *bptr, uint64_t rel_lo,
+                                              uint64_t rel_hi, uint32_t seed, uint32_t lane, uint64_t *t_tail,
+                                              const uint4 *pre = nullptr);
+
 // Descriptors of up to 64 pieces of a range walk (kWin), lane k = piece k of
 // the window that starts at walk position k0.
 struct PieceWindow {
@@ -422,10 +427,6 @@ __device__ __forceinline__ uint64_t process_range(const BatchArgs &args, const B
                                                   const uint32_t *s_lds, const TableBlob *tab, uint64_t S0,
                                                   uint64_t S1, bool last_wave, uint32_t salt, uint32_t lane,
                                                   bool band, uint64_t first0, uint64_t lb1, uint64_t *t_tail = nullptr) {
-  // lane constants for the braided lookups
-  const uint32_t lo0 = (lane & 31u) * 4u;
-  const uint32_t o0 = lo0, o1 = lo0 + 128u, o2 = lo0 + 65536u, o3 = lo0 + 65536u + 128u;
-
   // Buffers [i_first, i_end) overlap this wave's range [S0, S1).
   // first0: the first buffer overlapping it, lb1 = lower_bound(S1) (BatchView::range)
   const uint64_t i_first = uni64(first0);
@@ -486,25 +487,87 @@ __device__ __forceinline__ uint64_t process_range(const BatchArgs &args, const B
       continue;
     }
 
-    // ---- one piece: bytes [pstart, pend) of buffer i ----------------------
-    const uint64_t pstart = (uint64_t)bptr + rel_lo;
-    const uint64_t pend = (uint64_t)bptr + rel_hi;
-    const uint64_t astart = uni64(pstart & ~(uint64_t)15);
-    const uint64_t aend = uni64((pend + 15) & ~(uint64_t)15);
-    const uint32_t span = uni32((uint32_t)(aend - astart));  // < 2^31 (kMaxLaunchBytes)
-    const uint32_t K = uni32((span + 1023u) >> 10);
-    const uint32_t tpad = uni32((uint32_t)(aend - pend));
-    const uint32_t inj = uni32((rel_lo == 0) ? ~seed : 0u);
-    // chunk-relative bounds of lane's chunk in block 0: chunk address
-    // c(it) = astart + (span - 1024K) + 1024 it + 16 lane
-    // all chunk-relative offsets fit in int32 because span < 2^31
-    const int32_t c0 = (int32_t)span - 1024 * (int32_t)K + 16 * (int32_t)lane;  // rel. to astart
-    const int32_t rs = (int32_t)uni32((uint32_t)(pstart - astart));
-    const int32_t re = (int32_t)uni32((uint32_t)(pend - astart));
+    const uint32_t r = piece_raw<kD, kAblate, kAux, kStamp>(s_lds, bptr, rel_lo, rel_hi, seed, lane, t_tail);
+    if (whole) {
+      if (lane == 0) args.out[oi] = ~r;
+    } else {
+      const uint64_t d = n - rel_hi;  // bytes after this piece, multiple of kSplitGrain
+      uint32_t contrib = d ? shift_bytes(tab, r, d) : (r ^ 0xFFFFFFFFu);
+      if (kFused) {
+        if (lane == 0) split_accumulate(args, i, n, rel_lo, rel_hi, contrib);
+      } else if (lane == 0) {
+        atomicXor(args.out + oi, contrib);
+      }
+    }
+  }
+  return npieces;
+}
 
-    __amdgpu_buffer_rsrc_t rsrc =
-        __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void *>(astart), (short)0, (int)span, 0x00020000);
-    const uint32_t voff0 = (uint32_t)c0;  // negative wraps -> out of range -> zeros
+// Geometry of a piece: blocks are aligned to the piece's 16-B-aligned end
+// aend; block `it` of lane l is the chunk astart + (span - 1024 K) + 1024 it +
+// 16 l, addressed through a buffer resource over [astart, aend) (chunks
+// before astart read as zeros).
+struct PieceGeom {
+  __amdgpu_buffer_rsrc_t rsrc;
+  uint32_t voff0, K, tpad;
+  int32_t c0, rs, re;
+};
+
+__device__ __forceinline__ PieceGeom piece_geom(const uint8_t *bptr, uint64_t rel_lo, uint64_t rel_hi,
+                                                uint32_t lane) {
+  PieceGeom g;
+  const uint64_t pstart = (uint64_t)bptr + rel_lo;
+  const uint64_t pend = (uint64_t)bptr + rel_hi;
+  const uint64_t astart = uni64(pstart & ~(uint64_t)15);
+  const uint64_t aend = uni64((pend + 15) & ~(uint64_t)15);
+  const uint32_t span = uni32((uint32_t)(aend - astart));  // < 2^31 (kMaxLaunchBytes)
+  g.K = uni32((span + 1023u) >> 10);
+  g.tpad = uni32((uint32_t)(aend - pend));
+  // chunk-relative bounds of lane's chunk in block 0, relative to astart; all
+  // fit in int32 because span < 2^31
+  g.c0 = (int32_t)span - 1024 * (int32_t)g.K + 16 * (int32_t)lane;
+  g.rs = (int32_t)uni32((uint32_t)(pstart - astart));
+  g.re = (int32_t)uni32((uint32_t)(pend - astart));
+  g.rsrc = __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void *>(astart), (short)0, (int)span, 0x00020000);
+  g.voff0 = (uint32_t)g.c0;  // negative wraps -> out of range -> zeros
+  return g;
+}
+
+// The loads of a piece's first two groups (2 kD blocks; blocks past the
+// piece read zeros), issued ahead of piece_raw<..., kPre = true> -- e.g.
+// before the workgroup's LDS fill and barrier.  Issued unconditionally (an
+// empty range when !valid: zeros, no memory access), so that the waits for
+// loads issued before them stay counted ones, not vmcnt(0).
+template <uint32_t kD, int kAux>
+__device__ __forceinline__ void piece_preload(const uint8_t *bptr, uint64_t rel_lo, uint64_t rel_hi, uint32_t lane,
+                                              bool valid, uint4 *pre) {
+  const PieceGeom g = piece_geom(bptr, rel_lo, rel_hi, lane);
+  const __amdgpu_buffer_rsrc_t rsrc = valid ? g.rsrc : __builtin_amdgcn_make_buffer_rsrc(nullptr, (short)0, 0, 0x00020000);
+#pragma unroll
+  for (uint32_t u = 0; u < 2 * kD; u++) {
+    auto v = __builtin_amdgcn_raw_buffer_load_b128(rsrc, g.voff0 + 1024u * u, 0, kAux);
+    pre[u] = make_uint4(v[0], v[1], v[2], v[3]);
+  }
+}
+
+// One piece, bytes [rel_lo, rel_hi) of the buffer at bptr (at least 4 bytes
+// long), as the raw register at the piece end; the seed is injected when the
+// piece starts the buffer.  kPre: groups 0 and 1 were loaded by
+// piece_preload into pre[0 .. 2 kD).  Wave-uniform; no barriers.
+template <uint32_t kD, int kAblate, int kAux, bool kStamp, bool kPre>
+__device__ __forceinline__ uint32_t piece_raw(const uint32_t *s_lds, const uint8_t *bptr, uint64_t rel_lo,
+                                              uint64_t rel_hi, uint32_t seed, uint32_t lane, uint64_t *t_tail,
+                                              const uint4 *pre) {
+  // lane constants for the braided lookups
+  const uint32_t lo0 = (lane & 31u) * 4u;
+  const uint32_t o0 = lo0, o1 = lo0 + 128u, o2 = lo0 + 65536u, o3 = lo0 + 65536u + 128u;
+  {
+    // ---- one piece: bytes [pstart, pend) of the buffer --------------------
+    const PieceGeom geo = piece_geom(bptr, rel_lo, rel_hi, lane);
+    const uint32_t K = geo.K, tpad = geo.tpad, voff0 = geo.voff0;
+    const int32_t c0 = geo.c0, rs = geo.rs, re = geo.re;
+    const __amdgpu_buffer_rsrc_t rsrc = geo.rsrc;
+    const uint32_t inj = uni32((rel_lo == 0) ? ~seed : 0u);
 
     uint32_t s0 = 0, s1 = 0, s2 = 0, s3 = 0;
     // Two register groups of kD blocks: one streams in while the other
@@ -552,8 +615,13 @@ __device__ __forceinline__ uint64_t process_range(const BatchArgs &args, const B
     // (bounds + fix-ups), groups 1..ngroups-2 are plain.  Loop invariant: gb
     // holds group g, loaded; ga is free.
     const uint32_t ngroups = (K + kD - 1) / kD;  // >= 1
-    ZCRC_LOADG(ga, 0u);
-    if (ngroups > 1) ZCRC_LOADG(gb, 1u);
+    if (kPre) {
+#pragma unroll
+      for (uint32_t u = 0; u < kD; u++) ga[u] = pre[u], gb[u] = pre[kD + u];
+    } else {
+      ZCRC_LOADG(ga, 0u);
+      if (ngroups > 1) ZCRC_LOADG(gb, 1u);
+    }
     ZCRC_EDGE(ga, 0u);
     if (ngroups > 1) {
       const uint32_t nplain = ngroups - 2;
@@ -591,20 +659,8 @@ __device__ __forceinline__ uint64_t process_range(const BatchArgs &args, const B
     const uint64_t tt0 = kStamp ? __builtin_amdgcn_s_memrealtime() : 0;
     if (tpad) r = shift_back(s_lds, r, tpad);  // -> register at pend
     if (kStamp) r = uni32(r), *t_tail += __builtin_amdgcn_s_memrealtime() - tt0;  // diagnostic: padding MCT
-
-    if (whole) {
-      if (lane == 0) args.out[oi] = ~r;
-    } else {
-      const uint64_t d = n - rel_hi;  // bytes after this piece, multiple of kSplitGrain
-      uint32_t contrib = d ? shift_bytes(tab, r, d) : (r ^ 0xFFFFFFFFu);
-      if (kFused) {
-        if (lane == 0) split_accumulate(args, i, n, rel_lo, rel_hi, contrib);
-      } else if (lane == 0) {
-        atomicXor(args.out + oi, contrib);
-      }
-    }
+    return r;
   }
-  return npieces;
 }
 
 // zcrc_small_kernel.h (included at the end of this header)
@@ -683,6 +739,60 @@ __global__ __launch_bounds__(kThreads) void crc32_batch_kernel(BatchArgs args) {
       const uint64_t idx = 8u * tid + k;
       v[k] = idx < args.n ? args.lens[idx] : 0;
       sum += v[k];
+    }
+    // Per-buffer mode: no more buffers than waves and none longer than
+    // kPerBufMax.  The two-launch path would then give every wave at most one
+    // range of whole buffers (W = n, no splits); here wave slot s of workgroup
+    // g takes buffer s * grid + g whole -- spread over every CU, with no
+    // prefix, no range search and no plan.  Every workgroup reads all the
+    // lengths, so all of them take the same decision.
+    if (args.n <= (uint64_t)grid * kWaves) {
+      const uint32_t lane = tid & 63u, slot = uni32(tid >> 6);
+      const uint64_t b = (uint64_t)slot * grid + blockIdx.x;
+      uint64_t blen = 0, bp = 0;
+      uint32_t bseed = 0;
+      if (b < args.n) {  // issued before the decision: in flight with the table loads
+        blen = uni64(args.lens[b]);
+        bp = uni64(reinterpret_cast<uint64_t>(args.ptrs[b]));
+        bseed = args.seeds ? uni32(args.seeds[b]) : 0u;
+      }
+      bool big = false;
+#pragma unroll
+      for (uint32_t k = 0; k < 8; k++) big |= v[k] > kPerBufMax;
+      // the buffer's first 2 kD KiB, in flight across the decision, the LDS
+      // fill and the barriers (used only if the mode is taken)
+      const uint8_t *bptr = reinterpret_cast<const uint8_t *>(bp);
+      uint4 pre[2 * kD];
+      piece_preload<kD, kAux>(bptr, 0, blen, lane, b < args.n && blen >= 4 && blen <= kPerBufMax, pre);
+      uint32_t *flags = s_lds + kLdsCombDword;  // 16 words, overwritten by the fill after the second barrier
+      const uint64_t m = __ballot(big);
+      if (lane == 0) flags[slot] = m ? 1u : 0u;
+      __syncthreads();
+      uint32_t any_big = 0;
+#pragma unroll
+      for (int s = 0; s < kWaves; s++) any_big |= flags[s];
+      __syncthreads();  // every wave has read the flags
+      if (!any_big) {
+        if (blockIdx.x >= args.n) return;  // whole workgroup idle (uniform: no barrier is skipped)
+        uint4 *dst = reinterpret_cast<uint4 *>(s_lds);
+#pragma unroll
+        for (int k = 0; k < 8; k++)
+          dst[tid + 1024u * k] = make_uint4(braid_val[k], braid_val[k], braid_val[k], braid_val[k]);
+        uint4 *cdst = reinterpret_cast<uint4 *>(s_lds + kLdsCombDword);
+        cdst[tid] = comb0;
+        cdst[tid + 1024u] = comb1;
+        __syncthreads();
+        if (b >= args.n) return;  // no barrier after this point
+        uint32_t r;
+        if (blen < 4) {  // bytewise with the standard table
+          r = ~bseed;
+          for (uint32_t p = 0; p < (uint32_t)blen; p++) r = (r >> 8) ^ tab->stdtab[(r ^ bptr[p]) & 0xFFu];
+        } else {
+          r = piece_raw<kD, kAblate, kAux, false, true>(s_lds, bptr, 0, blen, bseed, lane, nullptr, pre);
+        }
+        if (lane == 0) args.out[b] = ~r;
+        return;
+      }
     }
     uint64_t tot;
     uint64_t run = block_excl_scan(sum, lds_pre + kFusedMaxN + 8, &tot);

@@ -22,6 +22,7 @@ constexpr uint32_t kLdsCombDword = 32768;      // combine tables start at 128 Ki
 constexpr uint32_t kPlanPerThread = 8;
 constexpr bool kWindowed = true;       // piece descriptors fetched 64 at a time
 constexpr uint64_t kFusedMaxN = 8192;  // one-launch small batches: the kernel scans the lengths itself
+constexpr uint64_t kPerBufMax = kMinRange;  // one-launch batches of buffers up to this: one wave per buffer
 constexpr uint64_t kPlanTile = 1024 * kPlanPerThread;
 // one launch covers at most this many bytes (keeps every piece < 2 GiB)
 constexpr uint64_t kMaxLaunchBytes = 1ull << 42;
@@ -126,6 +127,7 @@ enum ScratchUse { kScratchBatch = 0, kScratchInflateOrder = 1, kScratchFused = 2
 
 inline uint64_t plan_tiles(uint64_t n) { return n == 0 ? 1 : (n + kPlanTile - 1) / kPlanTile; }
 const char *product_kernel_name();
+const char *fused_kernel_name();
 hipError_t launch_plan(const uint64_t *d_lens, uint64_t n, uint64_t *d_prefix, uint64_t *d_tile_sum,
                        uint32_t *d_out, uint32_t *d_ctr, hipStream_t stream);
 

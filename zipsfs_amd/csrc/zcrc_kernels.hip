@@ -354,6 +354,17 @@ hipError_t launch_small(const SmallArgs &args, bool strided, int lanes, int num_
   return hipGetLastError();
 }
 
+// the one-launch form (launch_batch with fused = true)
+const char *fused_kernel_name() {
+  static char name[160];
+  static std::once_flag once;
+  std::call_once(once, [] {
+    snprintf(name, sizeof name, "zcrc::crc32_batch_kernel<false, %uu, 0, true, false, 1, %d, true, %s>", kDepth,
+             kLoadNt, kWindowed ? "true" : "false");
+  });
+  return name;
+}
+
 // the general-form small kernels as rocprofv3 names them
 const char *small_kernel_name(int lanes) {
   return lanes == 8 ? "zcrc::crc32_small_kernel<false, 8, 4>" : "zcrc::crc32_small_kernel<false, 16, 8>";

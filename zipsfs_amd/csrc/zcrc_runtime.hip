@@ -333,18 +333,22 @@ int batch_device_ws(const void *const *d_ptrs, const uint64_t *d_lens, const uin
   return launch_main(a, false, *dc, stream);
 }
 
-// Small eager batches (n <= kFusedMaxN) in ONE launch: the kernel scans the
-// lengths itself (no plan kernel, no queue gap between two dependent
-// launches).  Its scratch -- claim counter, finished-wave counter, split-piece
-// accumulators, prefix -- is zero-filled when allocated and the kernel leaves
-// the counters and accumulators zero, so it has its own per-stream slot
-// (the two-launch path leaves its counter nonzero).  Opt-in (ZCRC_FUSED=1):
-// on config 2 the in-kernel scan made the CRC launch 7.7 us longer than the
-// plan launch it replaced, 3,713-3,724 vs 3,810-3,839 GiB/s per step on one
-// box (profiles/r02/fused_vs_two_launch_c2.jsonl).
-bool fused_enabled() {
+// Small eager batches in ONE launch: the kernel scans the lengths itself (no
+// plan kernel, no queue gap between two dependent launches).  Its scratch --
+// claim counter, finished-wave counter, split-piece accumulators, prefix -- is
+// zero-filled when allocated and the kernel leaves the counters and
+// accumulators zero, so it has its own per-stream slot (the two-launch path
+// leaves its counter nonzero).  Default for batches of at most one buffer per
+// wave (n <= 16 x CUs), where the kernel takes the per-buffer mode when no
+// buffer exceeds kPerBufMax (one wave per whole buffer: no scan, no search).
+// ZCRC_FUSED=1 takes it for every n <= kFusedMaxN, ZCRC_FUSED=0 never (the
+// in-kernel scan alone made config 2's CRC launch 7.7 us longer than the plan
+// launch it replaced: profiles/r02/fused_vs_two_launch_c2.jsonl).
+bool fused_enabled(size_t n, int num_cus) {
   const char *e = getenv("ZCRC_FUSED");  // read per call: tests switch it
-  return e && e[0] == '1';
+  if (e && e[0] == '0') return false;
+  if (e && e[0] == '1') return n <= kFusedMaxN;
+  return n <= (size_t)num_cus * kWaves && n <= kFusedMaxN;
 }
 
 // Fixed layout, whatever n: counters | acc[kFusedMaxN] | prefix[kFusedMaxN+1].
@@ -1040,6 +1044,12 @@ const char *zcrc_version(void) { return "zcrc 0.2 (gfx950, braided slice-by-4, L
 
 const char *zcrc_kernel_name(void) { return product_kernel_name(); }
 
+const char *zcrc_kernel_name_for(size_t n) {
+  DeviceCtx *dc = nullptr;
+  if (device_ctx(&dc) == ZCRC_OK && fused_enabled(n, dc->num_cus)) return fused_kernel_name();
+  return product_kernel_name();
+}
+
 const char *zcrc_small_kernel_name(void) { return small_kernel_name(16); }
 
 int zcrc32_checked(const void *data, size_t n_bytes, uint32_t crc, uint32_t *out_crc) {
@@ -1130,7 +1140,9 @@ int zcrc32_batch_device(const void *const *d_ptrs, const uint64_t *d_lens, const
   void *scratch = nullptr;
   size_t have = 0;
   std::unique_lock<std::mutex> lk;
-  if (n <= kFusedMaxN && fused_enabled()) {
+  DeviceCtx *dc = nullptr;
+  if (const int rc = device_ctx(&dc)) return rc;
+  if (fused_enabled(n, dc->num_cus)) {
     const int rc = stream_scratch(st, kScratchFused, fused_scratch_bytes(), &scratch, &have, &lk);
     if (rc) return rc;
     return batch_device_fused(d_ptrs, d_lens, d_seeds_or_null, d_out, n, scratch, st);
