@@ -77,8 +77,11 @@ class Workload:
             lens_all = zipf_lens(100000)
             mine = np.arange(rank, 100000, world)
             L = lens_all[mine]
+            # buffer start alignment (16 B; ZCRC_BENCH_ALIGN: a measurement knob for
+            # the HBM-traffic experiments of DESIGN.md section 7b)
+            al = int(os.environ.get("ZCRC_BENCH_ALIGN", "16"))
             offs = np.zeros(len(L), dtype=np.int64)
-            offs[1:] = np.cumsum((L + 15) // 16 * 16)[:-1]
+            offs[1:] = np.cumsum((L + al - 1) // al * al)[:-1]
             mem = torch.empty(int(offs[-1] + L[-1] + 16), dtype=torch.uint8, device=dev)
             ptrs = mem.data_ptr() + torch.tensor(offs, device=dev)
             lens = torch.tensor(L, device=dev)
