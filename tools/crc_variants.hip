@@ -11,7 +11,7 @@
 
 #include "../zipsfs_amd/csrc/zcrc_batch_kernel.h"
 #include "../zipsfs_amd/csrc/zcrc_tables.h"
-#include "kernel_v1.h"
+#include "ab/kernel_v1.h"  // generated: tools/ab/make_v1.sh (make -C tools crc_variants)
 
 #define CHECK(x)                                                                               \
   do {                                                                                         \
