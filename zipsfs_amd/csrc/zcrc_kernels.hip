@@ -136,11 +136,19 @@ __global__ __launch_bounds__(1024) void plan_split_sums(SplitPlan p) {
   __syncthreads();
   const uint64_t base = (uint64_t)blockIdx.x * kPlanTile;
   uint64_t bl = 0, bs = 0, cnt = 0;
+  // all loads first: with the LDS atomics between them the compiler issued
+  // them one round trip at a time
+  uint64_t lv[kPlanPerThread];
+#pragma unroll
+  for (uint32_t k = 0; k < kPlanPerThread; k++) {
+    const uint64_t idx = base + (uint64_t)k * blockDim.x + threadIdx.x;
+    lv[k] = idx < p.n ? p.lens[idx] : 0;
+  }
 #pragma unroll
   for (uint32_t k = 0; k < kPlanPerThread; k++) {
     const uint64_t idx = base + (uint64_t)k * blockDim.x + threadIdx.x;
     if (idx < p.n) {
-      const uint64_t L = p.lens[idx];
+      const uint64_t L = lv[k];
       if (L > kSmallMax) {
         bl += L, cnt += 1;
       } else {
@@ -182,6 +190,22 @@ __global__ __launch_bounds__(1024) void plan_split_scan(SplitPlan p) {
   __shared__ uint64_t s_cls_prev[kSizeClasses], s_cls_all[kSizeClasses], s_cls_at[kSizeClasses];
   __shared__ uint32_t s_cls_cur[kSizeClasses];
   if (blockIdx.x == 0 && threadIdx.x == 0) *p.ctr = 0u;  // the CRC kernel's work counter
+  // this thread's lengths, pointers and seeds, loaded before the tile sums
+  // are read (the scatter below stores between its uses, so loads left in
+  // its loop were issued one round trip at a time: 25 us per launch on
+  // config 4)
+  const uint64_t base = (uint64_t)blockIdx.x * kPlanTile + (uint64_t)threadIdx.x * kPlanPerThread;
+  uint64_t v[kPlanPerThread];
+  const uint8_t *pv[kPlanPerThread];
+  uint32_t sv[kPlanPerThread];
+#pragma unroll
+  for (uint32_t k = 0; k < kPlanPerThread; k++) {
+    const uint64_t idx = base + k;
+    const bool in = idx < p.n;
+    v[k] = in ? p.lens[idx] : 0;
+    pv[k] = in ? p.ptrs[idx] : nullptr;
+    sv[k] = in && p.seeds ? p.seeds[idx] : 0u;
+  }
   if (threadIdx.x >= 64 && threadIdx.x < 64 + kSizeClasses) {  // wave 1: class counts
     const uint32_t c = threadIdx.x - 64;
     uint64_t prev = 0, all = 0;
@@ -236,13 +260,10 @@ __global__ __launch_bounds__(1024) void plan_split_scan(SplitPlan p) {
   }
   __syncthreads();
   const bool split = s_mode != 0;
-  const uint64_t base = (uint64_t)blockIdx.x * kPlanTile + (uint64_t)threadIdx.x * kPlanPerThread;
-  uint64_t v[kPlanPerThread];
   uint64_t bytes = 0, cnt = 0;
 #pragma unroll
   for (uint32_t k = 0; k < kPlanPerThread; k++) {
     const uint64_t idx = base + k;
-    v[k] = idx < p.n ? p.lens[idx] : 0;
     if (idx < p.n) {
       const bool large = !split || v[k] > kSmallMax;
       bytes += large ? v[k] : 0;
@@ -276,8 +297,8 @@ __global__ __launch_bounds__(1024) void plan_split_scan(SplitPlan p) {
     if (v[k] > kSmallMax) {
       const uint64_t j = rc & 0xFFFFFFFFull;
       p.prefix_c[j] = rb;
-      p.ptrs_c[j] = p.ptrs[idx];
-      if (p.seeds) p.seeds_c[j] = p.seeds[idx];
+      p.ptrs_c[j] = pv[k];
+      if (p.seeds) p.seeds_c[j] = sv[k];
       p.oidx[j] = (uint32_t)idx;
       p.out[idx] = 0u;
       rb += v[k];
