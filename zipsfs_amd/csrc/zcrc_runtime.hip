@@ -220,6 +220,16 @@ uint64_t dyn_unit_override() {
   return v;
 }
 
+// Measurement knob: ZCRC_DYN_SHIFT overrides the dynamic part's share
+// (total >> shift; 0 = none; unset = by mean buffer size, kDynAuto).
+uint32_t dyn_shift_setting() {
+  static const uint32_t v = [] {
+    const char *e = getenv("ZCRC_DYN_SHIFT");
+    return e ? (uint32_t)strtoul(e, nullptr, 0) : kDynShift;
+  }();
+  return v;
+}
+
 // Device batches of more than kFusedMaxN buffers go through the split plan
 // (launch_plan_split): when buffers of at most kSmallMax bytes carry enough
 // of the bytes, some of the batch kernel's workgroups run the small-buffer
@@ -298,7 +308,7 @@ int batch_device_split(const DeviceCtx &dc, const void *const *d_ptrs, const uin
   a.sidx = p.sidx;
   a.tab = dc.d_tab;
   a.ctr = p.ctr;
-  a.dyn_shift = kDynShift;
+  a.dyn_shift = dyn_shift_setting();
   a.dyn_unit = dyn_unit_override();
   ZCRC_HIP_TRY(launch_plan_split(p, stream));
   return launch_main(a, false, dc, stream);
@@ -328,7 +338,7 @@ int batch_device_ws(const void *const *d_ptrs, const uint64_t *d_lens, const uin
   a.n = n;
   a.tab = dc->d_tab;
   a.ctr = d_ctr;
-  a.dyn_shift = kDynShift;
+  a.dyn_shift = dyn_shift_setting();
   a.dyn_unit = dyn_unit_override();
   return launch_main(a, false, *dc, stream);
 }
@@ -371,7 +381,7 @@ int batch_device_fused(const void *const *d_ptrs, const uint64_t *d_lens, const 
   a.tab = dc->d_tab;
   a.ctr = reinterpret_cast<uint32_t *>(sc);
   a.done = reinterpret_cast<uint32_t *>(sc) + 1;
-  a.dyn_shift = kDynShift;
+  a.dyn_shift = dyn_shift_setting();
   a.acc = reinterpret_cast<uint64_t *>(sc + kCtrBytes);
   a.prefix = a.acc + kFusedMaxN;
   return launch_main(a, false, *dc, stream, true);
@@ -1186,7 +1196,7 @@ int zcrc32_batch_device_strided(const void *d_base, uint64_t stride, uint64_t le
     if (d_ctr) {
       ZCRC_HIP_TRY(hipMemsetAsync(d_ctr, 0, 4, st));
       a.ctr = d_ctr;
-      a.dyn_shift = kDynShift;
+      a.dyn_shift = dyn_shift_setting();
     }
     a.base = static_cast<const uint8_t *>(d_base) + first * stride;
     a.stride = stride;
