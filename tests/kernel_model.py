@@ -416,3 +416,24 @@ def split_plan(lens, grid: int = 256, force: bool = False, small_cost: int = K_S
     by_class = sorted(small, key=lambda i: (lens[i] + 255) >> 8)  # within a class: any order
     lanes = 8 if as_ <= 2048 * len(small) else 16
     return dict(split=True, large=large, small=by_class, wgs=wgs, lanes=lanes)
+
+
+# ---------------------------------------------------------------- one launch
+K_PER_BUF_MAX = K_MIN_RANGE  # zcrc_internal.h kPerBufMax
+
+
+def per_buffer_plan(lens, num_cus: int = 256):
+    """The one-launch kernel's per-buffer mode (zcrc_batch_kernel.h,
+    crc32_batch_kernel, kFused): taken when n <= 16 x grid and no length
+    exceeds kPerBufMax; then wave slot s of workgroup g checksums buffer
+    s * grid + g whole.  Returns {buffer: (g, s)} or None (in-kernel scan)."""
+    n = len(lens)
+    if n > K_WAVES * num_cus or any(L > K_PER_BUF_MAX for L in lens):
+        return None
+    out = {}
+    for g in range(num_cus):
+        for s in range(K_WAVES):
+            b = s * num_cus + g
+            if b < n:
+                out[b] = (g, s)
+    return out

@@ -195,3 +195,21 @@ def test_split_plan_model_lists():
     # a handful of small buffers among large ones is not worth two workgroups
     few = [1 << 20] * 9000 + [100] * 5
     assert not km.split_plan(few)["split"] and km.split_plan(few, force=True)["split"]
+
+
+def test_per_buffer_mode_rule_and_mapping():
+    """One-launch batches: the per-buffer mode covers every buffer exactly
+    once, spreads a batch of n < 16 x CUs over all CUs (at most
+    ceil(n / CUs) waves per workgroup), and falls back for a buffer above
+    64 KiB or more buffers than waves."""
+    for n in (1, 5, 255, 256, 257, 1000, 4095, 4096):
+        m = km.per_buffer_plan([65536] * n)
+        assert sorted(m) == list(range(n))
+        per_wg = {}
+        for g, s in m.values():
+            per_wg[g] = per_wg.get(g, 0) + 1
+        assert max(per_wg.values()) == -(-n // 256)
+        assert len(per_wg) == min(n, 256)
+    assert km.per_buffer_plan([65537]) is None
+    assert km.per_buffer_plan([1] * 4097) is None
+    assert km.per_buffer_plan([1] * 4097, num_cus=512) is not None
