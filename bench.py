@@ -75,6 +75,9 @@ class Workload:
             self._strided(n, L, pools=pools, dev=dev)
         elif cfg == 4:
             lens_all = zipf_lens(100000)
+            rnd = int(os.environ.get("ZCRC_BENCH_LEN_ROUND", "0"))  # traffic experiments only:
+            if rnd:                                                  # lengths rounded up (parity then fails)
+                lens_all = (lens_all + rnd - 1) // rnd * rnd
             mine = np.arange(rank, 100000, world)
             L = lens_all[mine]
             # buffer start alignment (16 B; ZCRC_BENCH_ALIGN: a measurement knob for
@@ -137,6 +140,8 @@ def golden_check(cfg: int, glob: np.ndarray) -> str:
         if len(idx) < 256:
             raise SystemExit(f"PARITY: only {len(idx)} config-5 samples fall inside {len(glob)} buffers")
     ok = int((glob[idx] == exp).sum())
+    if ok != len(idx) and cfg == 4 and os.environ.get("ZCRC_BENCH_LEN_ROUND"):
+        return "not checked: ZCRC_BENCH_LEN_ROUND changed the workload (traffic experiment)"
     if ok != len(idx):
         raise SystemExit(f"PARITY FAILURE: {len(idx) - ok} of {len(idx)} sampled CRCs differ from the reference")
     return f"{ok}/{len(idx)} sampled CRCs equal the reference golden vectors"
