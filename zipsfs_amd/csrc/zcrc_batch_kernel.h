@@ -78,7 +78,10 @@ __device__ __forceinline__ uint32_t comb_apply(const uint32_t *lds, int c, uint3
 // cost ~4 us per piece under the stream, 7.6% of a wave's time on config 4
 // (tools/crc_variants padding-MCT stamps).
 __device__ __forceinline__ uint32_t shift_back(const uint32_t *lds, uint32_t r, uint32_t t) {
-  const uint32_t a = t >> 2;
+  const uint32_t a = t >> 2;  // t < 128: combine tables 0..4 are x^-32 .. x^-512 (4 .. 64 bytes)
+  if (a & 16u) r = (uint32_t)__builtin_amdgcn_readfirstlane((int)comb_apply(lds, 4, r));
+  if (a & 8u) r = (uint32_t)__builtin_amdgcn_readfirstlane((int)comb_apply(lds, 3, r));
+  if (a & 4u) r = (uint32_t)__builtin_amdgcn_readfirstlane((int)comb_apply(lds, 2, r));
   if (a & 2u) r = (uint32_t)__builtin_amdgcn_readfirstlane((int)comb_apply(lds, 1, r));
   if (a & 1u) r = (uint32_t)__builtin_amdgcn_readfirstlane((int)comb_apply(lds, 0, r));
   for (uint32_t i = 0; i < 8u * (t & 3u); i++) r = gf2_times_xinv(r);
@@ -520,12 +523,19 @@ __device__ __forceinline__ PieceGeom piece_geom(const uint8_t *bptr, uint64_t re
   const uint64_t pend = (uint64_t)bptr + rel_hi;
   const uint64_t astart = uni64(pstart & ~(uint64_t)15);
   const uint64_t aend = uni64((pend + 15) & ~(uint64_t)15);
+  // The block grid ends at the 128-B line after pend, so that no 1 KiB block
+  // straddles a line: anchored at aend, a piece of arbitrary length had every
+  // block straddle one, fetched by two blocks' loads (config 4 read 1.022x its
+  // payload; 1.001x with every length a 1 KiB multiple: DESIGN.md 7b).
+  // Chunks in [aend, agrid) are out of the resource range: zeros, no fetch.
+  const uint64_t agrid = uni64((pend + 127) & ~(uint64_t)127);
   const uint32_t span = uni32((uint32_t)(aend - astart));  // < 2^31 (kMaxLaunchBytes)
-  g.K = uni32((span + 1023u) >> 10);
-  g.tpad = uni32((uint32_t)(aend - pend));
+  const uint32_t gspan = uni32((uint32_t)(agrid - astart));
+  g.K = uni32((gspan + 1023u) >> 10);
+  g.tpad = uni32((uint32_t)(agrid - pend));  // < 128
   // chunk-relative bounds of lane's chunk in block 0, relative to astart; all
   // fit in int32 because span < 2^31
-  g.c0 = (int32_t)span - 1024 * (int32_t)g.K + 16 * (int32_t)lane;
+  g.c0 = (int32_t)gspan - 1024 * (int32_t)g.K + 16 * (int32_t)lane;
   g.rs = (int32_t)uni32((uint32_t)(pstart - astart));
   g.re = (int32_t)uni32((uint32_t)(pend - astart));
   g.rsrc = __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void *>(astart), (short)0, (int)span, 0x00020000);
