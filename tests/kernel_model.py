@@ -261,10 +261,12 @@ def crc_piece(mem: np.ndarray, pstart: int, pend: int, inj: int, T: Tables) -> i
     lanes = np.arange(64, dtype=np.int64)
     astart = pstart & ~15
     aend = (pend + 15) & ~15
-    span = aend - astart
-    K = (span + 1023) >> 10
-    tpad = aend - pend
-    c0 = span - 1024 * K + 16 * lanes
+    span = aend - astart  # the buffer resource's range: chunks outside read zeros
+    agrid = (pend + 127) & ~127  # the block grid ends at the 128-B line after pend
+    gspan = agrid - astart
+    K = (gspan + 1023) >> 10
+    tpad = agrid - pend
+    c0 = gspan - 1024 * K + 16 * lanes
     rs, re = pstart - astart, pend - astart
     s = np.zeros((64, 4), dtype=np.uint32)
     for it in range(K):
@@ -292,8 +294,8 @@ def crc_piece(mem: np.ndarray, pstart: int, pend: int, inj: int, T: Tables) -> i
         shifted[64 - d:] = moved[64 - d:]
         r = r ^ shifted
     r0 = int(r[0])
-    if tpad:
-        r0 = int(mct_apply(T.tshift[tpad], np.array([r0], dtype=np.uint32))[0])
+    if tpad:  # < 128 (the kernel: combine tables of 4..64 bytes, then x^-1 steps)
+        r0 = gf2_mul(r0, xinvpow8(tpad))
     return r0
 
 
@@ -340,18 +342,19 @@ def crc_small_group(mem: np.ndarray, pstart: int, length: int, seed: int, G: int
     rs = pstart - astart
     re = rs + length
     span = (re + 15) & ~15
-    K = (span + 255) >> 8
+    gspan = ((astart + re + 127) & ~127) - astart  # blocks end at the 128-B line after the buffer
+    K = (gspan + 255) >> 8
     kmax = K + extra_blocks
     inj = (~seed) & 0xFFFFFFFF
     lanes = np.arange(G, dtype=np.int64)
     s = np.zeros((G, 4 * C), dtype=np.uint32)
-    rel0 = span - 256 * kmax + 16 * C * lanes
+    rel0 = gspan - 256 * kmax + 16 * C * lanes
     for k in range(kmax):
         for c in range(C):
             rel = rel0 + 256 * k + 16 * c
             data = np.zeros((G, 16), dtype=np.uint8)
             for l in range(G):
-                if rel[l] >= 0:
+                if 0 <= rel[l] < span:
                     data[l] = mem[astart + rel[l]: astart + rel[l] + 16]
             words = data.view("<u4").astype(np.uint64)
             edge = (rel >= 0) & ((rel < rs + 4) | (rel + 16 > re))
@@ -380,11 +383,10 @@ def crc_small_group(mem: np.ndarray, pstart: int, length: int, seed: int, G: int
         r = r ^ shifted
         j += 1
     r0 = int(r[0])
-    tpad = span - re
-    if tpad >> 2 & 2:
-        r0 = int(mct_apply(T.comb[1], np.array([r0], dtype=np.uint32))[0])
-    if tpad >> 2 & 1:
-        r0 = int(mct_apply(T.comb[0], np.array([r0], dtype=np.uint32))[0])
+    tpad = gspan - re  # < 128: combine tables 4 .. 0 (64 .. 4 bytes)
+    for b in (4, 3, 2, 1, 0):
+        if tpad >> 2 & (1 << b):
+            r0 = int(mct_apply(T.comb[b], np.array([r0], dtype=np.uint32))[0])
     for _ in range(8 * (tpad & 3)):
         r0 = times_xinv(r0)
     return (~r0) & 0xFFFFFFFF
