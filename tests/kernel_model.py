@@ -342,19 +342,18 @@ def crc_small_group(mem: np.ndarray, pstart: int, length: int, seed: int, G: int
     rs = pstart - astart
     re = rs + length
     span = (re + 15) & ~15
-    gspan = ((astart + re + 127) & ~127) - astart  # blocks end at the 128-B line after the buffer
-    K = (gspan + 255) >> 8
+    K = (span + 255) >> 8
     kmax = K + extra_blocks
     inj = (~seed) & 0xFFFFFFFF
     lanes = np.arange(G, dtype=np.int64)
     s = np.zeros((G, 4 * C), dtype=np.uint32)
-    rel0 = gspan - 256 * kmax + 16 * C * lanes
+    rel0 = span - 256 * kmax + 16 * C * lanes
     for k in range(kmax):
         for c in range(C):
             rel = rel0 + 256 * k + 16 * c
             data = np.zeros((G, 16), dtype=np.uint8)
             for l in range(G):
-                if 0 <= rel[l] < span:
+                if rel[l] >= 0:
                     data[l] = mem[astart + rel[l]: astart + rel[l] + 16]
             words = data.view("<u4").astype(np.uint64)
             edge = (rel >= 0) & ((rel < rs + 4) | (rel + 16 > re))
@@ -383,8 +382,8 @@ def crc_small_group(mem: np.ndarray, pstart: int, length: int, seed: int, G: int
         r = r ^ shifted
         j += 1
     r0 = int(r[0])
-    tpad = gspan - re  # < 128: combine tables 4 .. 0 (64 .. 4 bytes)
-    for b in (4, 3, 2, 1, 0):
+    tpad = span - re  # < 16
+    for b in (1, 0):
         if tpad >> 2 & (1 << b):
             r0 = int(mct_apply(T.comb[b], np.array([r0], dtype=np.uint32))[0])
     for _ in range(8 * (tpad & 3)):

@@ -91,17 +91,13 @@ __device__ __forceinline__ void small_body(const SmallArgs &a, uint32_t *s_lds, 
     const bool tiny = len < 4u;  // bytewise below (the 4-byte seed injection needs 4 bytes)
     const uint64_t astart = pstart & ~(uint64_t)15;
     const int32_t rs = (int32_t)(pstart & 15u), re = rs + (int32_t)len, span = (re + 15) & ~15;
-    // blocks end at the 128-B line after the buffer (as in the batch kernel:
-    // a 256-B block anchored at an unaligned end straddles lines that two
-    // blocks' loads fetch); chunks past `span` are not loaded
-    const int32_t gspan = (int32_t)(((astart + (uint64_t)re + 127) & ~(uint64_t)127) - astart);
     const uint32_t inj = ~seed;
-    const uint32_t kq = (active && !tiny) ? (uint32_t)(gspan + 255) >> 8 : 0u;
+    const uint32_t kq = (active && !tiny) ? (uint32_t)(span + 255) >> 8 : 0u;
     const uint32_t kmax = uni32(__reduce_max_sync(0xFFFFFFFFFFFFFFFFull, kq));
     uint32_t s[NS];
 #pragma unroll
     for (int t = 0; t < NS; t++) s[t] = 0u;
-    int32_t rel0 = kq ? gspan - 256 * (int32_t)kmax + 16 * C * (int32_t)lg : -(1 << 30);
+    int32_t rel0 = kq ? span - 256 * (int32_t)kmax + 16 * C * (int32_t)lg : -(1 << 30);
     for (uint32_t k = 0; k < kmax; k += kD) {
       small_v4u d[kD][C];
 #pragma unroll
@@ -110,7 +106,7 @@ __device__ __forceinline__ void small_body(const SmallArgs &a, uint32_t *s_lds, 
         for (int c = 0; c < C; c++) {
           const int32_t rel = rel0 + 256 * b + 16 * c;
           d[b][c] = (small_v4u)(0u);
-          if (k + b < kmax && rel >= 0 && rel < span)
+          if (k + b < kmax && rel >= 0)
             d[b][c] = __builtin_nontemporal_load(reinterpret_cast<const small_v4u *>(astart + (uint32_t)rel));
         }
 #pragma unroll
@@ -139,10 +135,7 @@ __device__ __forceinline__ void small_body(const SmallArgs &a, uint32_t *s_lds, 
     uint32_t r = s[0];
 #pragma unroll
     for (int t = 0; t < LOG_G; t++) r ^= __shfl_down(comb_apply(s_lds, LOG_NS + t, r), 1u << t, 64);
-    const uint32_t tpad = (uint32_t)(gspan - re), a4 = tpad >> 2;  // < 128
-    if (a4 & 16u) r = comb_apply(s_lds, 4, r);
-    if (a4 & 8u) r = comb_apply(s_lds, 3, r);
-    if (a4 & 4u) r = comb_apply(s_lds, 2, r);
+    const uint32_t tpad = (uint32_t)(span - re), a4 = tpad >> 2;
     if (a4 & 2u) r = comb_apply(s_lds, 1, r);
     if (a4 & 1u) r = comb_apply(s_lds, 0, r);
     const uint32_t nbits = 8u * (tpad & 3u);
