@@ -323,6 +323,9 @@ def main() -> None:
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-secondary", action="store_true",
                     help="N=1 config 3: skip the configs 2 and 4 timed after the headline")
+    ap.add_argument("--collective", action="store_true",
+                    help="init the process group and gather the CRCs even at one rank (exercises the "
+                         "RCCL path on a one-GPU box: init_process_group, all_gather on the device)")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="nccl = RCCL over xGMI (default); gloo only to rehearse ranks sharing one GPU")
     ap.add_argument("--cpu-budget-s", type=float, default=12.0)
@@ -353,14 +356,20 @@ def main() -> None:
     gpu = local % max(ndev, 1)
     torch.cuda.set_device(gpu)
     dev = torch.device("cuda", gpu)
-    if world > 1:
+    use_dist = world > 1 or args.collective
+    if use_dist:
+        if world == 1:  # --collective without a launcher: a one-rank group on 127.0.0.1
+            os.environ.setdefault("RANK", "0")
+            os.environ.setdefault("WORLD_SIZE", "1")
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            os.environ.setdefault("MASTER_PORT", str(free_port()))
         if args.dist_backend == "nccl":
             dist.init_process_group("nccl", device_id=dev)
         else:
             dist.init_process_group("gloo")
 
     def barrier():
-        if world > 1:
+        if use_dist:
             if args.dist_backend == "nccl":
                 dist.barrier(device_ids=[gpu])
             else:
@@ -376,7 +385,7 @@ def main() -> None:
         def step(s: int) -> None:
             ptrs, lens = wl.batches[s % len(wl.batches)]
             z.crc32_batch_device(ptrs, lens, out=out)
-            if world > 1:  # the one exchange: all-gather of the 32-bit CRCs
+            if use_dist:  # the one exchange: all-gather of the 32-bit CRCs
                 result["global"] = shard.gather_crcs(out, wl.n_total)
 
         for s in range(warmup):
@@ -392,7 +401,7 @@ def main() -> None:
             t1 = time.perf_counter()
         barrier()
         elapsed = t1 - t0
-        if world > 1:
+        if use_dist:
             rdev = dev if args.dist_backend == "nccl" else torch.device("cpu")
             et = torch.tensor([elapsed], dtype=torch.float64, device=rdev)
             dist.all_reduce(et, op=dist.ReduceOp.MAX)
@@ -406,6 +415,7 @@ def main() -> None:
         # sampled CRCs with the reference-generated golden vectors (data only)
         step(0)
         torch.cuda.synchronize()
+        gathered_on = str(result["global"].device)
         glob = result["global"].cpu().numpy().view(np.uint32)
         parity = golden_check(cfg, glob) if rank == 0 else None
         # the device path runs in one batch-kernel launch per step (the split
@@ -415,7 +425,7 @@ def main() -> None:
         small_b = 0
         res = {"wl_desc": wl.desc, "n_local": wl.n_local, "kernel": z.kernel_name_for(wl.n_local), "bytes_local": wl.bytes_local, "elapsed": elapsed,
                "bytes_all": bytes_all, "avg_kernel_ms": prof.total_ms / max(prof.launches, 1),
-               "launches": prof.launches, "parity": parity, "bytes_main": wl.bytes_local - small_b,
+               "launches": prof.launches, "parity": parity, "gathered_on": gathered_on, "bytes_main": wl.bytes_local - small_b,
                "small": None if not prof.small_launches else {
                    "kernel": z.small_kernel_name(), "launches_timed": prof.small_launches,
                    "avg_kernel_ms": round(prof.small_ms / prof.small_launches, 4),
@@ -497,7 +507,7 @@ def main() -> None:
                         if m["kernel"] != z.kernel_name() else
                         "zcrc32_batch_device (plan scan + persistent CRC kernel)") +
                        (f" + {'RCCL' if args.dist_backend == 'nccl' else 'gloo'} all_gather of uint32 CRCs"
-                        if world > 1 else ""),
+                        if use_dist else ""),
                 "parallelism": f"round-robin buffer sharding over {world} GPU(s)",
             },
             "roofline": {
@@ -518,11 +528,15 @@ def main() -> None:
             },
             "cpu_baseline": cpu,
             "parity": parity,
+            "collective": None if not use_dist else {
+                "backend": "RCCL" if args.dist_backend == "nccl" else "gloo", "ranks": world,
+                "op": "all_gather_into_tensor of the int32 CRCs (zipsfs_amd/shard.py)",
+                "results_on": m["gathered_on"]},
             "secondary": secondary,
             "device": torch.cuda.get_device_name(dev),
         }
         print(json.dumps(line), flush=True)
-    if world > 1:
+    if use_dist:
         dist.destroy_process_group()
 
 

@@ -1,0 +1,63 @@
+"""Config 5 on one MI355X: the per-GPU shard through the
+RCCL path, and two ranks sharing the GPU over gloo.
+
+The 8-GPU run is the driver's; these put every part of the multi-GPU path
+that one GPU can run on hardware:
+* `init_process_group("nccl")` at world size 1, `shard.gather_crcs` through
+  RCCL's all_gather on the device, and the config-5 golden CRCs (generated
+  from the reference's src/cg_crc32.c) checked in global order after it;
+* `bench.py --gpus 2` spawning two fresh ranks (gloo, both on cuda:0) whose
+  gathered vector interleaves rank 0's and rank 1's shards (i mod 2).
+Each runs bench.py in fresh child processes, as the driver does.  The
+reference has no counterpart: one core per entry
+(src/ZIPsFS_preloadfileram.c:243).
+"""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+pytestmark = pytest.mark.gpu
+
+
+def _bench_line(args, env_extra=None, timeout=240):
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    env.update(env_extra or {})
+    p = subprocess.run([sys.executable, "-u", os.path.join(ROOT, "bench.py")] + args, env=env, cwd=ROOT,
+                       capture_output=True, text=True, timeout=timeout)
+    assert p.returncode == 0, f"bench.py {args} exited {p.returncode}\n{p.stdout[-3000:]}\n{p.stderr[-3000:]}"
+    lines = [l for l in p.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, p.stdout[-3000:]
+    return json.loads(lines[0])
+
+
+@pytest.mark.timeout(300)
+def test_config5_shard_through_rccl_at_world_size_1():
+    d = _bench_line(["--config", "5", "--buffers-per-gpu", "32768", "--collective", "--dist-backend", "nccl",
+                     "--steps", "3", "--warmup", "1", "--no-cpu-baseline"])
+    assert d["ranks"] == 1 and d["n_gpus"] == 1
+    assert d["config"]["buffers_per_gpu"] == 32768
+    assert d["config"]["bytes_per_gpu_per_step"] == 32768 << 20
+    c = d["collective"]
+    assert c["backend"] == "RCCL" and c["results_on"].startswith("cuda"), c
+    assert "RCCL all_gather" in d["config"]["api"]
+    # >= 256 config-5 fixtures fall inside the first 32768 global buffers
+    assert d["parity"].startswith("256/256"), d["parity"]
+    assert d["value"] > 1000.0, d["value"]  # GiB/s: the CRC ran on the GPU
+
+
+@pytest.mark.timeout(300)
+def test_two_ranks_spawned_over_gloo_on_one_gpu():
+    d = _bench_line(["--gpus", "2", "--dist-backend", "gloo", "--buffers-per-gpu", "32768",
+                     "--steps", "3", "--warmup", "1"])
+    assert d["ranks"] == 2 and d["n_gpus"] == 1
+    assert d["collective"]["backend"] == "gloo"
+    assert d["config"]["bytes_per_gpu_per_step"] == 32768 << 20
+    # global buffers 0..65535, rank r holding i mod 2 == r: 512 fixtures
+    assert d["parity"].startswith("512/512"), d["parity"]

@@ -183,9 +183,10 @@ def test_config4_golden_replicated_through_split_plan(golden):
 
 
 def test_split_plan_graph_capture_replays():
-    """The split path (plan, batch kernel, small kernel on the forked stream,
-    join) captured in a HIP graph and replayed after lengths and bytes change
-    in place, so the small/large partition differs on every replay."""
+    """The split path (plan launch, then one batch-kernel launch whose top
+    workgroups run the small body on the small list) captured in a HIP graph
+    and replayed after lengths and bytes change in place, so the small/large
+    partition differs on every replay."""
     rnd = random.Random(17)
     n, cap = 12_000, 20_000
     mem = torch.zeros(n * cap, dtype=torch.uint8, device=DEV)
