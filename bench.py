@@ -12,8 +12,10 @@ buffer i lives on rank i mod N, weak scaling).
     python bench.py [--gpus N] [--steps K] [--warmup W] [--config 2|3|4|5]
 
 Prints ONE JSON line on rank 0.  `roofline.achieved` is algorithmic bytes per
-launch (sum of buffer lengths) / average kernel time, the kernel timed with
-HIP events recorded by libzcrc on the stream it launches on.
+launch (sum of buffer lengths) / average kernel time: one HIP event pair on
+the stream the launches go to, around the timed steps, divided by the
+launches (back-to-back launches leave no gap on the stream; per-launch events
+did, ~10 us each: ZCRC_BENCH_KERNEL_EVENTS=1).
 `cpu_baseline` times the reference's own src/cg_crc32.c (oracle/_ref, built
 from the reference sources) on the host cores over a bounded sample.
 """
@@ -118,6 +120,16 @@ class Workload:
         self.n_local = n
         self.n_total = n * self.world
         self.bytes_local = n * L
+
+
+class _NoProfile:
+    total_ms, launches, small_ms, small_launches = float("nan"), 0, 0.0, 0
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        return False
 
 
 def golden_check(cfg: int, glob: np.ndarray) -> str:
@@ -393,14 +405,34 @@ def main() -> None:
         torch.cuda.synchronize()
         barrier()
         torch.cuda.synchronize()
-        with z.profile() as prof:
+        # Kernel time: one HIP event pair on the stream the launches go to
+        # (torch's current stream), bracketing the timed steps -- GPU time per
+        # step / CRC launches per step.  Back-to-back launches leave no gap on
+        # the stream (rocprofv3 kernel trace: end-to-next-start 0 us), so this
+        # is the average launch duration; when a plan kernel precedes the CRC
+        # launch (n > 8192) its few us are counted in too (conservative).
+        # Events on every launch (hipExtLaunchKernel; ZCRC_BENCH_KERNEL_EVENTS=1
+        # restores them) left a ~10 us bubble before each launch: config 2
+        # stepped at 54.9 us instead of 51.2 (profiles/r03/s2).
+        per_launch = os.environ.get("ZCRC_BENCH_KERNEL_EVENTS") == "1"
+        ev0 = torch.cuda.Event(enable_timing=True)
+        ev1 = torch.cuda.Event(enable_timing=True)
+        with (z.profile() if per_launch else _NoProfile()) as prof:
             t0 = time.perf_counter()
+            ev0.record()
             for s in range(steps):
                 step(warmup + s)
+            ev1.record()
             torch.cuda.synchronize()
             t1 = time.perf_counter()
         barrier()
         elapsed = t1 - t0
+        if per_launch:
+            avg_kernel_ms, launches, timing = prof.total_ms / max(prof.launches, 1), prof.launches, \
+                "HIP events on every CRC launch (hipExtLaunchKernel)"
+        else:
+            avg_kernel_ms, launches, timing = ev0.elapsed_time(ev1) / steps, steps, \
+                "one HIP event pair on the launch stream around the timed steps / launches"
         if use_dist:
             rdev = dev if args.dist_backend == "nccl" else torch.device("cpu")
             et = torch.tensor([elapsed], dtype=torch.float64, device=rdev)
@@ -419,18 +451,11 @@ def main() -> None:
         glob = result["global"].cpu().numpy().view(np.uint32)
         parity = golden_check(cfg, glob) if rank == 0 else None
         # the device path runs in one batch-kernel launch per step (the split
-        # plan's small list, when it splits, runs inside it: zcrc_kernels.hip);
-        # launches of the separate small kernel (strided/host paths) are
-        # reported beside it
-        small_b = 0
-        res = {"wl_desc": wl.desc, "n_local": wl.n_local, "kernel": z.kernel_name_for(wl.n_local), "bytes_local": wl.bytes_local, "elapsed": elapsed,
-               "bytes_all": bytes_all, "avg_kernel_ms": prof.total_ms / max(prof.launches, 1),
-               "launches": prof.launches, "parity": parity, "gathered_on": gathered_on, "bytes_main": wl.bytes_local - small_b,
-               "small": None if not prof.small_launches else {
-                   "kernel": z.small_kernel_name(), "launches_timed": prof.small_launches,
-                   "avg_kernel_ms": round(prof.small_ms / prof.small_launches, 4),
-                   "algorithmic_bytes_per_launch": small_b,
-                   "achieved": round(small_b / (prof.small_ms / prof.small_launches * 1e-3) / 1e9, 1)}}
+        # plan's small list, when it splits, runs inside it: zcrc_kernels.hip)
+        res = {"wl_desc": wl.desc, "n_local": wl.n_local, "kernel": z.kernel_name_for(wl.n_local),
+               "bytes_local": wl.bytes_local, "elapsed": elapsed, "bytes_all": bytes_all,
+               "avg_kernel_ms": avg_kernel_ms, "kernel_timing": timing, "launches": launches, "parity": parity,
+               "gathered_on": gathered_on, "bytes_main": wl.bytes_local, "small": None}
         del wl, out, result
         torch.cuda.empty_cache()
         return res
@@ -524,6 +549,7 @@ def main() -> None:
                 "kernel_source_hash": z.kernel_source_hash(),
                 "avg_kernel_ms": round(avg_kernel_ms, 4),
                 "launches_timed": m["launches"],
+                "kernel_timing": m["kernel_timing"],
                 "small_kernel": m["small"],
             },
             "cpu_baseline": cpu,

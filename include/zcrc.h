@@ -51,7 +51,8 @@ extern "C" {
  * of at least zcrc32_set_gpu_min_bytes() bytes (env ZCRC_GPU_MIN_BYTES; the
  * default is the measured host/GPU crossover) are checksummed
  * on the GPU; smaller ones, calls that find every staging slot busy (the
- * drop-in never waits for staging: the caller holds the lock), and any call
+ * drop-in never waits for nor creates staging: the caller holds the lock;
+ * see zcrc32_prewarm), and any call
  * whose GPU attempt fails (no device, HIP error) are answered by libzcrc's
  * own host CRC-32 (PCLMUL folding, zcrc_host.cpp).  The first fallback is
  * reported on stderr; all are counted by zcrc32_dropin_stats. */
@@ -138,16 +139,41 @@ int zcrc_inflate_batch(const void *const *src, const size_t *src_len, void *cons
 /* Streaming / incremental CRC.  ZIPsFS fills a preload
  * buffer in <= 16 MiB zip_fread() chunks (src/ZIPsFS_preloadfileram.c:286-306)
  * and only then CRCs the whole entry under mutex_fhandle (:309-321).  A
- * stream checksums each chunk as it lands: update() copies the chunk to
- * pinned staging and enqueues H2D + kernel on the stream's own HIP stream
- * (the running CRC stays on the device), so the GPU work overlaps the next
- * inflate; final() waits and returns crc32(seed, all bytes so far).
- * One thread at a time per stream; streams are independent. */
+ * stream checksums each chunk as it lands: update() enqueues the chunk's H2D
+ * copy and kernel on the stream's own HIP stream (the running CRC stays on
+ * the device), so the GPU work overlaps the next inflate; final() waits and
+ * returns crc32(seed, all bytes so far).  One thread at a time per stream;
+ * streams are independent.
+ *
+ * zcrc32_stream_open_registered(seed, segment, bytes) also page-locks the
+ * caller's preload segment (ZIPsFS: the entry's textbuffer segment,
+ * src/cg_textbuffer.c:103-106) until close(): chunks inside it are DMA'd to
+ * the GPU straight from it and update() returns at once, without copying.
+ * The segment must stay mapped, and its updated bytes unchanged, until
+ * close().  If the segment cannot be registered the stream works as an
+ * unregistered one.  Without registration update() copies each piece into a
+ * pinned staging slot (never waiting for one: with every slot of the pool
+ * leased, the HIP runtime copies from the pageable source itself).  Errors are sticky: after a
+ * failed update() every later update() and final() return that error until
+ * the stream is closed; a partial CRC is never returned. */
 typedef struct zcrc32_stream zcrc32_stream;
 zcrc32_stream *zcrc32_stream_open(uint32_t seed);            /* NULL on failure */
+zcrc32_stream *zcrc32_stream_open_registered(uint32_t seed, const void *segment, size_t segment_bytes);
 int zcrc32_stream_update(zcrc32_stream *s, const void *data, size_t n_bytes);
 int zcrc32_stream_final(zcrc32_stream *s, uint32_t *crc);      /* stream stays usable */
 void zcrc32_stream_close(zcrc32_stream *s);
+/* How the stream's 4 MiB pieces went to the GPU: DMA from the registered
+ * segment / copied through pinned staging / runtime-staged pageable copy (no
+ * slot was free).  Every piece is checksummed on the GPU. */
+int zcrc32_stream_stats(const zcrc32_stream *s, uint64_t *dma_pieces, uint64_t *staged_pieces,
+                        uint64_t *pageable_pieces);
+
+/* Device initialisation plus up to `staging_slots` pinned staging slots,
+ * created now -- call it at startup (ZIPsFS: before the preload threads),
+ * outside any lock.  The drop-in never creates a slot itself (it runs under
+ * mutex_fhandle): a call that finds none free answers from the host CRC and
+ * a background thread creates one for the next call. */
+int zcrc32_prewarm(size_t staging_slots);
 
 /* Batched ZIP verification.  ZIPsFS takes each
  * entry's expected CRC from the central directory (libzip zip_stat, st.crc:

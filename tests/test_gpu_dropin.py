@@ -46,6 +46,7 @@ def test_dropin_gpu_path_launches_kernel():
     it no kernel runs; both answers are the reference's."""
     from oracle import oracle as o
     lib = _lib.lib()
+    z.prewarm(1)  # the drop-in never creates a staging slot itself (it runs under mutex_fhandle)
     data = o.payload(3 << 20, 11)
     exp = o.payload_crc(3 << 20, 11)
     old = lib.zcrc32_set_gpu_min_bytes(1 << 20)

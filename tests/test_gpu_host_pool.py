@@ -97,7 +97,26 @@ after = ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_uint64()
 lib.zcrc32_dropin_stats(*[ctypes.byref(x) for x in after])
 assert got == exp[1]
 assert after[1].value == before[1].value + 1 and after[0].value == before[0].value, "busy pool -> host answer"
+# a second stream finds no slot either: its pieces are copied from pageable
+# memory by the HIP runtime (it never waits for a slot and never returns a
+# partial CRC: ADVICE r2)
+t = z.Crc32Stream(seed=9)
+for off in range(0, big[2].size, 16 << 20):
+    t.update(big[2][off: off + (16 << 20)])
+assert t.final() == zlib.crc32(big[2].tobytes(), 9), "pageable stream pieces"
+st = t.stats()
+assert st["pageable"] == -(-big[2].size // (4 << 20)) and st["staged"] == 0 and st["dma"] == 0, st
+t.close()
+# a registered segment needs no slot at all: its pieces are DMA'd from it
+seg = big[0].copy()
+r = z.Crc32Stream(segment=seg)
+for off in range(0, seg.size, 16 << 20):
+    r.update(seg[off: off + (16 << 20)])
+assert r.final() == exp[0], "registered stream with the pool exhausted"
+assert r.stats() == {"dma": 10, "staged": 0, "pageable": 0}, r.stats()
+r.close()
 assert s.final() == zlib.crc32(big[0][: 1 << 20].tobytes())
+assert s.stats()["staged"] == 1, s.stats()
 s.close()
 info = z.staging_info()
 assert info["slots_budget"] == 1 and info["slots_peak"] == 1 and info["slots_in_use"] == 0, info
@@ -107,9 +126,10 @@ print("one-slot pool ok", info)
 
 def test_staging_pool_with_one_slot(tmp_path):
     """ZCRC_STAGING_MIB=16 (one slot): buffers larger than a slot chain their
-    launches through it, the waiting GPU path works, and a drop-in call made
-    while a stream holds the only slot is answered by the host CRC instead of
-    waiting (it runs under mutex_fhandle)."""
+    launches through it, the waiting GPU path works, and while a stream holds
+    the only slot a drop-in call is answered by the host CRC instead of
+    waiting (it runs under mutex_fhandle), a second stream copies its pieces
+    from pageable memory, and a registered stream DMAs from its segment."""
     import os
     import subprocess
     import sys

@@ -29,7 +29,7 @@ def test_preload_loop_modes(tmp_path, size):
     o.payload(size, 41).tofile(path)
     exp = o.payload_crc(size, 41)
     reps = 7 if size <= (16 << 20) else 5
-    modes = ["dropin", "stream"] + (["ref"] if os.path.exists(du.REF_O0) else [])
+    modes = ["none", "dropin", "stream", "stream_reg"] + (["ref"] if os.path.exists(du.REF_O0) else [])
     rc, rows, stats, err = du.run_preload(exe, path, exp, reps, modes)
     assert rc == 0, err
     rc2, rows_gpu, stats2, err2 = du.run_preload(exe, path, exp, reps, ["dropin"], {"ZCRC_GPU_MIN_BYTES": "0"})
@@ -38,6 +38,7 @@ def test_preload_loop_modes(tmp_path, size):
     for m, r in rows.items():
         if "skipped" not in r:
             assert r["ok"] and int(r["crc"], 16) == exp, (m, r)
+    assert set(rows) >= {"none", "dropin", "stream", "stream_reg", "dropin_all_gpu"}, rows.keys()
     assert stats2 == {"gpu": reps, "host": 0, "fallback": 0}, stats2
     line = {"size": size, "rows": rows}
     print(json.dumps(line))

@@ -44,6 +44,9 @@ _SIGNATURES = {
     "zcrc32_stream_update": (_c_int, [_c_p, _c_p, _c_sz]),
     "zcrc32_stream_final": (_c_int, [_c_p, ctypes.POINTER(_c_u32)]),
     "zcrc32_stream_close": (None, [_c_p]),
+    "zcrc32_stream_open_registered": (_c_p, [_c_u32, _c_p, _c_sz]),
+    "zcrc32_stream_stats": (_c_int, [_c_p] + [ctypes.POINTER(_c_u64)] * 3),
+    "zcrc32_prewarm": (_c_int, [_c_sz]),
     "zcrc_fill_synthetic": (_c_int, [_c_p, _c_p, _c_sz, _c_u64, _c_u64, _c_u64, _c_p]),
     "zcrc_last_error": (ctypes.c_char_p, []),
     "zcrc_version": (ctypes.c_char_p, []),

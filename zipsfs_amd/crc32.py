@@ -115,17 +115,38 @@ class Crc32Stream:
     ``final()`` returns crc32(seed, everything so far) almost immediately.
     """
 
-    def __init__(self, seed: int = 0):
-        self._s = lib().zcrc32_stream_open(seed & 0xFFFFFFFF)
+    def __init__(self, seed: int = 0, segment=None):
+        """``segment``: optional writable host buffer (numpy array, mmap,
+        bytearray) that the updates will come from -- the preload segment.  It
+        is page-locked until ``close()`` (zcrc32_stream_open_registered), and
+        updates inside it are DMA'd from it without a copy; it must stay alive
+        and unchanged until then (this object keeps a reference)."""
+        self._seg = None
+        if segment is None:
+            self._s = lib().zcrc32_stream_open(seed & 0xFFFFFFFF)
+        else:
+            keep, addr, nbytes = _host_view(segment)
+            self._seg = keep
+            self._s = lib().zcrc32_stream_open_registered(seed & 0xFFFFFFFF, addr, nbytes)
         if not self._s:
             msg = lib().zcrc_last_error()
             raise ZcrcError(f"zcrc32_stream_open failed: {msg.decode() if msg else ''}")
+        self._keep = []  # registered updates are read by DMA after update() returns
 
     def update(self, data) -> "Crc32Stream":
         keep, addr, nbytes = _host_view(data)
         check(lib().zcrc32_stream_update(self._s, addr, nbytes), "zcrc32_stream_update")
+        if self._seg is not None:
+            self._keep.append(keep)
         del keep
         return self
+
+    def stats(self) -> dict:
+        """4 MiB pieces DMA'd from the registered segment / copied through
+        pinned staging / copied from pageable memory (no staging slot free)."""
+        v = [ctypes.c_uint64() for _ in range(3)]
+        check(lib().zcrc32_stream_stats(self._s, *[ctypes.byref(x) for x in v]), "zcrc32_stream_stats")
+        return dict(zip(["dma", "staged", "pageable"], [x.value for x in v]))
 
     def final(self) -> int:
         out = ctypes.c_uint32(0)
@@ -136,6 +157,8 @@ class Crc32Stream:
         if self._s:
             lib().zcrc32_stream_close(self._s)
             self._s = None
+        self._seg = None
+        self._keep = []
 
     def __enter__(self):
         return self
@@ -375,6 +398,12 @@ def device_info() -> dict:
     a, b, c = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
     check(lib().zcrc_device_info(ctypes.byref(a), ctypes.byref(b), ctypes.byref(c)), "zcrc_device_info")
     return {"num_cus": a.value, "major": b.value, "minor": c.value}
+
+
+def prewarm(staging_slots: int = 16) -> None:
+    """zcrc32_prewarm: device init plus up to ``staging_slots`` pinned
+    staging slots now (the drop-in never creates one under its caller's lock)."""
+    check(lib().zcrc32_prewarm(int(staging_slots)), "zcrc32_prewarm")
 
 
 def staging_info() -> dict:

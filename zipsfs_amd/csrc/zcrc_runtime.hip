@@ -242,7 +242,9 @@ uint32_t dyn_shift_setting() {
 struct SplitScratch {
   size_t counts, prefix, tiles, ptrs, seeds, oidx, sidx, total;
   explicit SplitScratch(size_t n) {
-    counts = 128;  // [n_large, n_small, split, lanes]: in the counter area, off the counter's cache line
+    // [n_large, n_small, split, small lanes per buffer, small workgroups]
+    // (SplitPlan::counts): in the counter area, off the counter's cache line
+    counts = 128;
     prefix = kCtrBytes;
     tiles = prefix + 8 * (n + 1);
     ptrs = tiles + 8 * kTileWords * plan_tiles(n);
@@ -252,7 +254,7 @@ struct SplitScratch {
     total = sidx + 4 * n;
   }
 };
-static_assert(kCtrBytes >= 128 + 32, "split counts share the counter area");
+static_assert(kCtrBytes >= 128 + 5 * 8, "the five split counts share the counter area");
 
 bool split_batch(size_t n) { return n > kFusedMaxN && n < (1ull << 31) && small_enabled(); }
 
@@ -455,9 +457,12 @@ class SlotPool {
     static SlotPool *pool = new SlotPool();  // never destroyed: slots outlive static destructors
     return *pool;
   }
-  // A slot of device `dev`: a free one, a new one while under budget, else
-  // (wait) the next one released -- or *out = nullptr (no wait).
-  int acquire(int dev, bool wait, StageSlot **out) {
+  // A slot of device `dev`: a free one, a new one while under budget
+  // (`create`), else (wait) the next one released -- or *out = nullptr (no
+  // wait).  Without `create` (the drop-in, under the caller's mutex_fhandle:
+  // pinning 16 MiB there cost milliseconds) a missing slot is
+  // created by a background thread for the next call instead.
+  int acquire(int dev, bool wait, StageSlot **out, bool create = true) {
     *out = nullptr;
     std::unique_lock<std::mutex> lk(mu_);
     Dev &d = dev_[dev];
@@ -468,14 +473,21 @@ class SlotPool {
         note_in_use(+1);
         return ZCRC_OK;
       }
+      if (d.created < budget_slots_ && !create) {
+        if (!d.creating) {
+          d.creating = true;
+          d.created++;
+          std::thread([this, dev] { create_free(dev); }).detach();
+        }
+        return ZCRC_OK;
+      }
       if (d.created < budget_slots_) {
         d.created++;
         note_in_use(+1);
         lk.unlock();
-        StageSlot *s = new (std::nothrow) StageSlot();
-        const int rc = s ? slot_create(dev, s) : fail(ZCRC_ERR_HIP, "out of host memory");
+        StageSlot *s = nullptr;
+        const int rc = make_slot(dev, &s);
         if (rc) {
-          if (s) slot_destroy(s);
           lk.lock();
           d.created--;
           note_in_use(-1);
@@ -494,13 +506,43 @@ class SlotPool {
                                       std::to_string(kSlotWaitSeconds) + " s (ZCRC_STAGING_MIB)");
     }
   }
+  // Create up to `slots` free slots of device `dev` now (zcrc32_prewarm: at
+  // startup, outside any caller lock).  Returns the number of free slots.
+  int prewarm(int dev, size_t slots, size_t *free_now) {
+    for (;;) {
+      {
+        std::lock_guard<std::mutex> lk(mu_);
+        Dev &d = dev_[dev];
+        if (d.free.size() >= slots || d.created >= budget_slots_) {
+          *free_now = d.free.size();
+          return ZCRC_OK;
+        }
+        d.created++;
+      }
+      StageSlot *s = nullptr;
+      const int rc = make_slot(dev, &s);
+      std::lock_guard<std::mutex> lk(mu_);
+      Dev &d = dev_[dev];
+      if (rc) {
+        d.created--;
+        return rc;
+      }
+      d.free.push_back(s);
+      cv_.notify_one();
+    }
+  }
   void release(StageSlot *s) {
     if (!s) return;
-    (void)hipStreamSynchronize(s->stream);  // nothing of the last user still queued
+    // nothing of the last user still queued; a slot whose stream failed is
+    // destroyed, not pooled (every later lease of it would fail: ADVICE r2)
+    const bool broken = hipStreamSynchronize(s->stream) != hipSuccess;
     s->busy = false;
     s->scatter.clear();
+    const int dev = s->dev;
+    if (broken) slot_destroy(s);
     std::lock_guard<std::mutex> lk(mu_);
-    dev_[s->dev].free.push_back(s);
+    if (broken) dev_[dev].created--;
+    else dev_[dev].free.push_back(s);
     note_in_use(-1);
     cv_.notify_one();
   }
@@ -517,8 +559,32 @@ class SlotPool {
  private:
   struct Dev {
     std::vector<StageSlot *> free;
-    size_t created = 0;
+    size_t created = 0;    // including one being created in the background
+    bool creating = false;  // a background creation is running
   };
+  static int make_slot(int dev, StageSlot **out) {
+    StageSlot *s = new (std::nothrow) StageSlot();
+    const int rc = s ? slot_create(dev, s) : fail(ZCRC_ERR_HIP, "out of host memory");
+    if (rc) {
+      if (s) slot_destroy(s);
+      return rc;
+    }
+    *out = s;
+    return ZCRC_OK;
+  }
+  void create_free(int dev) {  // background thread: one slot for the free list
+    StageSlot *s = nullptr;
+    int rc = hipSetDevice(dev) == hipSuccess ? make_slot(dev, &s) : ZCRC_ERR_HIP;
+    std::lock_guard<std::mutex> lk(mu_);
+    Dev &d = dev_[dev];
+    d.creating = false;
+    if (rc) {
+      d.created--;
+      return;
+    }
+    d.free.push_back(s);
+    cv_.notify_one();
+  }
   SlotPool() {
     size_t mib = kDefaultStagingMiB;
     if (const char *e = getenv("ZCRC_STAGING_MIB")) {
@@ -544,14 +610,16 @@ struct Lease {
   int count = 0;
   // first slot: waits while none is free (or, !wait, returns with count 0);
   // second slot only if one is free right now (a holder never waits)
-  int take(bool wait, bool want_two) {
+  // create: a missing slot may be created on this thread (not under the
+  // drop-in's caller lock: SlotPool::acquire)
+  int take(bool wait, bool want_two, bool create = true) {
     int dev = 0;
     ZCRC_HIP_TRY(hipGetDevice(&dev));
-    int rc = SlotPool::get().acquire(dev, wait, &slot[0]);
+    int rc = SlotPool::get().acquire(dev, wait, &slot[0], create);
     if (rc || !slot[0]) return rc;
     count = 1;
     if (want_two) {
-      rc = SlotPool::get().acquire(dev, false, &slot[1]);
+      rc = SlotPool::get().acquire(dev, false, &slot[1], create);
       if (rc) return ZCRC_OK;  // one slot will do
       if (slot[1]) count = 2;
     }
@@ -730,6 +798,37 @@ int batch_host_direct(const DeviceCtx &dc, StageSlot &s, const void *const *ptrs
 // kBusy: no staging slot was free and the caller asked not to wait
 constexpr int kBusy = 1;
 
+// Diagnostics (ZCRC_TRACE_HOST=1): per-phase wall time of each staged host
+// call, one JSON line on stderr -- lease, waits for a slot's previous launch,
+// copies into pinned memory, queueing, the final wait.
+struct HostTrace {
+  static bool on() {
+    static const bool v = [] {
+      const char *e = getenv("ZCRC_TRACE_HOST");
+      return e && e[0] == '1';
+    }();
+    return v;
+  }
+  using clk = std::chrono::steady_clock;
+  clk::time_point t0 = clk::now(), mark = t0;
+  double us[5] = {0, 0, 0, 0, 0};  // lease, slot wait, copy, enqueue, final wait
+  int launches = 0, slots = 0;
+  size_t bytes = 0;
+  void lap(int k) {
+    const clk::time_point t = clk::now();
+    us[k] += std::chrono::duration<double, std::micro>(t - mark).count();
+    mark = t;
+  }
+  void print() const {
+    fprintf(stderr,
+            "{\"zcrc_trace_host\": {\"bytes\": %zu, \"slots\": %d, \"launches\": %d, \"lease_us\": %.1f, "
+            "\"slot_wait_us\": %.1f, \"copy_us\": %.1f, \"enqueue_us\": %.1f, \"final_wait_us\": %.1f, "
+            "\"total_us\": %.1f}}\n",
+            bytes, slots, launches, us[0], us[1], us[2], us[3], us[4],
+            std::chrono::duration<double, std::micro>(clk::now() - t0).count());
+  }
+};
+
 int batch_host(const void *const *ptrs, const size_t *lens, const uint32_t *seeds, uint32_t *out, size_t n,
                bool wait = true) {
   if (n == 0) return ZCRC_OK;
@@ -743,11 +842,14 @@ int batch_host(const void *const *ptrs, const size_t *lens, const uint32_t *seed
     total += (lens[i] + 15) & ~size_t(15);
     direct = direct && lens[i] <= kDirectMaxBuf && total <= kDirectBytes;
   }
+  const bool trace = HostTrace::on();
+  HostTrace tr;
   Lease lease;
-  rc = lease.take(wait, !direct && total > kStageBytes);
+  rc = lease.take(wait, !direct && total > kStageBytes, /*create=*/wait);
   if (rc) return rc;
   if (!lease.count) return kBusy;
   if (direct) return batch_host_direct(*dc, *lease.slot[0], ptrs, lens, seeds, out, n);
+  if (trace) tr.lap(0), tr.slots = lease.count, tr.bytes = total;
 
   int cur = 0;
   size_t i = 0;          // next buffer
@@ -758,6 +860,7 @@ int batch_host(const void *const *ptrs, const size_t *lens, const uint32_t *seed
     StageSlot &s = *lease.slot[cur];
     rc = slot_finish(s, out);
     if (rc) return rc;
+    if (trace) tr.lap(1);
     uint64_t *h_ptrs = reinterpret_cast<uint64_t *>(s.h_meta + kMetaPtrs);
     uint64_t *h_prefix = reinterpret_cast<uint64_t *>(s.h_meta + kMetaPrefix);
     uint32_t *h_seeds = reinterpret_cast<uint32_t *>(s.h_meta + kMetaSeeds);
@@ -798,6 +901,7 @@ int batch_host(const void *const *ptrs, const size_t *lens, const uint32_t *seed
     }
     h_prefix[items] = pos;
     CopyPool::get().run(jobs);
+    if (trace) tr.lap(2);
     // small whole buffers go last, to the small-buffer kernel, ordered by
     // size class (as the device split plan orders them); the rest keep their
     // order (a continuation stays item 0) for the batch kernel
@@ -888,25 +992,29 @@ int batch_host(const void *const *ptrs, const size_t *lens, const uint32_t *seed
     prev_slot = cur;
     prev_item = last_item;
     cur = (cur + 1) % lease.count;
+    if (trace) tr.lap(3), tr.launches++;
   }
   for (int k = 0; k < lease.count; k++) {
     rc = slot_finish(*lease.slot[k], out);
     if (rc) return rc;
   }
+  if (trace) tr.lap(4), tr.print();
   return ZCRC_OK;
 }
 
 // ------------------------------------------------------------- streaming
 
-// A stream stages each update in 4 MiB pieces, each copied, sent and
-// checksummed on its own, so that final() -- called under mutex_fhandle --
-// waits for the last piece only.  Lock hold per piece size (16-256 MiB
-// entries, tests/test_gpu_preload.py): 16 MiB 0.39-0.40 ms, 4 MiB 0.28-0.32,
-// 2 MiB 0.36-0.40, 1 MiB 0.6-0.7 (the per-piece memset/launch/copy
-// overheads queue up).  Each slot holds kStreamRegions pieces.
+// A stream moves each update in 4 MiB pieces, each sent and checksummed on
+// its own, so that final() -- called under mutex_fhandle -- waits for the
+// last piece only.  Lock hold per piece size (16-256 MiB entries,
+// tests/test_gpu_preload.py): 16 MiB 0.39-0.40 ms, 4 MiB 0.28-0.32, 2 MiB
+// 0.36-0.40, 1 MiB 0.6-0.7 (the per-piece memset/launch/copy overheads queue
+// up).  The stream owns a device ring of kStreamRegions pieces; a piece of a
+// registered segment (zcrc32_stream_open_registered) is DMA'd straight from
+// it, any other piece is first copied into a pinned region of a staging slot.
 constexpr size_t kStreamPiece = 4ull << 20;
 constexpr int kStreamRegions = (int)(kStageBytes / kStreamPiece);
-static_assert(kStreamRegions == 4, "zcrc32_stream::staged holds 2 slots x 4 regions");
+static_assert(kStreamRegions == 4, "zcrc32_stream::staged holds one slot's 4 regions");
 
 }  // namespace
 
@@ -914,19 +1022,28 @@ int set_error(int code, const char *msg) { return fail(code, msg); }
 
 }  // namespace zcrc
 
-// A stream object owns a HIP stream, two events and a 2-word device CRC cell;
-// closed streams go back to a free list (no allocation per ZIP entry).  Its
-// pinned/HBM staging is leased from the SlotPool by the first update() and
+// A stream object owns a HIP stream, events, a 2-word device CRC cell and a
+// 16 MiB device ring; closed streams go back to a free list (no allocation per
+// ZIP entry).  Pinned staging for unregistered data is leased from the
+// SlotPool by the first such update() -- never waiting: with no slot free,
+// the pieces are copied from pageable memory by the HIP runtime -- and
 // returned by final() and close(), so an open but idle stream holds none.
 struct zcrc32_stream {
   int dev = -1;
   hipStream_t stream = nullptr;
-  zcrc::StageSlot *slot[2] = {nullptr, nullptr};
-  int nslot = 0;
-  hipEvent_t staged[2 * 4] = {};  // H2D from pinned region r (slot r / kStreamRegions) finished
-  uint32_t *d_crc = nullptr;                  // [2] ping-pong running CRC
-  uint64_t parts = 0;                         // chunk launches so far
+  zcrc::StageSlot *slot = nullptr;
+  bool slot_tried = false;        // the pool had no free slot for this entry: pageable copies
+  hipEvent_t staged[4] = {};      // H2D from pinned region r finished (region reusable)
+  uint32_t *d_crc = nullptr;      // [2] ping-pong running CRC
+  uint8_t *d_ring = nullptr;      // kStreamRegions x kStreamPiece of HBM
+  uint64_t parts = 0;             // pieces so far
   uint32_t seed = 0;
+  int err = 0;                    // sticky: the first failed update, returned by final()
+  std::string err_msg;
+  const uint8_t *reg_base = nullptr;  // registered caller segment [reg_base, reg_base + reg_size)
+  size_t reg_size = 0;
+  bool reg_owned = false;             // registered by us (unregistered at close)
+  uint64_t dma_pieces = 0, staged_pieces = 0, pageable_pieces = 0;
 };
 
 namespace zcrc {
@@ -937,17 +1054,27 @@ std::mutex g_streams_mu;
 std::vector<zcrc32_stream *> g_streams_free;
 
 void stream_release_slots(zcrc32_stream *s) {
-  for (int b = 0; b < 2; b++) SlotPool::get().release(s->slot[b]), s->slot[b] = nullptr;
-  s->nslot = 0;
+  SlotPool::get().release(s->slot);
+  s->slot = nullptr;
+  s->slot_tried = false;
+}
+
+void stream_unregister(zcrc32_stream *s) {
+  if (s->reg_owned) (void)hipHostUnregister(const_cast<uint8_t *>(s->reg_base));
+  s->reg_base = nullptr;
+  s->reg_size = 0;
+  s->reg_owned = false;
 }
 
 void stream_destroy(zcrc32_stream *s) {
   if (!s) return;
   if (s->stream) (void)hipStreamSynchronize(s->stream);
   stream_release_slots(s);
+  stream_unregister(s);
   for (auto &e : s->staged)
     if (e) (void)hipEventDestroy(e);
   if (s->d_crc) (void)hipFree(s->d_crc);
+  if (s->d_ring) (void)hipFree(s->d_ring);
   if (s->stream) (void)hipStreamDestroy(s->stream);
   delete s;
 }
@@ -957,6 +1084,7 @@ int stream_create(zcrc32_stream *s) {
   ZCRC_HIP_TRY(hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking));
   for (auto &e : s->staged) ZCRC_HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
   ZCRC_HIP_TRY(hipMalloc(reinterpret_cast<void **>(&s->d_crc), 2 * sizeof(uint32_t)));
+  ZCRC_HIP_TRY(hipMalloc(reinterpret_cast<void **>(&s->d_ring), kStreamRegions * kStreamPiece));
   return ZCRC_OK;
 }
 
@@ -964,6 +1092,9 @@ int stream_create(zcrc32_stream *s) {
 int stream_reset(zcrc32_stream *s, uint32_t seed) {
   s->seed = seed;
   s->parts = 0;
+  s->err = 0;
+  s->err_msg.clear();
+  s->dma_pieces = s->staged_pieces = s->pageable_pieces = 0;
   ZCRC_HIP_TRY(hipMemcpyAsync(s->d_crc, &s->seed, 4, hipMemcpyHostToDevice, s->stream));
   ZCRC_HIP_TRY(hipStreamSynchronize(s->stream));  // s->seed is a host source
   return ZCRC_OK;
@@ -975,22 +1106,35 @@ int stream_update(zcrc32_stream *s, const uint8_t *data, size_t n) {
   if (rc) return rc;
   while (n > 0) {
     const size_t take = std::min(n, kStreamPiece);
-    if (s->nslot < 2) {  // first slot: wait while none is free; second: only if free now
-      rc = SlotPool::get().acquire(s->dev, s->nslot == 0, &s->slot[s->nslot]);
-      if (rc && s->nslot == 0) return rc;
-      if (!rc && s->slot[s->nslot]) s->nslot++;
+    const int r = (int)(s->parts % (uint64_t)kStreamRegions);
+    uint8_t *d = s->d_ring + (size_t)r * kStreamPiece;
+    const bool registered = s->reg_base && data >= s->reg_base && take <= s->reg_size &&
+                            (size_t)(data - s->reg_base) <= s->reg_size - take;
+    if (!registered && !s->slot && !s->slot_tried) {  // never waits: a free slot or none
+      rc = SlotPool::get().acquire(s->dev, false, &s->slot, /*create=*/true);
+      if (rc) return rc;
+      s->slot_tried = s->slot == nullptr;
     }
-    const int r = (int)(s->parts % (uint64_t)(kStreamRegions * s->nslot));
-    StageSlot &st = *s->slot[r / kStreamRegions];
-    uint8_t *h = st.h_data + (size_t)(r % kStreamRegions) * kStreamPiece;
-    uint8_t *d = st.d_data + (size_t)(r % kStreamRegions) * kStreamPiece;
-    // pinned region r is free once its previous H2D finished
-    ZCRC_HIP_TRY(hipEventSynchronize(s->staged[r]));
-    CopyPool::get().run({CopyJob{h, data, take}});
-    ZCRC_HIP_TRY(hipMemcpyAsync(d, h, take, hipMemcpyHostToDevice, s->stream));
-    ZCRC_HIP_TRY(hipEventRecord(s->staged[r], s->stream));
+    // the device ring region r is free: the kernel that last read it was
+    // queued earlier on this same stream
+    if (registered) {  // DMA straight from the caller's registered segment
+      ZCRC_HIP_TRY(hipMemcpyAsync(d, data, take, hipMemcpyHostToDevice, s->stream));
+      s->dma_pieces++;
+    } else if (s->slot) {  // pinned region r is free once its previous H2D finished
+      uint8_t *h = s->slot->h_data + (size_t)r * kStreamPiece;
+      ZCRC_HIP_TRY(hipEventSynchronize(s->staged[r]));
+      CopyPool::get().run({CopyJob{h, data, take}});
+      ZCRC_HIP_TRY(hipMemcpyAsync(d, h, take, hipMemcpyHostToDevice, s->stream));
+      ZCRC_HIP_TRY(hipEventRecord(s->staged[r], s->stream));
+      s->staged_pieces++;
+    } else {  // no slot free: the HIP runtime stages the pageable source itself
+      // (the copy returns once the source is consumed); still on the GPU --
+      // never waiting for a slot, never a CRC of part of the entry
+      ZCRC_HIP_TRY(hipMemcpyAsync(d, data, take, hipMemcpyHostToDevice, s->stream));
+      s->pageable_pieces++;
+    }
     // running CRC: seed from d_crc[cur], result to d_crc[cur ^ 1] (zeroed:
-    // split pieces xor into it).  One HIP stream => chunks chain in order.
+    // split pieces xor into it).  One HIP stream => pieces chain in order.
     uint32_t *cur = s->d_crc + (s->parts & 1u), *nxt = s->d_crc + ((s->parts + 1) & 1u);
     ZCRC_HIP_TRY(hipMemsetAsync(nxt, 0, 4, s->stream));
     BatchArgs a{};
@@ -1414,17 +1558,49 @@ zcrc32_stream *zcrc32_stream_open(uint32_t seed) {
   return s;
 }
 
+zcrc32_stream *zcrc32_stream_open_registered(uint32_t seed, const void *segment, size_t segment_bytes) {
+  if (segment_bytes && !segment) {
+    fail(ZCRC_ERR_ARG, "null segment");
+    return nullptr;
+  }
+  zcrc32_stream *s = zcrc32_stream_open(seed);
+  if (!s || !segment_bytes) return s;
+  // page-locks the segment (and maps it for the DMA engines) until close();
+  // memory someone else registered is used as it is and left registered
+  const hipError_t e = hipHostRegister(const_cast<void *>(segment), segment_bytes, hipHostRegisterDefault);
+  if (e == hipSuccess || e == hipErrorHostMemoryAlreadyRegistered) {
+    s->reg_base = static_cast<const uint8_t *>(segment);
+    s->reg_size = segment_bytes;
+    s->reg_owned = e == hipSuccess;
+  } else {
+    (void)hipGetLastError();  // not sticky: this stream stages through pinned copies instead
+  }
+  return s;
+}
+
 int zcrc32_stream_update(zcrc32_stream *s, const void *data, size_t n_bytes) {
   if (!s) return fail(ZCRC_ERR_ARG, "null stream");
-  if (n_bytes && !data) return fail(ZCRC_ERR_ARG, "null data");
+  if (s->err) return fail(s->err, "stream failed earlier: " + s->err_msg);
   int dev = -1;
-  ZCRC_HIP_TRY(hipGetDevice(&dev));
-  if (dev != s->dev) return fail(ZCRC_ERR_ARG, "stream used on another device");
-  return stream_update(s, static_cast<const uint8_t *>(data), n_bytes);
+  int rc;
+  if (n_bytes && !data) rc = fail(ZCRC_ERR_ARG, "null data");
+  else if (hipGetDevice(&dev) != hipSuccess) rc = fail(ZCRC_ERR_HIP, "hipGetDevice failed");
+  else if (dev != s->dev) rc = fail(ZCRC_ERR_ARG, "stream used on another device");
+  else rc = stream_update(s, static_cast<const uint8_t *>(data), n_bytes);
+  if (rc) {  // sticky: final() must never return the CRC of part of the entry
+    s->err = rc;
+    s->err_msg = t_last_error;
+  }
+  return rc;
 }
 
 int zcrc32_stream_final(zcrc32_stream *s, uint32_t *crc) {
   if (!s || !crc) return fail(ZCRC_ERR_ARG, "null argument");
+  if (s->err) {
+    (void)hipStreamSynchronize(s->stream);
+    stream_release_slots(s);
+    return fail(s->err, "stream failed earlier: " + s->err_msg);
+  }
   uint32_t v = 0;
   ZCRC_HIP_TRY(hipMemcpyAsync(&v, s->d_crc + (s->parts & 1u), 4, hipMemcpyDeviceToHost, s->stream));
   ZCRC_HIP_TRY(hipStreamSynchronize(s->stream));
@@ -1440,12 +1616,32 @@ void zcrc32_stream_close(zcrc32_stream *s) {
     return;
   }
   stream_release_slots(s);
+  stream_unregister(s);  // after the stream's last DMA from the segment
   std::lock_guard<std::mutex> lk(g_streams_mu);
   if (g_streams_free.size() < kStreamFreeMax) {
     g_streams_free.push_back(s);
     return;
   }
   stream_destroy(s);
+}
+
+int zcrc32_stream_stats(const zcrc32_stream *s, uint64_t *dma_pieces, uint64_t *staged_pieces,
+                        uint64_t *pageable_pieces) {
+  if (!s) return fail(ZCRC_ERR_ARG, "null stream");
+  if (dma_pieces) *dma_pieces = s->dma_pieces;
+  if (staged_pieces) *staged_pieces = s->staged_pieces;
+  if (pageable_pieces) *pageable_pieces = s->pageable_pieces;
+  return ZCRC_OK;
+}
+
+int zcrc32_prewarm(size_t staging_slots) {
+  DeviceCtx *dc = nullptr;
+  int rc = device_ctx(&dc);
+  if (rc) return rc;
+  int dev = 0;
+  ZCRC_HIP_TRY(hipGetDevice(&dev));
+  size_t have = 0;
+  return SlotPool::get().prewarm(dev, staging_slots, &have);
 }
 
 int zcrc_staging_info(uint64_t *pinned_bytes, uint64_t *slots_in_use, uint64_t *slots_peak, uint64_t *slots_budget) {
