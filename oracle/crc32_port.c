@@ -201,6 +201,35 @@ static int run_batch(crc_fn_t fn, const uint8_t *const *ptrs, const uint64_t *le
   return 0;
 }
 
+/* Payload of buffers i (index idx[i]) written by the thread that will own
+ * them in run_batch (round-robin): first touch places each page on the
+ * NUMA node of the core that later checksums it (bench.py cpu_baseline). */
+typedef struct {
+  uint8_t *const *ptrs; const uint64_t *lens, *idx; uint64_t seed, n; int tid, nthreads;
+} fill_job_t;
+
+static void *fill_worker(void *arg) {
+  fill_job_t *j = (fill_job_t *)arg;
+  for (uint64_t i = (uint64_t)j->tid; i < j->n; i += (uint64_t)j->nthreads)
+    oracle_fill_payload(j->ptrs[i], j->lens[i], j->idx[i], j->seed);
+  return NULL;
+}
+
+int oracle_fill_payload_batch(uint8_t *const *ptrs, const uint64_t *lens, const uint64_t *idx, uint64_t seed,
+                              uint64_t n, int nthreads) {
+  if (nthreads < 1) nthreads = 1;
+  if (nthreads > 1024) nthreads = 1024;
+  pthread_t th[1024];
+  fill_job_t jobs[1024];
+  for (int t = 0; t < nthreads; t++) {
+    jobs[t] = (fill_job_t){ptrs, lens, idx, seed, n, t, nthreads};
+    if (t && pthread_create(&th[t], NULL, fill_worker, &jobs[t]) != 0) return -1;
+  }
+  fill_worker(&jobs[0]);
+  for (int t = 1; t < nthreads; t++) pthread_join(th[t], NULL);
+  return 0;
+}
+
 int oracle_crc32_batch(const uint8_t *const *ptrs, const uint64_t *lens, const uint32_t *seeds,
                        uint32_t *out, uint64_t n, int nthreads) {
   pthread_once(&tables_once, build_tables);

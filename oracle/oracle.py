@@ -49,6 +49,9 @@ def _setup_port(lib: ctypes.CDLL) -> ctypes.CDLL:
     lib.oracle_mix64.argtypes = [ctypes.c_uint64]
     lib.oracle_fill_payload.restype = None
     lib.oracle_fill_payload.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64]
+    lib.oracle_fill_payload_batch.restype = ctypes.c_int
+    lib.oracle_fill_payload_batch.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64,
+                                              ctypes.c_uint64, ctypes.c_int]
     lib.oracle_zipf_len.restype = ctypes.c_uint64
     lib.oracle_zipf_len.argtypes = [ctypes.c_uint64]
     lib.oracle_crc_payload.restype = ctypes.c_uint32

@@ -436,6 +436,27 @@ int slot_create(int dev, StageSlot *s) {
   ZCRC_HIP_TRY(hipMalloc(reinterpret_cast<void **>(&s->d_meta), kMetaBytes));
   ZCRC_HIP_TRY(hipHostGetDevicePointer(reinterpret_cast<void **>(&s->h_data_dev), s->h_data, 0));
   ZCRC_HIP_TRY(hipHostGetDevicePointer(reinterpret_cast<void **>(&s->h_meta_dev), s->h_meta, 0));
+  // First use of a slot -- its first H2D from the pinned pages, its stream's
+  // first launch, D2H and event -- cost 1-9 ms (profiles/r03/s3,
+  // ZCRC_TRACE_HOST: the first staged drop-in call of a process held the
+  // caller's lock 1.9-15 ms).  Paid here, at creation, instead.
+  DeviceCtx *dc = nullptr;
+  if (const int rc = device_ctx(&dc)) return rc;
+  memset(s->h_data, 0, kStageBytes);
+  memset(s->h_meta, 0, kMetaBytes);
+  ZCRC_HIP_TRY(hipMemcpyAsync(s->d_data, s->h_data, kStageBytes, hipMemcpyHostToDevice, s->stream));
+  ZCRC_HIP_TRY(hipMemcpyAsync(s->d_meta, s->h_meta, kMetaBytes, hipMemcpyHostToDevice, s->stream));
+  BatchArgs a{};
+  a.base = s->d_data;
+  a.stride = a.len = kStageBytes;
+  a.n = 1;
+  a.out = reinterpret_cast<uint32_t *>(s->d_meta + kMetaRes);
+  a.tab = dc->d_tab;
+  ZCRC_HIP_TRY(launch_batch(a, true, dc->num_cus, s->stream));  // not profiled (zcrc_profile_*)
+  ZCRC_HIP_TRY(hipEventRecord(s->kernel, s->stream));
+  ZCRC_HIP_TRY(hipMemcpyAsync(s->h_meta + kMetaRes, s->d_meta + kMetaRes, 4, hipMemcpyDeviceToHost, s->stream));
+  ZCRC_HIP_TRY(hipEventRecord(s->done, s->stream));
+  ZCRC_HIP_TRY(hipEventSynchronize(s->done));
   return ZCRC_OK;
 }
 
@@ -1034,6 +1055,7 @@ struct zcrc32_stream {
   zcrc::StageSlot *slot = nullptr;
   bool slot_tried = false;        // the pool had no free slot for this entry: pageable copies
   hipEvent_t staged[4] = {};      // H2D from pinned region r finished (region reusable)
+  hipEvent_t dma_end = nullptr;   // the DMA of a registered segment's last bytes finished
   uint32_t *d_crc = nullptr;      // [2] ping-pong running CRC
   uint8_t *d_ring = nullptr;      // kStreamRegions x kStreamPiece of HBM
   uint64_t parts = 0;             // pieces so far
@@ -1073,6 +1095,7 @@ void stream_destroy(zcrc32_stream *s) {
   stream_unregister(s);
   for (auto &e : s->staged)
     if (e) (void)hipEventDestroy(e);
+  if (s->dma_end) (void)hipEventDestroy(s->dma_end);
   if (s->d_crc) (void)hipFree(s->d_crc);
   if (s->d_ring) (void)hipFree(s->d_ring);
   if (s->stream) (void)hipStreamDestroy(s->stream);
@@ -1083,6 +1106,7 @@ int stream_create(zcrc32_stream *s) {
   ZCRC_HIP_TRY(hipGetDevice(&s->dev));
   ZCRC_HIP_TRY(hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking));
   for (auto &e : s->staged) ZCRC_HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  ZCRC_HIP_TRY(hipEventCreateWithFlags(&s->dma_end, hipEventDisableTiming));
   ZCRC_HIP_TRY(hipMalloc(reinterpret_cast<void **>(&s->d_crc), 2 * sizeof(uint32_t)));
   ZCRC_HIP_TRY(hipMalloc(reinterpret_cast<void **>(&s->d_ring), kStreamRegions * kStreamPiece));
   return ZCRC_OK;
@@ -1104,6 +1128,7 @@ int stream_update(zcrc32_stream *s, const uint8_t *data, size_t n) {
   DeviceCtx *dc = nullptr;
   int rc = device_ctx(&dc);
   if (rc) return rc;
+  bool last_dma = false;
   while (n > 0) {
     const size_t take = std::min(n, kStreamPiece);
     const int r = (int)(s->parts % (uint64_t)kStreamRegions);
@@ -1120,6 +1145,12 @@ int stream_update(zcrc32_stream *s, const uint8_t *data, size_t n) {
     if (registered) {  // DMA straight from the caller's registered segment
       ZCRC_HIP_TRY(hipMemcpyAsync(d, data, take, hipMemcpyHostToDevice, s->stream));
       s->dma_pieces++;
+      // the piece that ends the segment: final() comes next, under the
+      // caller's lock -- wait for this DMA here, outside it (below)
+      if (data + take == s->reg_base + s->reg_size) {
+        ZCRC_HIP_TRY(hipEventRecord(s->dma_end, s->stream));
+        last_dma = true;
+      }
     } else if (s->slot) {  // pinned region r is free once its previous H2D finished
       uint8_t *h = s->slot->h_data + (size_t)r * kStreamPiece;
       ZCRC_HIP_TRY(hipEventSynchronize(s->staged[r]));
@@ -1151,6 +1182,9 @@ int stream_update(zcrc32_stream *s, const uint8_t *data, size_t n) {
     data += take;
     n -= take;
   }
+  // registered segment complete: its last DMA is waited for here, so that
+  // final() (under mutex_fhandle) waits for the last kernels only
+  if (last_dma) ZCRC_HIP_TRY(hipEventSynchronize(s->dma_end));
   return ZCRC_OK;
 }
 
