@@ -78,8 +78,14 @@ static int preload_once(const char *path, int mode, ref_fn ref, result_t *r) {
   if (fstat(fd, &st)) return -1;
   const off_t st_size = st.st_size;
   const int use_mmap = st_size > THRESHOLD_MALLOC_MMAP;
-  char *dst = use_mmap ? mmap(NULL, st_size ? st_size : 1, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0)
-                       : malloc(st_size ? st_size : 1);
+  /* ZCRC_PRELOAD_REUSE=1 (diagnostics): one segment for every repetition,
+   * never unmapped in between */
+  static char *kept = NULL;
+  const int reuse = getenv("ZCRC_PRELOAD_REUSE") && use_mmap;
+  char *dst = reuse && kept ? kept
+              : use_mmap ? mmap(NULL, st_size ? st_size : 1, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0)
+                         : malloc(st_size ? st_size : 1);
+  if (reuse) kept = dst;
   if (!dst || dst == MAP_FAILED) return -1;
   zcrc32_stream *s = NULL;
   r->open_us = r->close_us = 0;
@@ -117,7 +123,7 @@ static int preload_once(const char *path, int mode, ref_fn ref, result_t *r) {
     zcrc32_stream_close(s);
     r->close_us = now_us() - t;
   }
-  if (use_mmap) munmap(dst, st_size ? st_size : 1);
+  if (use_mmap && !reuse) munmap(dst, st_size ? st_size : 1);
   else free(dst);
   close(fd);
   return 0;

@@ -397,9 +397,10 @@ K_SMALL_COST = 14  # zcrc_internal.h kSmallCostDefault (quarters of a batch-kern
 
 
 def split_plan(lens, grid: int = 256, force: bool = False, small_cost: int = K_SMALL_COST):
-    """zcrc_kernels.hip plan_split_scan's decisions and lists: (split,
-    large list in order with its prefix, small list by size class, small
-    workgroups, small lanes)."""
+    """zcrc_kernels.hip plan_split_scatter's decisions and lists: (split,
+    large list in order with its prefix, small list tile by tile (8192
+    buffers), by size class within a tile and in index order within a class,
+    small workgroups, small lanes)."""
     lens = [int(x) for x in lens]
     small = [i for i, L in enumerate(lens) if L <= K_SMALL_MAX]
     large = [i for i, L in enumerate(lens) if L > K_SMALL_MAX]
@@ -414,7 +415,7 @@ def split_plan(lens, grid: int = 256, force: bool = False, small_cost: int = K_S
         wgs = min(max(wgs, 1), grid - 1)
     if not split:
         return dict(split=False, large=list(range(len(lens))), small=[], wgs=wgs, lanes=16)
-    by_class = sorted(small, key=lambda i: (lens[i] + 255) >> 8)  # within a class: any order
+    by_class = sorted(small, key=lambda i: (i // 8192, (lens[i] + 255) >> 8, i))
     lanes = 8 if as_ <= 2048 * len(small) else 16
     return dict(split=True, large=large, small=by_class, wgs=wgs, lanes=lanes)
 

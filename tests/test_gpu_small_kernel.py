@@ -281,3 +281,60 @@ def test_split_batches_overlapping_on_four_streams():
         for j, ((offs, ln), got) in enumerate(zip(plans[t], res[t])):
             exp = _oracle(host, offs, ln, np.zeros(len(ln), dtype=np.uint32))
             np.testing.assert_array_equal(got, exp, err_msg=f"thread {t} job {j}")
+
+
+def _split_lists(scratch, n):
+    """The split plan's outputs in caller-owned scratch (SplitScratch,
+    zcrc_runtime.hip): counts, prefix_c, oidx, sidx."""
+    raw = scratch.cpu().numpy()
+    T = -(-n // 8192)
+    prefix = 256
+    tiles = prefix + 8 * (n + 1)
+    tile_pre = tiles + 24 * T
+    ptrs = tile_pre + 24 * (T + 1)
+    seeds = ptrs + 8 * n
+    oidx = seeds + 4 * n
+    sidx = oidx + 4 * n
+    counts = raw[128:168].view(np.uint64)
+    return (counts, raw[prefix:prefix + 8 * (n + 1)].view(np.uint64), raw[oidx:oidx + 4 * n].view(np.uint32),
+            raw[sidx:sidx + 4 * n].view(np.uint32))
+
+
+@pytest.mark.parametrize("n,shape", [(20_000, "mixed"), (50_000, "all_small"), (4_200_000, "mixed"),
+                                     (4_300_000, "all_small")])
+def test_split_plan_lists_equal_the_model(n, shape):
+    """The plan's decision, the compacted batch (order and byte prefix) and the
+    small list (tile by tile, by size class, index order within a class) equal
+    tests/kernel_model.py's split_plan; above 512 tiles (n > 4,194,304) through
+    the tile-scan kernel.  Every CRC against the oracle."""
+    import kernel_model as km
+    rng = np.random.default_rng(n)
+    top = SMALL_MAX + 1 if n < 1_000_000 else 600  # keep the 4M-buffer batches near 1 GiB
+    if shape == "all_small":
+        lens = rng.integers(0, min(top, 700), n)
+    else:  # ZIP-entry-like: most small, some large
+        lens = np.where(rng.random(n) < 0.995, rng.integers(0, top, n), rng.integers(SMALL_MAX + 1, 40_000, n))
+    lens = lens.astype(np.int64)
+    offs = np.zeros(n, dtype=np.int64)
+    offs[1:] = np.cumsum(lens + 3)[:-1]
+    mem = torch.randint(0, 256, (int(offs[-1] + lens[-1] + 64),), dtype=torch.uint8, device=DEV)
+    ptrs = mem.data_ptr() + torch.tensor(offs, device=DEV)
+    lt = torch.tensor(lens, device=DEV)
+    scratch = torch.empty(z.scratch_bytes(n), dtype=torch.uint8, device=DEV)
+    got = u32(z.crc32_batch_device_ws(ptrs, lt, scratch))
+    counts, prefix, oidx, sidx = _split_lists(scratch, n)
+    model = km.split_plan(lens.tolist(), grid=z.device_info()["num_cus"])
+    assert bool(counts[2]) == model["split"], counts
+    if model["split"]:
+        nl, ns = int(counts[0]), int(counts[1])
+        assert (nl, ns) == (len(model["large"]), len(model["small"]))
+        np.testing.assert_array_equal(oidx[:nl], np.array(model["large"], dtype=np.uint32))
+        np.testing.assert_array_equal(sidx[:ns], np.array(model["small"], dtype=np.uint32))
+        large_lens = lens[model["large"]]
+        np.testing.assert_array_equal(prefix[:nl + 1], np.concatenate([[0], np.cumsum(large_lens)]).astype(np.uint64))
+        assert int(counts[3]) == model["lanes"] and int(counts[4]) == model["wgs"], counts
+    else:
+        np.testing.assert_array_equal(prefix, np.concatenate([[0], np.cumsum(lens)]).astype(np.uint64))
+    host = mem.cpu().numpy()
+    exp = o.crc32_batch((host.ctypes.data + offs).astype(np.uint64), lens.astype(np.uint64), None, nthreads=16)
+    np.testing.assert_array_equal(got, exp)

@@ -176,8 +176,9 @@ def test_small_group_model_matches_oracle(G):
 
 def test_split_plan_model_lists():
     """The split plan's lists: the large buffers keep their order, the small
-    list holds every buffer <= 8 KiB once, ordered by 256-B block count; the
-    split rule and the workgroup share follow zcrc_kernels.hip."""
+    list holds every buffer <= 8 KiB once, ordered by 256-B block count within
+    each 8192-buffer tile (index order within a class); the split rule and the
+    workgroup share follow zcrc_kernels.hip."""
     rng = np.random.default_rng(5)
     # config-4-like law: most buffers small, a few MiB-sized ones carry the bytes
     u = rng.random(20000)
@@ -186,8 +187,8 @@ def test_split_plan_model_lists():
     assert p["split"] and 1 <= p["wgs"] <= 255
     assert sorted(p["large"] + p["small"]) == list(range(len(lens)))
     assert p["large"] == sorted(p["large"]) and all(lens[i] > 8192 for i in p["large"])
-    cls = [(int(lens[i]) + 255) >> 8 for i in p["small"]]
-    assert cls == sorted(cls)
+    key = [(i // 8192, (int(lens[i]) + 255) >> 8, i) for i in p["small"]]
+    assert key == sorted(key)
     # all large: nothing to split; all small: every workgroup takes the small list
     assert not km.split_plan([70000] * 10000)["split"]
     q = km.split_plan([1000] * 10000)

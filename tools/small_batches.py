@@ -6,11 +6,12 @@ repeats) are checksummed through zcrc32_batch_device (general form: device
 pointer and length arrays; above 8192 buffers the split plan routes buffers
 of <= 8 KiB to the small-buffer kernel) and zcrc32_batch_device_strided, with
 ZCRC_SMALL=1 (default) and 0 (batch kernel only).  Reported per call: the
-wall time between events on the stream (plans, launch gaps included) and the
-CRC kernels' own time (zcrc_profile: dispatch-packet timestamps).  Results of
-all four routes are compared.
+GPU time between two events on the stream around `reps` x 2 back-to-back
+calls (plans and launch gaps included; no per-launch events, which leave a
+~10 us bubble before each launch: profiles/r03/s2).  Results of all four
+routes are compared.
 
-  python tools/small_batches.py [reps] > out.jsonl
+  python tools/small_batches.py [reps] [len,len,...] > out.jsonl
 """
 import json
 import os
@@ -25,8 +26,9 @@ import zipsfs_amd as z  # noqa: E402
 
 def main():
     reps = int(sys.argv[1]) if len(sys.argv) > 1 else 10
+    lengths = [int(x) for x in sys.argv[2].split(",")] if len(sys.argv) > 2 else [1024, 2048, 3000, 4096, 8192, 16384]
     dev = "cuda:0"
-    for L in (1024, 2048, 3000, 4096, 8192, 16384):
+    for L in lengths:
         n = (1 << 30) // L
         bat = []
         for b in range(2):
@@ -50,20 +52,16 @@ def main():
                     ref = [o.clone() for o in outs]
                 same = all(torch.equal(o, r) for o, r in zip(outs, ref))
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                wall = 0.0
-                with z.profile() as prof:
-                    for r in range(reps):
-                        for b in range(2):
-                            e0.record()
-                            call(b)
-                            e1.record()
-                            e1.synchronize()
-                            wall += e0.elapsed_time(e1)
+                e0.record()
+                for r in range(reps):
+                    for b in range(2):
+                        call(b)
+                e1.record()
+                e1.synchronize()
                 calls = 2 * reps
-                w_ms, k_ms = wall / calls, prof.total_ms / calls
+                w_ms = e0.elapsed_time(e1) / calls
                 print(json.dumps({"len": L, "n": n, "api": api, "small": small == "1", "wall_ms": round(w_ms, 4),
                                   "wall_GBps": round(n * L / (w_ms * 1e-3) / 1e9, 1),
-                                  "kernels_ms": round(k_ms, 4), "launches_per_call": prof.launches / calls,
                                   "same_results": same}), flush=True)
         del bat
 

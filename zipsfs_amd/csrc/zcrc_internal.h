@@ -146,7 +146,8 @@ struct SplitPlan {
   const uint64_t *lens;
   const uint32_t *seeds;  // nullable
   uint64_t n;
-  uint64_t *tile_sum;     // kTileWords per tile: large bytes, small bytes, packed counts, size-class counts
+  uint64_t *tile_sum;     // kTileWords per tile: large bytes, small bytes, packed counts
+  uint64_t *tile_pre;     // kTileWords x (tiles + 1): exclusive tile prefixes + totals (above kPlanDirectTiles)
   uint64_t *prefix_c;     // n + 1
   const uint8_t **ptrs_c;
   uint32_t *seeds_c;      // written when seeds != nullptr
@@ -159,8 +160,9 @@ struct SplitPlan {
 };
 hipError_t launch_plan_split(const SplitPlan &p, hipStream_t stream);
 constexpr uint32_t kSizeClasses = kSmallMax / 256 + 1;  // small list order: 256-B block count
-constexpr uint32_t kTileWords = 3 + kSizeClasses;
-constexpr uint32_t kSmallCostDefault = 14;  // 3.5 batch-kernel bytes (zcrc_kernels.hip, plan_split_scan)
+constexpr uint32_t kTileWords = 3;
+constexpr uint64_t kPlanDirectTiles = 512;  // up to this many tiles each scatter workgroup sums the tile words itself
+constexpr uint32_t kSmallCostDefault = 14;  // 3.5 batch-kernel bytes (zcrc_kernels.hip, plan_split_scatter)
 
 }  // namespace zcrc
 

@@ -116,212 +116,227 @@ __global__ __launch_bounds__(1024) void plan_one_tile(const uint64_t *lens, uint
 }
 
 // ------------------------------------------------------------ split plan
-// Two passes like plan_tile_sums/plan_tile_scan.  Per tile: bytes of the
-// buffers above kSmallMax, bytes of those at or below it, both counts packed
-// (low half: above, high half: at or below) and the small buffers' size-class
-// counts.  The scan decides for the whole launch (every workgroup reads all
-// tile sums, so all decide alike): split when the small list is worth at
-// least two of the batch kernel's workgroups (or p.force and there is any
-// small buffer); otherwise it writes the plain prefix of all buffers, as
-// plan_tile_scan does, and an empty small list.  The large buffers keep
-// their order; the small list is ordered by size class.
+// Two passes like plan_tile_sums/plan_tile_scan, both with plan_one_tile's
+// coalesced layout: wave w of a tile owns its buffers [512w, 512w + 512), lane
+// l takes 512w + 64k + l for k < 8.  Per tile: bytes of the buffers above
+// kSmallMax, bytes of those at or below it, both counts packed (low half:
+// above, high half: at or below).  The scatter decides for the whole launch
+// (every workgroup reads the same tile sums, so all decide alike): split when
+// the small list is worth at least two of the batch kernel's workgroups (or
+// p.force and there is any small buffer); otherwise it writes the plain prefix
+// of all buffers, as plan_tile_scan does, and an empty small list.  The large
+// buffers keep their order; each tile's small buffers are listed by size
+// class (256-B blocks), in index order within a class, so that the buffers a
+// wave of the small body takes together run equal block counts.  The ranking
+// is a counting sort by ballots -- six ballots give each lane the mask of
+// lanes with its class -- with per (class, wave, k) counts scanned in LDS: no
+// atomics (the LDS class atomics of the round-2 plan serialised on uniform
+// batches: 25.5 us per config-4 plan, ~60 us of a 1M x 1 KiB call).
 
 __device__ __forceinline__ uint32_t size_class(uint64_t len) { return (uint32_t)((len + 255) >> 8); }  // 256-B blocks
 
-__global__ __launch_bounds__(1024) void plan_split_sums(SplitPlan p) {
+__global__ __launch_bounds__(1024) void plan_split_count(SplitPlan p) {
   __shared__ uint64_t s_w[16][3];
-  __shared__ uint32_t s_cls[kSizeClasses];
   const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
-  if (threadIdx.x < kSizeClasses) s_cls[threadIdx.x] = 0;
-  __syncthreads();
-  const uint64_t base = (uint64_t)blockIdx.x * kPlanTile;
-  uint64_t bl = 0, bs = 0, cnt = 0;
-  // all loads first: with the LDS atomics between them the compiler issued
-  // them one round trip at a time
+  const uint64_t base = (uint64_t)blockIdx.x * kPlanTile + 512u * wv + lane;
   uint64_t lv[kPlanPerThread];
 #pragma unroll
   for (uint32_t k = 0; k < kPlanPerThread; k++) {
-    const uint64_t idx = base + (uint64_t)k * blockDim.x + threadIdx.x;
-    lv[k] = idx < p.n ? p.lens[idx] : 0;
+    const uint64_t idx = base + 64u * k;
+    lv[k] = idx < p.n ? p.lens[idx] : ~0ull;  // ~0: absent
   }
+  uint64_t bl = 0, bs = 0, cnt = 0;
 #pragma unroll
   for (uint32_t k = 0; k < kPlanPerThread; k++) {
-    const uint64_t idx = base + (uint64_t)k * blockDim.x + threadIdx.x;
-    if (idx < p.n) {
-      const uint64_t L = lv[k];
-      if (L > kSmallMax) {
-        bl += L, cnt += 1;
-      } else {
-        bs += L, cnt += 1ull << 32;
-        atomicAdd(&s_cls[size_class(L)], 1u);
-      }
-    }
+    const uint64_t L = lv[k];
+    if (L == ~0ull) continue;
+    if (L > kSmallMax) bl += L, cnt += 1;
+    else bs += L, cnt += 1ull << 32;
   }
-  // sums only (no scan): one butterfly per wave, then the 16 wave totals
 #pragma unroll
   for (int d = 32; d >= 1; d >>= 1)
     bl += __shfl_xor(bl, d, 64), bs += __shfl_xor(bs, d, 64), cnt += __shfl_xor(cnt, d, 64);
   if (lane == 0) s_w[wv][0] = bl, s_w[wv][1] = bs, s_w[wv][2] = cnt;
   __syncthreads();
-  uint64_t *t = p.tile_sum + (uint64_t)kTileWords * blockIdx.x;
   if (threadIdx.x < 3) {
     uint64_t v = 0;
     for (uint32_t w = 0; w < 16; w++) v += s_w[w][threadIdx.x];
-    t[threadIdx.x] = v;
-  } else if (threadIdx.x < 3 + kSizeClasses) {
-    t[threadIdx.x] = s_cls[threadIdx.x - 3];
+    p.tile_sum[(uint64_t)kTileWords * blockIdx.x + threadIdx.x] = v;
   }
 }
 
-// Thread t of a tile owns its buffers 8t .. 8t+7 (one block scan per
-// quantity: a lane-contiguous layout with a wave scan per k cost 16 dependent
-// 64-bit shuffle scans per thread and measured 30 us on config 4, against 12
-// for plan_tile_scan).  Without a split only the byte prefix is scanned.
-__global__ __launch_bounds__(1024) void plan_split_scan(SplitPlan p) {
-  __shared__ uint64_t s_b[16], s_c[16];
-  __shared__ uint64_t s_off[2];
+// Above kPlanDirectTiles tiles: one workgroup turns the tile sums into
+// exclusive prefixes (tile_pre[3t + q]) and totals (tile_pre[3 tiles + q]),
+// so that each scatter workgroup reads 6 words instead of every earlier
+// tile's (that read grew with the square of the tile count).
+__global__ __launch_bounds__(1024) void plan_split_tiles(SplitPlan p, uint32_t tiles) {
+  __shared__ uint64_t s_tmp[16];
+  const uint32_t per = (tiles + 1023u) / 1024u, t0 = threadIdx.x * per;
+  for (uint32_t q = 0; q < 3; q++) {
+    uint64_t acc = 0;
+    for (uint32_t t = t0; t < t0 + per && t < tiles; t++) acc += p.tile_sum[(uint64_t)kTileWords * t + q];
+    uint64_t tot;
+    uint64_t run = block_excl_scan(acc, s_tmp, &tot);
+    for (uint32_t t = t0; t < t0 + per && t < tiles; t++) {
+      const uint64_t x = p.tile_sum[(uint64_t)kTileWords * t + q];
+      p.tile_pre[(uint64_t)kTileWords * t + q] = run;
+      run += x;
+    }
+    if (threadIdx.x == 0) p.tile_pre[(uint64_t)kTileWords * tiles + q] = tot;
+  }
+}
+
+__global__ __launch_bounds__(1024) void plan_split_scatter(SplitPlan p) {
+  constexpr uint32_t kGroups = 16 * kPlanPerThread;  // (wave, k) groups of 64 buffers per tile
+  __shared__ uint64_t s_tw[3][2];                    // large bytes, small bytes, counts: earlier tiles, all
+  __shared__ uint64_t s_wb[16];                      // wave byte totals
+  __shared__ uint32_t s_wc[16];                      // wave large counts
+  __shared__ uint64_t s_tmp[16];
   __shared__ uint32_t s_mode;
-  __shared__ uint64_t s_small_bytes;
-  __shared__ uint32_t s_small_wgs;
-  // the small list is ordered by size class (256-B blocks), so that the
-  // buffers a wave of the small body takes together run equal block counts;
-  // within a class and tile the order is the LDS atomics' (any order is
-  // correct: results go out by index)
-  __shared__ uint64_t s_cls_prev[kSizeClasses], s_cls_all[kSizeClasses], s_cls_at[kSizeClasses];
-  __shared__ uint32_t s_cls_cur[kSizeClasses];
-  if (blockIdx.x == 0 && threadIdx.x == 0) *p.ctr = 0u;  // the CRC kernel's work counter
-  // this thread's lengths, pointers and seeds, loaded before the tile sums
-  // are read (the scatter below stores between its uses, so loads left in
-  // its loop were issued one round trip at a time: 25 us per launch on
-  // config 4)
-  const uint64_t base = (uint64_t)blockIdx.x * kPlanTile + (uint64_t)threadIdx.x * kPlanPerThread;
+  __shared__ uint32_t s_cls[kSizeClasses * kGroups];  // small count per (class, group) -> exclusive position
+  const uint32_t tid = threadIdx.x, lane = tid & 63u, wv = tid >> 6;
+  const uint64_t lt = (1ull << lane) - 1;
+  if (blockIdx.x == 0 && tid == 0) *p.ctr = 0u;  // the CRC kernel's work counter
+  const uint64_t base = (uint64_t)blockIdx.x * kPlanTile + 512u * wv + lane;
+  // this thread's lengths, pointers and seeds first (coalesced)
   uint64_t v[kPlanPerThread];
   const uint8_t *pv[kPlanPerThread];
   uint32_t sv[kPlanPerThread];
 #pragma unroll
   for (uint32_t k = 0; k < kPlanPerThread; k++) {
-    const uint64_t idx = base + k;
+    const uint64_t idx = base + 64u * k;
     const bool in = idx < p.n;
     v[k] = in ? p.lens[idx] : 0;
     pv[k] = in ? p.ptrs[idx] : nullptr;
     sv[k] = in && p.seeds ? p.seeds[idx] : 0u;
   }
-  // Tile sums and class counts, read in parallel (one thread summing the
-  // tile words 8 at a time cost ~1 us per 8 tiles: 28 us on 1M x 1 KiB).
-  // Wave w takes tile words w, w + 16, w + 32 (0..2: the sums, 3..: the class
-  // counts); its lanes stride over the tiles.
-  __shared__ uint64_t s_tw[3][2];
-  {
-    const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6, tiles = gridDim.x;
-    for (uint32_t q = wv; q < 3 + kSizeClasses; q += 16) {
-      const uint32_t word = q;  // tile word: 0..2 sums, 3.. class counts
-      uint64_t prev = 0, all = 0;
-      for (uint32_t t = lane; t < tiles; t += 64) {
-        const uint64_t x = p.tile_sum[(uint64_t)kTileWords * t + word];
-        all += x;
-        if (t < blockIdx.x) prev += x;
-      }
-#pragma unroll
-      for (int d = 32; d >= 1; d >>= 1) all += __shfl_xor(all, d, 64), prev += __shfl_xor(prev, d, 64);
-      if (lane == 0) {
-        if (q < 3) {
-          s_tw[q][0] = prev, s_tw[q][1] = all;
-        } else {
-          s_cls_prev[q - 3] = prev, s_cls_all[q - 3] = all, s_cls_cur[q - 3] = 0;
-        }
-      }
+  // earlier tiles' and all tiles' sums
+  if (p.tile_pre) {
+    if (tid < 3) s_tw[tid][0] = p.tile_pre[(uint64_t)kTileWords * blockIdx.x + tid];
+    else if (tid < 6) s_tw[tid - 3][1] = p.tile_pre[(uint64_t)kTileWords * gridDim.x + tid - 3];
+  } else if (wv < 3) {
+    uint64_t prev = 0, all = 0;
+    for (uint32_t t = lane; t < gridDim.x; t += 64) {
+      const uint64_t x = p.tile_sum[(uint64_t)kTileWords * t + wv];
+      all += x;
+      if (t < blockIdx.x) prev += x;
     }
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) all += __shfl_xor(all, d, 64), prev += __shfl_xor(prev, d, 64);
+    if (lane == 0) s_tw[wv][0] = prev, s_tw[wv][1] = all;
   }
+  for (uint32_t i = tid; i < kSizeClasses * kGroups; i += 1024) s_cls[i] = 0u;
   __syncthreads();
-  if (threadIdx.x == 0) {
-    const uint64_t pl = s_tw[0][0], ps = s_tw[1][0], pc = s_tw[2][0];  // previous tiles
-    const uint64_t al = s_tw[0][1], as = s_tw[1][1], ac = s_tw[2][1];  // all tiles
-    {
-      // workgroups for the small list: its share of the CU time, a
-      // small-list byte weighted small_cost/4 against a batch-kernel byte
-      // (config 4 forced to split, one box: weight 1 -> 2.90 ms per step,
-      // 1.5 -> 2.25, 2.5 -> 2.045, 3.5 -> 2.046, 5 -> 2.047, 7 -> 2.049,
-      // against 2.06-2.075 unsplit; profiles/r02/small_kernel/)
-      const uint64_t n_large = ac & 0xFFFFFFFFull, n_small = ac >> 32;
-      const uint64_t ws = p.small_cost * as, wl = 4 * al;
-      uint64_t wgs = p.grid;
-      if (n_large) wgs = ws ? (p.grid * ws + ws + wl - 1) / (ws + wl) : 0;
-      // split when the small list is worth at least two workgroups (a
-      // workgroup given to a handful of small buffers would idle a CU)
-      const uint32_t mode = n_small && (p.force || wgs >= 2);
-      if (n_large) wgs = wgs < 1 ? 1 : (wgs > p.grid - 1 ? p.grid - 1 : wgs);
-      s_mode = mode;
-      s_small_bytes = as;
-      s_small_wgs = (uint32_t)wgs;
-      s_off[0] = mode ? pl : pl + ps;
-      s_off[1] = pc;
+  const uint64_t al = s_tw[0][1], as = s_tw[1][1], ac = s_tw[2][1];  // all tiles
+  const uint64_t n_large = ac & 0xFFFFFFFFull, n_small = ac >> 32;
+  if (tid == 0) {
+    // workgroups for the small list: its share of the CU time, a small-list
+    // byte weighted small_cost/4 against a batch-kernel byte (config 4 forced
+    // to split, one box: weight 1 -> 2.90 ms per step, 1.5 -> 2.25, 2.5 ->
+    // 2.045, 3.5 -> 2.046, 5 -> 2.047, 7 -> 2.049, against 2.06-2.075
+    // unsplit; profiles/r02/small_kernel/)
+    const uint64_t ws = p.small_cost * as, wl = 4 * al;
+    uint64_t wgs = p.grid;
+    if (n_large) wgs = ws ? (p.grid * ws + ws + wl - 1) / (ws + wl) : 0;
+    // split when the small list is worth at least two workgroups (a
+    // workgroup given to a handful of small buffers would idle a CU)
+    const uint32_t mode = n_small && (p.force || wgs >= 2);
+    if (n_large) wgs = wgs < 1 ? 1 : (wgs > p.grid - 1 ? p.grid - 1 : wgs);
+    s_mode = mode;
+    if (blockIdx.x == 0) {  // totals: the batch kernel's count, prefix end and the small list
+      const uint64_t nl = mode ? n_large : p.n;
+      p.prefix_c[nl] = mode ? al : al + as;
+      p.counts[0] = nl;
+      p.counts[1] = mode ? n_small : 0;
+      p.counts[2] = mode;
+      p.counts[3] = mode && as <= 2048 * n_small ? 8 : 16;  // mean small length <= 2 KiB: 8 lanes
+      p.counts[4] = wgs;
     }
   }
   __syncthreads();
   const bool split = s_mode != 0;
-  uint64_t bytes = 0, cnt = 0;
+  // byte prefix of this tile's batch-kernel buffers (all of them without a
+  // split) along (k, lane) = index order, wave carries; their count from ballots
+  uint64_t ex[kPlanPerThread], bcarry = 0;
+  uint32_t cx[kPlanPerThread], ccarry = 0, rank[kPlanPerThread], cls[kPlanPerThread];
 #pragma unroll
   for (uint32_t k = 0; k < kPlanPerThread; k++) {
-    const uint64_t idx = base + k;
-    if (idx < p.n) {
-      const bool large = !split || v[k] > kSmallMax;
-      bytes += large ? v[k] : 0;
-      cnt += large ? 1ull : 1ull << 32;
-    }
-  }
-  uint64_t tb;
-  uint64_t rb = s_off[0] + block_excl_scan(bytes, s_b, &tb);
-  if (!split) {  // the plain prefix (plan_tile_scan's), counts {n, 0, 0}
+    const bool in = base + 64u * k < p.n;
+    const bool large = in && (!split || v[k] > kSmallMax);
+    const uint64_t x = large ? v[k] : 0;
+    const uint64_t inc = wave_incl_scan(x);
+    ex[k] = bcarry + inc - x;
+    bcarry += __shfl(inc, 63, 64);
+    const uint64_t m = __ballot(large);
+    cx[k] = ccarry + (uint32_t)__popcll(m & lt);
+    ccarry += (uint32_t)__popcll(m);
+    // small: rank among this (wave, k) group's lanes of the same class
+    cls[k] = in && !large ? size_class(v[k]) : 63u;
+    uint64_t match = ~0ull;
 #pragma unroll
-    for (uint32_t k = 0; k < kPlanPerThread; k++) {
-      const uint64_t idx = base + k;
-      if (idx >= p.n) break;
-      p.prefix_c[idx] = rb;
-      p.out[idx] = 0u;  // split pieces xor into it
-      rb += v[k];
-      if (idx + 1 == p.n) p.prefix_c[p.n] = rb, p.counts[0] = p.n, p.counts[1] = 0, p.counts[2] = 0, p.counts[3] = 16;
+    for (int bit = 0; bit < 6; bit++) {
+      const uint64_t b = __ballot((cls[k] >> bit) & 1u);
+      match &= ((cls[k] >> bit) & 1u) ? b : ~b;
     }
-    return;
+    rank[k] = (uint32_t)__popcll(match & lt);
+    if (split && cls[k] < kSizeClasses && rank[k] == 0) s_cls[cls[k] * kGroups + wv * kPlanPerThread + k] = (uint32_t)__popcll(match);
   }
-  if (threadIdx.x == 0) {  // where this tile's entries of each class start
-    uint64_t at = 0;
-    for (uint32_t c = 0; c < kSizeClasses; c++) s_cls_at[c] = at + s_cls_prev[c], at += s_cls_all[c];
+  if (lane == 0) s_wb[wv] = bcarry, s_wc[wv] = ccarry;
+  __syncthreads();
+  uint64_t boff = 0;
+  uint32_t coff = 0;
+  for (uint32_t j = 0; j < wv; j++) boff += s_wb[j], coff += s_wc[j];
+  const uint64_t b0 = (split ? s_tw[0][0] : s_tw[0][0] + s_tw[1][0]) + boff;  // earlier tiles + earlier waves
+  const uint64_t pc = s_tw[2][0];
+  const uint64_t c0 = (split ? (pc & 0xFFFFFFFFull) : (uint64_t)blockIdx.x * kPlanTile) + coff;
+  if (split) {
+    // exclusive positions over (class, wave, k): thread t scans 5 consecutive entries
+    constexpr uint32_t kPer = (kSizeClasses * kGroups + 1023) / 1024;
+    uint32_t loc[kPer];
+    uint64_t sum = 0;
+#pragma unroll
+    for (uint32_t e = 0; e < kPer; e++) {
+      const uint32_t i = tid * kPer + e;
+      loc[e] = i < kSizeClasses * kGroups ? s_cls[i] : 0u;
+      sum += loc[e];
+    }
+    uint64_t tot;
+    uint64_t run = block_excl_scan(sum, s_tmp, &tot);  // (its barriers order the reads above)
+#pragma unroll
+    for (uint32_t e = 0; e < kPer; e++) {
+      const uint32_t i = tid * kPer + e;
+      if (i < kSizeClasses * kGroups) s_cls[i] = (uint32_t)run;
+      run += loc[e];
+    }
+    __syncthreads();
   }
-  uint64_t tc;
-  uint64_t rc = s_off[1] + block_excl_scan(cnt, s_c, &tc);  // (its barriers order s_cls_at)
+  const uint64_t s0 = pc >> 32;  // earlier tiles' small buffers
 #pragma unroll
   for (uint32_t k = 0; k < kPlanPerThread; k++) {
-    const uint64_t idx = base + k;
+    const uint64_t idx = base + 64u * k;
     if (idx >= p.n) break;
-    if (v[k] > kSmallMax) {
-      const uint64_t j = rc & 0xFFFFFFFFull;
-      p.prefix_c[j] = rb;
-      p.ptrs_c[j] = pv[k];
-      if (p.seeds) p.seeds_c[j] = sv[k];
-      p.oidx[j] = (uint32_t)idx;
-      p.out[idx] = 0u;
-      rb += v[k];
-      rc += 1;
+    if (cls[k] == 63u) {  // batch kernel
+      const uint64_t j = c0 + cx[k];
+      p.prefix_c[j] = b0 + ex[k];
+      if (split) {
+        p.ptrs_c[j] = pv[k];
+        if (p.seeds) p.seeds_c[j] = sv[k];
+        p.oidx[j] = (uint32_t)idx;
+      }
+      p.out[idx] = 0u;  // split pieces xor into it
     } else {
-      const uint32_t c = size_class(v[k]);
-      p.sidx[s_cls_at[c] + atomicAdd(&s_cls_cur[c], 1u)] = (uint32_t)idx;
-      rc += 1ull << 32;
-    }
-    if (idx + 1 == p.n) {  // totals
-      p.prefix_c[rc & 0xFFFFFFFFull] = rb;
-      p.counts[0] = rc & 0xFFFFFFFFull;
-      p.counts[1] = rc >> 32;
-      p.counts[2] = 1;
-      p.counts[3] = s_small_bytes <= 2048 * (rc >> 32) ? 8 : 16;  // mean small length <= 2 KiB: 8 lanes
-      p.counts[4] = s_small_wgs;
+      p.sidx[s0 + s_cls[cls[k] * kGroups + wv * kPlanPerThread + k] + rank[k]] = (uint32_t)idx;
     }
   }
 }
 
 hipError_t launch_plan_split(const SplitPlan &p, hipStream_t stream) {
   const uint64_t tiles = plan_tiles(p.n);
-  hipLaunchKernelGGL(plan_split_sums, dim3((unsigned)tiles), dim3(1024), 0, stream, p);
-  hipLaunchKernelGGL(plan_split_scan, dim3((unsigned)tiles), dim3(1024), 0, stream, p);
+  SplitPlan q = p;
+  q.tile_pre = tiles > kPlanDirectTiles ? p.tile_pre : nullptr;
+  hipLaunchKernelGGL(plan_split_count, dim3((unsigned)tiles), dim3(1024), 0, stream, q);
+  if (q.tile_pre) hipLaunchKernelGGL(plan_split_tiles, dim3(1), dim3(1024), 0, stream, q, (uint32_t)tiles);
+  hipLaunchKernelGGL(plan_split_scatter, dim3((unsigned)tiles), dim3(1024), 0, stream, q);
   return hipGetLastError();
 }
 

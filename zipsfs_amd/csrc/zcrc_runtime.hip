@@ -240,14 +240,15 @@ uint32_t dyn_shift_setting() {
 // and the fork's event cost ~8 us before the batch kernel:
 // profiles/r02/small_kernel/.)  Scratch, in bytes:
 struct SplitScratch {
-  size_t counts, prefix, tiles, ptrs, seeds, oidx, sidx, total;
+  size_t counts, prefix, tiles, tile_pre, ptrs, seeds, oidx, sidx, total;
   explicit SplitScratch(size_t n) {
     // [n_large, n_small, split, small lanes per buffer, small workgroups]
     // (SplitPlan::counts): in the counter area, off the counter's cache line
     counts = 128;
     prefix = kCtrBytes;
     tiles = prefix + 8 * (n + 1);
-    ptrs = tiles + 8 * kTileWords * plan_tiles(n);
+    tile_pre = tiles + 8 * kTileWords * plan_tiles(n);
+    ptrs = tile_pre + 8 * kTileWords * (plan_tiles(n) + 1);
     seeds = ptrs + 8 * n;
     oidx = seeds + 4 * n;
     sidx = oidx + 4 * n;
@@ -285,6 +286,7 @@ int batch_device_split(const DeviceCtx &dc, const void *const *d_ptrs, const uin
   p.seeds = d_seeds;
   p.n = n;
   p.tile_sum = reinterpret_cast<uint64_t *>(b + L.tiles);
+  p.tile_pre = reinterpret_cast<uint64_t *>(b + L.tile_pre);
   p.prefix_c = reinterpret_cast<uint64_t *>(b + L.prefix);
   p.ptrs_c = reinterpret_cast<const uint8_t **>(b + L.ptrs);
   p.seeds_c = reinterpret_cast<uint32_t *>(b + L.seeds);
@@ -835,6 +837,13 @@ struct HostTrace {
   double us[5] = {0, 0, 0, 0, 0};  // lease, slot wait, copy, enqueue, final wait
   int launches = 0, slots = 0;
   size_t bytes = 0;
+  double worst_us = 0;       // slowest single queueing call ...
+  const char *worst = "";    // ... which
+  int worst_launch = -1;     // ... in which launch of the call
+  void call(const char *what, clk::time_point t) {
+    const double d = std::chrono::duration<double, std::micro>(clk::now() - t).count();
+    if (d > worst_us) worst_us = d, worst = what, worst_launch = launches;
+  }
   void lap(int k) {
     const clk::time_point t = clk::now();
     us[k] += std::chrono::duration<double, std::micro>(t - mark).count();
@@ -844,9 +853,9 @@ struct HostTrace {
     fprintf(stderr,
             "{\"zcrc_trace_host\": {\"bytes\": %zu, \"slots\": %d, \"launches\": %d, \"lease_us\": %.1f, "
             "\"slot_wait_us\": %.1f, \"copy_us\": %.1f, \"enqueue_us\": %.1f, \"final_wait_us\": %.1f, "
-            "\"total_us\": %.1f}}\n",
+            "\"total_us\": %.1f, \"worst_call\": \"%s\", \"worst_call_us\": %.1f, \"worst_launch\": %d}}\n",
             bytes, slots, launches, us[0], us[1], us[2], us[3], us[4],
-            std::chrono::duration<double, std::micro>(clk::now() - t0).count());
+            std::chrono::duration<double, std::micro>(clk::now() - t0).count(), worst, worst_us, worst_launch);
   }
 };
 
@@ -965,8 +974,15 @@ int batch_host(const void *const *ptrs, const size_t *lens, const uint32_t *seed
     const size_t meta_bytes = off_seeds + 4 * items;
     memmove(s.h_meta + off_prefix, h_prefix, 8 * (items + 1));
     memmove(s.h_meta + off_seeds, h_seeds, 4 * items);
-    ZCRC_HIP_TRY(hipMemcpyAsync(s.d_data, s.h_data, used, hipMemcpyHostToDevice, s.stream));
-    ZCRC_HIP_TRY(hipMemcpyAsync(s.d_meta, s.h_meta, meta_bytes, hipMemcpyHostToDevice, s.stream));
+    // ZCRC_TRACE_HOST: the slowest queueing call of the call (first-use costs)
+#define ZCRC_TRACED(what, expr)                         \
+  do {                                                  \
+    const HostTrace::clk::time_point tq_ = HostTrace::clk::now(); \
+    ZCRC_HIP_TRY(expr);                                 \
+    if (trace) tr.call(what, tq_);                      \
+  } while (0)
+    ZCRC_TRACED("h2d data", hipMemcpyAsync(s.d_data, s.h_data, used, hipMemcpyHostToDevice, s.stream));
+    ZCRC_TRACED("h2d meta", hipMemcpyAsync(s.d_meta, s.h_meta, meta_bytes, hipMemcpyHostToDevice, s.stream));
     uint32_t *d_seeds = reinterpret_cast<uint32_t *>(s.d_meta + off_seeds);
     uint32_t *d_res = reinterpret_cast<uint32_t *>(s.d_meta + kMetaRes);
     // The copies above overlap the previous launch's kernel; everything below
@@ -974,11 +990,11 @@ int batch_host(const void *const *ptrs, const size_t *lens, const uint32_t *seed
     // a continuation's read of the other slot's results ahead of that slot's
     // next memset.
     if (prev_slot >= 0 && prev_slot != cur)
-      ZCRC_HIP_TRY(hipStreamWaitEvent(s.stream, lease.slot[prev_slot]->kernel, 0));
+      ZCRC_TRACED("wait event", hipStreamWaitEvent(s.stream, lease.slot[prev_slot]->kernel, 0));
     if (continuation) {
       StageSlot &p = *lease.slot[prev_slot];
-      ZCRC_HIP_TRY(hipMemcpyAsync(d_seeds, reinterpret_cast<uint32_t *>(p.d_meta + kMetaRes) + prev_item, 4,
-                                  hipMemcpyDeviceToDevice, s.stream));
+      ZCRC_TRACED("d2d seed", hipMemcpyAsync(d_seeds, reinterpret_cast<uint32_t *>(p.d_meta + kMetaRes) + prev_item,
+                                             4, hipMemcpyDeviceToDevice, s.stream));
     }
     const uint8_t *const *d_ptrs = reinterpret_cast<const uint8_t *const *>(s.d_meta + kMetaPtrs);
     const uint64_t *d_prefix = reinterpret_cast<const uint64_t *>(s.d_meta + off_prefix);
@@ -991,9 +1007,11 @@ int batch_host(const void *const *ptrs, const size_t *lens, const uint32_t *seed
       a.n = n_large;
       a.tab = dc->d_tab;
       // split pieces xor into d_res: zero it first
-      ZCRC_HIP_TRY(hipMemsetAsync(d_res, 0, 4 * n_large, s.stream));
+      ZCRC_TRACED("memset", hipMemsetAsync(d_res, 0, 4 * n_large, s.stream));
+      const HostTrace::clk::time_point tl = HostTrace::clk::now();
       rc = launch_main(a, false, *dc, s.stream);
       if (rc) return rc;
+      if (trace) tr.call("launch", tl);
     }
     if (n_small) {
       SmallArgs a{};
@@ -1006,9 +1024,10 @@ int batch_host(const void *const *ptrs, const size_t *lens, const uint32_t *seed
       rc = launch_small_timed(a, false, small_lanes(small_mean), *dc, s.stream);
       if (rc) return rc;
     }
-    ZCRC_HIP_TRY(hipEventRecord(s.kernel, s.stream));
-    ZCRC_HIP_TRY(hipMemcpyAsync(s.h_meta + kMetaRes, d_res, 4 * items, hipMemcpyDeviceToHost, s.stream));
-    ZCRC_HIP_TRY(hipEventRecord(s.done, s.stream));
+    ZCRC_TRACED("record kernel", hipEventRecord(s.kernel, s.stream));
+    ZCRC_TRACED("d2h results", hipMemcpyAsync(s.h_meta + kMetaRes, d_res, 4 * items, hipMemcpyDeviceToHost, s.stream));
+    ZCRC_TRACED("record done", hipEventRecord(s.done, s.stream));
+#undef ZCRC_TRACED
     s.busy = true;
     prev_slot = cur;
     prev_item = last_item;
@@ -1672,6 +1691,7 @@ int zcrc32_prewarm(size_t staging_slots) {
   DeviceCtx *dc = nullptr;
   int rc = device_ctx(&dc);
   if (rc) return rc;
+  (void)CopyPool::get();  // its threads start now, not in the first staged call
   int dev = 0;
   ZCRC_HIP_TRY(hipGetDevice(&dev));
   size_t have = 0;
