@@ -100,6 +100,15 @@ int zcrc32_batch_device_ws(const void *const *d_ptrs, const uint64_t *d_lens,
                            const uint32_t *d_seeds_or_null, uint32_t *d_out, size_t n,
                            void *d_scratch, size_t scratch_bytes, void *stream);
 
+/* Integrity check of the last zcrc32_batch_device / _ws launch on a scratch
+ * (d_scratch, or NULL for the stream's own cached one): synchronizes `stream`
+ * and sets *faults nonzero when the CRC kernel found inconsistent length-
+ * prefix bounds in the scratch (a corrupted scratch -- e.g. written by
+ * another stream -- makes the kernel skip those buffers, with result 0,
+ * instead of reading outside them).  Batches of at most 16 x CUs buffers use
+ * no prefix and report 0. */
+int zcrc32_batch_device_faults(const void *d_scratch_or_null, void *stream, uint32_t *faults);
+
 /* Device-resident batch of equal-size chunks: buffer i = d_base + i*stride,
  * each `len` bytes (fixed-size cache chunks).  One launch per 4 TiB, plus a
  * memset of d_out when chunks may be split across waves and, for batches of
@@ -169,7 +178,9 @@ int zcrc32_stream_stats(const zcrc32_stream *s, uint64_t *dma_pieces, uint64_t *
                         uint64_t *pageable_pieces);
 
 /* Device initialisation plus up to `staging_slots` pinned staging slots,
- * created now -- call it at startup (ZIPsFS: before the preload threads),
+ * created now and exercised by two staged calls (~20 ms once; the HIP
+ * runtime's first few SDMA copies of a process can block their caller for
+ * milliseconds) -- call it at startup (ZIPsFS: before the preload threads),
  * outside any lock.  The drop-in never creates a slot itself (it runs under
  * mutex_fhandle): a call that finds none free answers from the host CRC and
  * a background thread creates one for the next call. */

@@ -123,8 +123,8 @@ static int preload_once(const char *path, int mode, ref_fn ref, result_t *r) {
     zcrc32_stream_close(s);
     r->close_us = now_us() - t;
   }
-  if (use_mmap && !reuse) munmap(dst, st_size ? st_size : 1);
-  else free(dst);
+  if (!use_mmap) free(dst);
+  else if (!reuse) munmap(dst, st_size ? st_size : 1);
   close(fd);
   return 0;
 }

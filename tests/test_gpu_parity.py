@@ -743,3 +743,32 @@ def test_scratch_growth_is_stream_ordered(fused, monkeypatch):
             ap = np.array([host.ctypes.data + q for q in offs], dtype=np.uint64)
             exp = o.crc32_batch(ap, np.array(ln, dtype=np.uint64), np.zeros(len(ln), dtype=np.uint32), nthreads=8)
             np.testing.assert_array_equal(u32(got), exp, err_msg=f"rep {rep} n={len(ln)}")
+
+
+@pytest.mark.parametrize("n", [20_000, 9_000])
+def test_corrupted_prefix_is_caught_not_walked(n, monkeypatch):
+    """A zeroed quarter of the length prefix after the plan (the round-1/2
+    fault: an unordered memset over the scratch) makes the CRC kernel skip the
+    inconsistent pieces (result 0) and set the scratch's fault word, instead
+    of reading outside every buffer; with the hook off the same batch is
+    bit-exact and reports no fault."""
+    rnd = np.random.default_rng(n)
+    lens = rnd.integers(9000, 300_000, n).astype(np.int64)  # no small buffers: the plain prefix
+    offs = np.zeros(n, dtype=np.int64)
+    offs[1:] = np.cumsum(lens + 5)[:-1]
+    mem = torch.randint(0, 256, (int(offs[-1] + lens[-1] + 64),), dtype=torch.uint8, device=DEV)
+    ptrs = mem.data_ptr() + torch.tensor(offs, device=DEV)
+    lt = torch.tensor(lens, device=DEV)
+    host = mem.cpu().numpy()  # kept alive while the oracle reads it
+    exp = o.crc32_batch((host.ctypes.data + offs).astype(np.uint64), lens.astype(np.uint64), None, nthreads=16)
+    got = z.crc32_batch_device(ptrs, lt).cpu().numpy().view(np.uint32)
+    np.testing.assert_array_equal(got, exp)
+    assert z.batch_device_faults() == 0
+    monkeypatch.setenv("ZCRC_TEST_CORRUPT_PREFIX", "1")
+    bad = z.crc32_batch_device(ptrs, lt).cpu().numpy().view(np.uint32)
+    assert z.batch_device_faults() != 0
+    assert (bad != exp).any()
+    monkeypatch.delenv("ZCRC_TEST_CORRUPT_PREFIX")
+    got = z.crc32_batch_device(ptrs, lt).cpu().numpy().view(np.uint32)
+    np.testing.assert_array_equal(got, exp)
+    assert z.batch_device_faults() == 0

@@ -285,7 +285,8 @@ def test_split_batches_overlapping_on_four_streams():
 
 def _split_lists(scratch, n):
     """The split plan's outputs in caller-owned scratch (SplitScratch,
-    zcrc_runtime.hip): counts, prefix_c, oidx, sidx."""
+    zcrc_runtime.hip): counts, prefix_c, oidx, and the small list's buffer
+    indices (word 2 of each 16-B descriptor), pointers and lengths."""
     raw = scratch.cpu().numpy()
     T = -(-n // 8192)
     prefix = 256
@@ -294,10 +295,10 @@ def _split_lists(scratch, n):
     ptrs = tile_pre + 24 * (T + 1)
     seeds = ptrs + 8 * n
     oidx = seeds + 4 * n
-    sidx = oidx + 4 * n
+    sdesc = (oidx + 4 * n + 15) // 16 * 16
     counts = raw[128:168].view(np.uint64)
     return (counts, raw[prefix:prefix + 8 * (n + 1)].view(np.uint64), raw[oidx:oidx + 4 * n].view(np.uint32),
-            raw[sidx:sidx + 4 * n].view(np.uint32))
+            raw[sdesc:sdesc + 16 * n].view(np.uint32).reshape(n, 4))
 
 
 @pytest.mark.parametrize("n,shape", [(20_000, "mixed"), (50_000, "all_small"), (4_200_000, "mixed"),
@@ -322,14 +323,18 @@ def test_split_plan_lists_equal_the_model(n, shape):
     lt = torch.tensor(lens, device=DEV)
     scratch = torch.empty(z.scratch_bytes(n), dtype=torch.uint8, device=DEV)
     got = u32(z.crc32_batch_device_ws(ptrs, lt, scratch))
-    counts, prefix, oidx, sidx = _split_lists(scratch, n)
+    counts, prefix, oidx, sdesc = _split_lists(scratch, n)
     model = km.split_plan(lens.tolist(), grid=z.device_info()["num_cus"])
     assert bool(counts[2]) == model["split"], counts
     if model["split"]:
         nl, ns = int(counts[0]), int(counts[1])
         assert (nl, ns) == (len(model["large"]), len(model["small"]))
         np.testing.assert_array_equal(oidx[:nl], np.array(model["large"], dtype=np.uint32))
-        np.testing.assert_array_equal(sidx[:ns], np.array(model["small"], dtype=np.uint32))
+        small = np.array(model["small"], dtype=np.int64)
+        np.testing.assert_array_equal(sdesc[:ns, 2], small.astype(np.uint32))
+        pw = sdesc[:ns, 0].astype(np.uint64) | (sdesc[:ns, 1].astype(np.uint64) << np.uint64(32))
+        np.testing.assert_array_equal(pw >> np.uint64(48), lens[small].astype(np.uint64))
+        np.testing.assert_array_equal(pw & np.uint64((1 << 48) - 1), (mem.data_ptr() + offs[small]).astype(np.uint64))
         large_lens = lens[model["large"]]
         np.testing.assert_array_equal(prefix[:nl + 1], np.concatenate([[0], np.cumsum(large_lens)]).astype(np.uint64))
         assert int(counts[3]) == model["lanes"] and int(counts[4]) == model["wgs"], counts

@@ -109,6 +109,7 @@ int main(int argc, char **argv) {
   BatchArgs a{};
   a.ptrs = reinterpret_cast<const uint8_t *const *>(dp);
   a.prefix = dpre;
+  a.lens = dl;  // round 3: the kernel checks each piece's prefix bounds against the lengths
   a.n = nbuf;
   a.tab = d_tab;
   a.ctr = ctr;
@@ -116,8 +117,15 @@ int main(int argc, char **argv) {
   const double bytes = (double)prefix[nbuf];
   printf("crc_ab: %llu buffers, %.2f GiB (%s), %d CUs, %d rounds\n", (unsigned long long)nbuf, bytes / (1 << 30),
          len ? "uniform" : "zipf", cus, rounds);
+  // AB_B_NOWIN: B is the working tree's kernel with the piece-descriptor
+  // windows off (kWin = false)
+#ifdef AB_B_NOWIN
+  kfn ka = va::crc32_batch_kernel<false, 4u, 0, true, false, 1, 2>;
+  kfn kb = vb::crc32_batch_kernel<false, 4u, 0, true, false, 1, 2, false, false>;
+#else
   kfn ka = va::crc32_batch_kernel<false, 4u, 0, true, false, 1, 2>;
   kfn kb = vb::crc32_batch_kernel<false, 4u, 0, true, false, 1, 2>;
+#endif
   BatchArgs aa = a, ab = a;
   aa.out = outa;
   ab.out = outb;

@@ -255,6 +255,16 @@ def scratch_bytes(n: int) -> int:
     return int(lib().zcrc32_batch_device_scratch_bytes(n))
 
 
+def batch_device_faults(scratch=None, stream=None) -> int:
+    """zcrc32_batch_device_faults: nonzero when the last device batch on
+    ``scratch`` (or the stream's cached scratch) met an inconsistent length
+    prefix and skipped those buffers instead of reading outside them."""
+    v = ctypes.c_uint32(0)
+    check(lib().zcrc32_batch_device_faults(None if scratch is None else scratch.data_ptr(), _stream_ptr(stream),
+                                           ctypes.byref(v)), "zcrc32_batch_device_faults")
+    return int(v.value)
+
+
 def crc32_batch_strided(base, stride: int, length: int, n: int, seeds=None, out=None, stream=None,
                         base_offset: int = 0):
     """Equal-size chunks: buffer i = base + base_offset + i*stride, ``length`` bytes."""

@@ -65,6 +65,16 @@ __device__ __forceinline__ uint32_t braid_step(const uint32_t *lds, uint32_t x, 
   return lds_u32(lds, a0) ^ lds_u32(lds, a1) ^ lds_u32(lds, a2) ^ lds_u32(lds, a3);
 }
 
+// Lane i gets lane i + d's value, d < 16, inside its 16-lane row (DPP
+// row_shl; lanes past the row end get 0).  The folds below only read it in
+// lanes whose source is in the same row, where it equals __shfl_down(x, d) --
+// which went through ds_bpermute, an LDS round trip per level.
+template <int kD>
+__device__ __forceinline__ uint32_t row_shl(uint32_t x) {
+  static_assert(kD >= 1 && kD < 16, "row_shl:1..15");
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x100 + kD, 0xF, 0xF, false);
+}
+
 // r * c for one of the 8 combine constants resident in LDS.
 __device__ __forceinline__ uint32_t comb_apply(const uint32_t *lds, int c, uint32_t r) {
   const uint32_t *t = lds + kLdsCombDword + c * 1024;
@@ -320,13 +330,26 @@ struct BatchView {
 // ------------------------------------------------------------ plan scan
 // Exclusive prefix helpers for the plan (zcrc_kernels.hip) and the fused plan.
 
+// One DPP step of a 64-bit wave scan: each half moved by the same DPP
+// control (lanes without a source, or outside row_mask, read 0).
+template <int kCtrl, int kRowMask>
+__device__ __forceinline__ uint64_t dpp64(uint64_t v) {
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)v, kCtrl, kRowMask, 0xF, false);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)(v >> 32), kCtrl, kRowMask, 0xF, false);
+  return (uint64_t)lo | ((uint64_t)hi << 32);
+}
+
+// Inclusive wave64 scan in DPP steps (row_shr 1/2/4/8 inside 16-lane rows,
+// then row_bcast 15/31 across rows): a few VALU cycles per step.  The
+// __shfl_up form went through ds_bpermute, an LDS round trip per step:
+// 148 of them and 6.9 us per plan_split_scatter launch (tools/plan_probe).
 __device__ __forceinline__ uint64_t wave_incl_scan(uint64_t v) {
-  const uint32_t lane = threadIdx.x & 63u;
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    const uint64_t o = __shfl_up(v, d, 64);
-    if (lane >= (uint32_t)d) v += o;
-  }
+  v += dpp64<0x111, 0xF>(v);  // row_shr:1
+  v += dpp64<0x112, 0xF>(v);  // row_shr:2
+  v += dpp64<0x114, 0xF>(v);  // row_shr:4
+  v += dpp64<0x118, 0xF>(v);  // row_shr:8
+  v += dpp64<0x142, 0xA>(v);  // row_bcast:15 -> rows 1, 3
+  v += dpp64<0x143, 0xC>(v);  // row_bcast:31 -> rows 2, 3
   return v;
 }
 
@@ -397,6 +420,7 @@ __device__ __forceinline__ uint32_t piece_raw(const uint32_t *s_lds, const uint8
 struct PieceWindow {
   uint64_t i, b0, b1, p;
   uint32_t s, o;  // o: result index (split plan: oidx[i])
+  uint64_t len;   // the caller's length of the buffer (~0: not known), to check b1 - b0 against
 };
 
 template <bool kStrided>
@@ -410,6 +434,7 @@ __device__ __forceinline__ void load_window(const BatchView<kStrided> &bv, uint6
   w.p = reinterpret_cast<uint64_t>(bv.ptr(w.i));
   w.s = bv.seed(w.i);
   if (!kStrided && bv.a.oidx) w.o = bv.a.oidx[w.i];
+  w.len = !kStrided && bv.a.lens ? bv.a.lens[bv.a.oidx ? w.o : w.i] : ~0ull;
 }
 
 // Per-wave rotated visiting order.  Pieces are independent, and the rotation
@@ -444,15 +469,16 @@ __device__ __forceinline__ uint64_t process_range(const BatchArgs &args, const B
   uint64_t done = 0;
   if (kPrio && band) __builtin_amdgcn_s_setprio(3);
 
-  PieceWindow win{0, 0, 0, 0, 0, 0};  // kWin: the current window
+  PieceWindow win{0, 0, 0, 0, 0, 0, 0};  // kWin: the current window
   for (uint64_t k = 0; k < npieces; k++) {
-    uint64_t i, b0, b1;
+    uint64_t i, b0, b1, blen = ~0ull;
     if (kWin && !kStrided) {
       const uint32_t kk = (uint32_t)(k & 63u);
       if (kk == 0) load_window(bv, i_first, npieces, rot, k, lane, win);
       i = rdlane64(win.i, kk);
       b0 = rdlane64(win.b0, kk);
       b1 = rdlane64(win.b1, kk);
+      blen = rdlane64(win.len, kk);
     } else {
       i = i_first + k + rot;
       if (i >= i_end) i -= npieces;
@@ -481,6 +507,19 @@ __device__ __forceinline__ uint64_t process_range(const BatchArgs &args, const B
       seed = uni32(bv.seed(i));
       bptr = reinterpret_cast<const uint8_t *>(uni64(reinterpret_cast<uint64_t>(bv.ptr(i))));
       if (!kStrided && args.oidx) oi = uni32(args.oidx[i]);
+    }
+
+    // A prefix that disagrees with the caller's lengths (corrupted scratch --
+    // the round-1/2 fault: an unordered memset zero-filled it under queued
+    // launches) must not send the piece walk outside the buffer: the piece is
+    // skipped, its result zeroed, and the scratch's fault word set
+    // (zcrc32_batch_device_faults).
+    if (b1 < b0 || rel_lo > rel_hi || rel_hi > n || (blen != ~0ull && n != blen)) {
+      if (lane == 0) {
+        args.out[oi] = 0u;
+        if (args.fault) atomicOr(args.fault, 1u);
+      }
+      continue;
     }
 
     if (n < 4) {  // tiny buffer: bytewise with the standard table (never split)
@@ -660,12 +699,19 @@ __device__ __forceinline__ uint32_t piece_raw(const uint32_t *s_lds, const uint8
     // ---- fold 256 stream registers into one raw register at `aend` -------
     // stream (lane l, dword q) sits at aend + 16 l + 4 q
     uint32_t r = (s0 ^ comb_apply(s_lds, 0, s1)) ^ comb_apply(s_lds, 1, s2 ^ comb_apply(s_lds, 0, s3));
-#pragma unroll
-    for (int j = 0; j < 6; j++) {
-      const uint32_t moved = __shfl_down(comb_apply(s_lds, 2 + j, r), 1u << j, 64);
-      r ^= moved;
+    // cross-lane levels x^(-128 * 2^j): j < 4 inside 16-lane rows (DPP);
+    // the last two on the four row results, read into scalars
+    r ^= row_shl<1>(comb_apply(s_lds, 2, r));
+    r ^= row_shl<2>(comb_apply(s_lds, 3, r));
+    r ^= row_shl<4>(comb_apply(s_lds, 4, r));
+    r ^= row_shl<8>(comb_apply(s_lds, 5, r));
+    {
+      const uint32_t r0 = uni32(r);
+      const uint32_t r16 = (uint32_t)__builtin_amdgcn_readlane((int)r, 16);
+      const uint32_t r32 = (uint32_t)__builtin_amdgcn_readlane((int)r, 32);
+      const uint32_t r48 = (uint32_t)__builtin_amdgcn_readlane((int)r, 48);
+      r = uni32(r0 ^ comb_apply(s_lds, 6, r16) ^ comb_apply(s_lds, 7, r32 ^ comb_apply(s_lds, 6, r48)));
     }
-    r = uni32(r);
     const uint64_t tt0 = kStamp ? __builtin_amdgcn_s_memrealtime() : 0;
     if (tpad) r = shift_back(s_lds, r, tpad);  // -> register at pend
     if (kStamp) r = uni32(r), *t_tail += __builtin_amdgcn_s_memrealtime() - tt0;  // diagnostic: padding MCT
@@ -693,7 +739,7 @@ __global__ __launch_bounds__(kThreads) void crc32_batch_kernel(BatchArgs args) {
         SmallArgs sa{};
         sa.ptrs = args.ptrs;
         sa.lens = args.lens;
-        sa.sidx = args.sidx;
+        sa.sdesc = args.sdesc;
         sa.seeds = args.seeds;
         sa.out = args.out;
         sa.tab = args.tab;

@@ -72,22 +72,25 @@ struct BatchArgs {
   const uint32_t *oidx;
   const uint8_t *const *ptrs_split;
   const uint32_t *seeds_split;
-  const uint32_t *sidx;  // the split plan's small list (with lens, ptrs, seeds)
+  const uint4 *sdesc;    // the split plan's small list: SmallArgs::sdesc
+  uint32_t *fault;       // nullable: set to nonzero when a piece's prefix bounds are inconsistent
 };
+constexpr size_t kFaultByte = 192;  // the fault word's offset in a scratch's counter area (kCtrBytes)
 
 // Small-buffer kernel (zcrc_small_kernel.h): whole buffers of at most
 // kSmallMax bytes, 8 or 16 lanes per buffer.  General form: entry k of the
-// list is buffer j = sidx ? sidx[k] : k with ptrs[j], length lens[j] (or
-// prefix[j+1] - prefix[j] when lens is null), seeds[j], out[j]; the count is
-// n.  Strided form: buffer k = base + k*stride of length len.  The split
-// plan's small list runs inside the batch kernel's launch instead
-// (crc32_batch_kernel, BatchArgs::sidx).
+// list is buffer j = k with ptrs[j], length lens[j] (or prefix[j+1] -
+// prefix[j] when lens is null), seeds[j], out[j] -- or, with sdesc, the
+// pointer, length, index j and seed of sdesc[k]; the count is n.  Strided
+// form: buffer k = base + k*stride of length len.  The split plan's small
+// list (sdesc) runs inside the batch kernel's launch (crc32_batch_kernel,
+// BatchArgs::sdesc).
 constexpr uint64_t kSmallMax = 8192;
 struct SmallArgs {
   const uint8_t *const *ptrs;
   const uint64_t *lens;
   const uint64_t *prefix;
-  const uint32_t *sidx;
+  const uint4 *sdesc;  // split plan: entry k = {pointer | length << 48 (2 words), buffer index, seed}
   const uint8_t *base;
   uint64_t stride;
   uint64_t len;
@@ -133,7 +136,7 @@ hipError_t launch_plan(const uint64_t *d_lens, uint64_t n, uint64_t *d_prefix, u
 
 // Split plan (device batches of more than kFusedMaxN buffers).  When buffers
 // of at most kSmallMax bytes are worth at least two of the batch kernel's
-// workgroups (zcrc_kernels.hip), they are listed for the small-buffer kernel (sidx, count counts[1]) and the
+// workgroups (zcrc_kernels.hip), they are listed for the small-buffer kernel (sdesc, count counts[1]) and the
 // others compacted, in order, into a batch for the batch kernel (ptrs_c,
 // seeds_c, prefix_c, original index oidx, count counts[0]); counts[2] = 1.
 // Otherwise prefix_c is the plain prefix of all n buffers, counts = {n, 0,
@@ -151,12 +154,14 @@ struct SplitPlan {
   uint64_t *prefix_c;     // n + 1
   const uint8_t **ptrs_c;
   uint32_t *seeds_c;      // written when seeds != nullptr
-  uint32_t *oidx, *sidx, *out;
+  uint32_t *oidx, *out;
+  uint4 *sdesc;           // the small list, one 16-B descriptor per entry (SmallArgs::sdesc)
   uint64_t *counts;       // [0] n_large, [1] n_small, [2] split, [3] small lanes per buffer, [4] small workgroups
   uint32_t grid;          // the batch kernel's workgroups
   uint32_t small_cost;    // CU time of a small-list byte, in quarters of a batch-kernel byte
   uint32_t force;
   uint32_t *ctr;          // the batch kernel's work counter (zeroed)
+  uint64_t *stamps;       // diagnostics (tools/plan_probe): 8 s_memrealtime stamps per scatter workgroup, or null
 };
 hipError_t launch_plan_split(const SplitPlan &p, hipStream_t stream);
 constexpr uint32_t kSizeClasses = kSmallMax / 256 + 1;  // small list order: 256-B block count

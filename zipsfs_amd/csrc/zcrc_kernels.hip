@@ -41,7 +41,7 @@ __global__ __launch_bounds__(1024) void plan_tile_scan(const uint64_t *lens, uin
                                                        uint32_t *ctr) {
   __shared__ uint64_t s_tmp[16];
   __shared__ uint64_t s_off;
-  if (ctr && blockIdx.x == 0 && threadIdx.x == 0) *ctr = 0u;  // the CRC kernel's work counter
+  if (ctr && blockIdx.x == 0 && threadIdx.x == 0) ctr[0] = 0u, ctr[kFaultByte / 4] = 0u;  // work counter, fault word
   if (threadIdx.x < 64) {
     uint64_t acc = 0;
     for (uint32_t b = threadIdx.x; b < blockIdx.x; b += 64) acc += tile_sum[b];
@@ -84,7 +84,7 @@ __global__ __launch_bounds__(1024) void plan_one_tile(const uint64_t *lens, uint
   __shared__ uint64_t s_wsum[16];
   const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
   const uint64_t base = (uint64_t)wv * (64u * kPlanPerThread);
-  if (ctr && threadIdx.x == 0) *ctr = 0u;  // the CRC kernel's work counter
+  if (ctr && threadIdx.x == 0) ctr[0] = 0u, ctr[kFaultByte / 4] = 0u;  // the CRC kernel's work counter, fault word
   uint64_t v[kPlanPerThread];
 #pragma unroll
   for (uint32_t k = 0; k < kPlanPerThread; k++) {
@@ -97,7 +97,7 @@ __global__ __launch_bounds__(1024) void plan_one_tile(const uint64_t *lens, uint
   for (uint32_t k = 0; k < kPlanPerThread; k++) {
     const uint64_t inc = wave_incl_scan(v[k]);
     v[k] = carry + inc - v[k];  // exclusive within the wave's 512 buffers
-    carry += __shfl(inc, 63, 64);
+    carry += rdlane64(inc, 63);
   }
   if (lane == 0) s_wsum[wv] = carry;
   __syncthreads();
@@ -153,9 +153,10 @@ __global__ __launch_bounds__(1024) void plan_split_count(SplitPlan p) {
     if (L > kSmallMax) bl += L, cnt += 1;
     else bs += L, cnt += 1ull << 32;
   }
-#pragma unroll
-  for (int d = 32; d >= 1; d >>= 1)
-    bl += __shfl_xor(bl, d, 64), bs += __shfl_xor(bs, d, 64), cnt += __shfl_xor(cnt, d, 64);
+  // wave totals: DPP scans, lane 63 (butterflies of __shfl_xor were LDS round trips)
+  bl = rdlane64(wave_incl_scan(bl), 63);
+  bs = rdlane64(wave_incl_scan(bs), 63);
+  cnt = rdlane64(wave_incl_scan(cnt), 63);
   if (lane == 0) s_w[wv][0] = bl, s_w[wv][1] = bs, s_w[wv][2] = cnt;
   __syncthreads();
   if (threadIdx.x < 3) {
@@ -196,7 +197,9 @@ __global__ __launch_bounds__(1024) void plan_split_scatter(SplitPlan p) {
   __shared__ uint32_t s_cls[kSizeClasses * kGroups];  // small count per (class, group) -> exclusive position
   const uint32_t tid = threadIdx.x, lane = tid & 63u, wv = tid >> 6;
   const uint64_t lt = (1ull << lane) - 1;
-  if (blockIdx.x == 0 && tid == 0) *p.ctr = 0u;  // the CRC kernel's work counter
+  uint64_t st[6] = {0, 0, 0, 0, 0, 0};  // diagnostics: phase stamps (p.stamps)
+  if (p.stamps) st[0] = __builtin_amdgcn_s_memrealtime();
+  if (blockIdx.x == 0 && tid == 0) p.ctr[0] = 0u, p.ctr[kFaultByte / 4] = 0u;  // work counter, fault word
   const uint64_t base = (uint64_t)blockIdx.x * kPlanTile + 512u * wv + lane;
   // this thread's lengths, pointers and seeds first (coalesced)
   uint64_t v[kPlanPerThread];
@@ -221,12 +224,13 @@ __global__ __launch_bounds__(1024) void plan_split_scatter(SplitPlan p) {
       all += x;
       if (t < blockIdx.x) prev += x;
     }
-#pragma unroll
-    for (int d = 32; d >= 1; d >>= 1) all += __shfl_xor(all, d, 64), prev += __shfl_xor(prev, d, 64);
+    all = rdlane64(wave_incl_scan(all), 63);
+    prev = rdlane64(wave_incl_scan(prev), 63);
     if (lane == 0) s_tw[wv][0] = prev, s_tw[wv][1] = all;
   }
   for (uint32_t i = tid; i < kSizeClasses * kGroups; i += 1024) s_cls[i] = 0u;
   __syncthreads();
+  if (p.stamps) st[1] = __builtin_amdgcn_s_memrealtime();
   const uint64_t al = s_tw[0][1], as = s_tw[1][1], ac = s_tw[2][1];  // all tiles
   const uint64_t n_large = ac & 0xFFFFFFFFull, n_small = ac >> 32;
   if (tid == 0) {
@@ -254,6 +258,7 @@ __global__ __launch_bounds__(1024) void plan_split_scatter(SplitPlan p) {
     }
   }
   __syncthreads();
+  if (p.stamps) st[2] = __builtin_amdgcn_s_memrealtime();
   const bool split = s_mode != 0;
   // byte prefix of this tile's batch-kernel buffers (all of them without a
   // split) along (k, lane) = index order, wave carries; their count from ballots
@@ -266,23 +271,27 @@ __global__ __launch_bounds__(1024) void plan_split_scatter(SplitPlan p) {
     const uint64_t x = large ? v[k] : 0;
     const uint64_t inc = wave_incl_scan(x);
     ex[k] = bcarry + inc - x;
-    bcarry += __shfl(inc, 63, 64);
+    bcarry += rdlane64(inc, 63);
     const uint64_t m = __ballot(large);
     cx[k] = ccarry + (uint32_t)__popcll(m & lt);
     ccarry += (uint32_t)__popcll(m);
     // small: rank among this (wave, k) group's lanes of the same class
     cls[k] = in && !large ? size_class(v[k]) : 63u;
-    uint64_t match = ~0ull;
+    rank[k] = 0;
+    if (split) {  // uniform: without a split every buffer is the batch kernel's
+      uint64_t match = ~0ull;
 #pragma unroll
-    for (int bit = 0; bit < 6; bit++) {
-      const uint64_t b = __ballot((cls[k] >> bit) & 1u);
-      match &= ((cls[k] >> bit) & 1u) ? b : ~b;
+      for (int bit = 0; bit < 6; bit++) {
+        const uint64_t b = __ballot((cls[k] >> bit) & 1u);
+        match &= ((cls[k] >> bit) & 1u) ? b : ~b;
+      }
+      rank[k] = (uint32_t)__popcll(match & lt);
+      if (cls[k] < kSizeClasses && rank[k] == 0) s_cls[cls[k] * kGroups + wv * kPlanPerThread + k] = (uint32_t)__popcll(match);
     }
-    rank[k] = (uint32_t)__popcll(match & lt);
-    if (split && cls[k] < kSizeClasses && rank[k] == 0) s_cls[cls[k] * kGroups + wv * kPlanPerThread + k] = (uint32_t)__popcll(match);
   }
   if (lane == 0) s_wb[wv] = bcarry, s_wc[wv] = ccarry;
   __syncthreads();
+  if (p.stamps) st[3] = __builtin_amdgcn_s_memrealtime();
   uint64_t boff = 0;
   uint32_t coff = 0;
   for (uint32_t j = 0; j < wv; j++) boff += s_wb[j], coff += s_wc[j];
@@ -310,6 +319,7 @@ __global__ __launch_bounds__(1024) void plan_split_scatter(SplitPlan p) {
     }
     __syncthreads();
   }
+  if (p.stamps) st[4] = __builtin_amdgcn_s_memrealtime();
   const uint64_t s0 = pc >> 32;  // earlier tiles' small buffers
 #pragma unroll
   for (uint32_t k = 0; k < kPlanPerThread; k++) {
@@ -325,8 +335,16 @@ __global__ __launch_bounds__(1024) void plan_split_scatter(SplitPlan p) {
       }
       p.out[idx] = 0u;  // split pieces xor into it
     } else {
-      p.sidx[s0 + s_cls[cls[k] * kGroups + wv * kPlanPerThread + k] + rank[k]] = (uint32_t)idx;
+      // the small list's descriptor: pointer (48-bit VA) | length << 48, index, seed
+      const uint64_t pw = reinterpret_cast<uint64_t>(pv[k]) | (v[k] << 48);
+      p.sdesc[s0 + s_cls[cls[k] * kGroups + wv * kPlanPerThread + k] + rank[k]] =
+          make_uint4((uint32_t)pw, (uint32_t)(pw >> 32), (uint32_t)idx, sv[k]);
     }
+  }
+  if (p.stamps && tid == 0) {
+    __builtin_amdgcn_s_waitcnt(0);
+    st[5] = __builtin_amdgcn_s_memrealtime();
+    for (int i = 0; i < 6; i++) p.stamps[8 * blockIdx.x + i] = st[i];
   }
 }
 

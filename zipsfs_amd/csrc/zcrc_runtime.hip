@@ -240,7 +240,7 @@ uint32_t dyn_shift_setting() {
 // and the fork's event cost ~8 us before the batch kernel:
 // profiles/r02/small_kernel/.)  Scratch, in bytes:
 struct SplitScratch {
-  size_t counts, prefix, tiles, tile_pre, ptrs, seeds, oidx, sidx, total;
+  size_t counts, prefix, tiles, tile_pre, ptrs, seeds, oidx, sdesc, total;
   explicit SplitScratch(size_t n) {
     // [n_large, n_small, split, small lanes per buffer, small workgroups]
     // (SplitPlan::counts): in the counter area, off the counter's cache line
@@ -251,8 +251,8 @@ struct SplitScratch {
     ptrs = tile_pre + 8 * kTileWords * (plan_tiles(n) + 1);
     seeds = ptrs + 8 * n;
     oidx = seeds + 4 * n;
-    sidx = oidx + 4 * n;
-    total = sidx + 4 * n;
+    sdesc = (oidx + 4 * n + 15) & ~size_t(15);
+    total = sdesc + 16 * n;
   }
 };
 static_assert(kCtrBytes >= 128 + 5 * 8, "the five split counts share the counter area");
@@ -276,6 +276,15 @@ bool split_forced() {
   return e && e[0] == '2';
 }
 
+// Test hook (ZCRC_TEST_CORRUPT_PREFIX=1, read per call): zero a quarter of
+// the prefix after the plan, as the unordered scratch memset of rounds 1-2
+// did, so that tests/test_gpu_parity.py can check the CRC kernel's guard.
+hipError_t test_corrupt_prefix(uint64_t *prefix, size_t n, hipStream_t stream) {
+  const char *e = getenv("ZCRC_TEST_CORRUPT_PREFIX");
+  if (!e || e[0] != '1' || n < 8) return hipSuccess;
+  return hipMemsetAsync(prefix + n / 2, 0, 8 * (n / 4), stream);
+}
+
 int batch_device_split(const DeviceCtx &dc, const void *const *d_ptrs, const uint64_t *d_lens,
                        const uint32_t *d_seeds, uint32_t *d_out, size_t n, void *scratch, hipStream_t stream) {
   uint8_t *b = static_cast<uint8_t *>(scratch);
@@ -291,7 +300,7 @@ int batch_device_split(const DeviceCtx &dc, const void *const *d_ptrs, const uin
   p.ptrs_c = reinterpret_cast<const uint8_t **>(b + L.ptrs);
   p.seeds_c = reinterpret_cast<uint32_t *>(b + L.seeds);
   p.oidx = reinterpret_cast<uint32_t *>(b + L.oidx);
-  p.sidx = reinterpret_cast<uint32_t *>(b + L.sidx);
+  p.sdesc = reinterpret_cast<uint4 *>(b + L.sdesc);
   p.out = d_out;
   p.counts = reinterpret_cast<uint64_t *>(b + L.counts);
   p.ctr = reinterpret_cast<uint32_t *>(b);
@@ -309,12 +318,14 @@ int batch_device_split(const DeviceCtx &dc, const void *const *d_ptrs, const uin
   a.n_dev = p.counts;
   a.oidx = p.oidx;
   a.lens = d_lens;
-  a.sidx = p.sidx;
+  a.sdesc = p.sdesc;
   a.tab = dc.d_tab;
   a.ctr = p.ctr;
   a.dyn_shift = dyn_shift_setting();
   a.dyn_unit = dyn_unit_override();
+  a.fault = reinterpret_cast<uint32_t *>(b + kFaultByte);
   ZCRC_HIP_TRY(launch_plan_split(p, stream));
+  ZCRC_HIP_TRY(test_corrupt_prefix(p.prefix_c, n, stream));
   return launch_main(a, false, dc, stream);
 }
 
@@ -344,6 +355,9 @@ int batch_device_ws(const void *const *d_ptrs, const uint64_t *d_lens, const uin
   a.ctr = d_ctr;
   a.dyn_shift = dyn_shift_setting();
   a.dyn_unit = dyn_unit_override();
+  a.fault = reinterpret_cast<uint32_t *>(static_cast<uint8_t *>(scratch) + kFaultByte);
+  a.lens = d_lens;  // the kernel checks every piece's prefix bounds against it
+  ZCRC_HIP_TRY(test_corrupt_prefix(d_prefix, n, stream));
   return launch_main(a, false, *dc, stream);
 }
 
@@ -821,6 +835,18 @@ int batch_host_direct(const DeviceCtx &dc, StageSlot &s, const void *const *ptrs
 // kBusy: no staging slot was free and the caller asked not to wait
 constexpr int kBusy = 1;
 
+// Staged launches read the pinned copy over PCIe (the kernel's loads, from
+// the slot's device view of its pinned pages) instead of an SDMA copy into
+// HBM first: as fast or faster per call (drop-in lock hold, same box: 16 MiB
+// 574 vs 667 us, 64 MiB 1.57 vs 1.98 ms, 256 MiB 5.64 vs 5.59 ms), and no
+// SDMA copy call ever blocks the caller -- one of them blocked it for 8-19 ms
+// now and then (ZCRC_TRACE_HOST, profiles/r03/s5-s8).  ZCRC_STAGE_ZEROCOPY=0
+// (read per call) restores the SDMA copy (measurement).
+bool stage_zerocopy() {
+  const char *e = getenv("ZCRC_STAGE_ZEROCOPY");
+  return !(e && e[0] == '0');
+}
+
 // Diagnostics (ZCRC_TRACE_HOST=1): per-phase wall time of each staged host
 // call, one JSON line on stderr -- lease, waits for a slot's previous launch,
 // copies into pinned memory, queueing, the final wait.
@@ -898,6 +924,8 @@ int batch_host(const void *const *ptrs, const size_t *lens, const uint32_t *seed
     std::vector<CopyJob> jobs;
     std::vector<uint8_t> is_small;  // item is a whole buffer of <= kSmallMax bytes
     const bool small_on = small_enabled();
+    const bool zerocopy = stage_zerocopy();
+    uint8_t *const data_view = zerocopy ? s.h_data_dev : s.d_data;  // what the kernel reads
     bool continuation = false;  // item 0 continues the previous launch's last item
     uint64_t pos = 0;
     while (i < n && items < kStageItems) {
@@ -909,7 +937,7 @@ int batch_host(const void *const *ptrs, const size_t *lens, const uint32_t *seed
       const size_t take = std::min(remaining, room);
       if (take && !src) return fail(ZCRC_ERR_ARG, "null buffer pointer");
       if (take) jobs.push_back({s.h_data + used, src + part_off, take});
-      h_ptrs[items] = reinterpret_cast<uint64_t>(s.d_data + used);
+      h_ptrs[items] = reinterpret_cast<uint64_t>(data_view + used);
       h_prefix[items] = pos;
       h_seeds[items] = (part_off == 0 && seeds) ? seeds[i] : 0u;
       if (part_off != 0) continuation = true;  // only ever item 0
@@ -981,7 +1009,8 @@ int batch_host(const void *const *ptrs, const size_t *lens, const uint32_t *seed
     ZCRC_HIP_TRY(expr);                                 \
     if (trace) tr.call(what, tq_);                      \
   } while (0)
-    ZCRC_TRACED("h2d data", hipMemcpyAsync(s.d_data, s.h_data, used, hipMemcpyHostToDevice, s.stream));
+    if (!zerocopy)
+      ZCRC_TRACED("h2d data", hipMemcpyAsync(s.d_data, s.h_data, used, hipMemcpyHostToDevice, s.stream));
     ZCRC_TRACED("h2d meta", hipMemcpyAsync(s.d_meta, s.h_meta, meta_bytes, hipMemcpyHostToDevice, s.stream));
     uint32_t *d_seeds = reinterpret_cast<uint32_t *>(s.d_meta + off_seeds);
     uint32_t *d_res = reinterpret_cast<uint32_t *>(s.d_meta + kMetaRes);
@@ -1359,6 +1388,24 @@ int zcrc32_batch_device(const void *const *d_ptrs, const uint64_t *d_lens, const
   return batch_device_ws(d_ptrs, d_lens, d_seeds_or_null, d_out, n, scratch, have, st);
 }
 
+int zcrc32_batch_device_faults(const void *d_scratch_or_null, void *stream, uint32_t *faults) {
+  if (!faults) return fail(ZCRC_ERR_ARG, "null faults");
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  const void *sc = d_scratch_or_null;
+  std::unique_lock<std::mutex> lk;
+  if (!sc) {
+    void *p = nullptr;
+    size_t have = 0;
+    const int rc = stream_scratch(st, kScratchBatch, 0, &p, &have, &lk);
+    if (rc) return rc;
+    sc = p;
+  }
+  ZCRC_HIP_TRY(hipStreamSynchronize(st));
+  *faults = 0;
+  if (sc) ZCRC_HIP_TRY(hipMemcpy(faults, static_cast<const uint8_t *>(sc) + kFaultByte, 4, hipMemcpyDeviceToHost));
+  return ZCRC_OK;
+}
+
 int zcrc32_batch_device_strided(const void *d_base, uint64_t stride, uint64_t len, size_t n,
                                 const uint32_t *d_seeds_or_null, uint32_t *d_out, void *stream) {
   if (n == 0) return ZCRC_OK;
@@ -1695,7 +1742,19 @@ int zcrc32_prewarm(size_t staging_slots) {
   int dev = 0;
   ZCRC_HIP_TRY(hipGetDevice(&dev));
   size_t have = 0;
-  return SlotPool::get().prewarm(dev, staging_slots, &have);
+  rc = SlotPool::get().prewarm(dev, staging_slots, &have);
+  if (rc || !have) return rc;
+  // Two staged calls of 4 slot-sizes each, the drop-in's own pattern (both
+  // slots, continuations, cross-stream waits): one of a process's first few
+  // 16 MiB pinned H2D copies blocked its caller for 8-19 ms inside the HIP
+  // runtime's SDMA copy (ZCRC_TRACE_HOST, profiles/r03/s5-s6), which the
+  // drop-in would otherwise pay under mutex_fhandle.
+  std::vector<uint8_t> zeros(4 * kStageBytes + 4096, 0);
+  const void *ptrs[1] = {zeros.data()};
+  const size_t lens[1] = {zeros.size()};
+  uint32_t crc = 0;
+  for (int r = 0; r < 2 && !rc; r++) rc = batch_host(ptrs, lens, nullptr, &crc, 1, true);
+  return rc;
 }
 
 int zcrc_staging_info(uint64_t *pinned_bytes, uint64_t *slots_in_use, uint64_t *slots_peak, uint64_t *slots_budget) {

@@ -54,7 +54,16 @@ __device__ __forceinline__ void small_body(const SmallArgs &a, uint32_t *s_lds, 
       p = reinterpret_cast<uint64_t>(a.base) + k * a.stride;
       l = a.len;
     } else {
-      j = a.sidx ? a.sidx[k] : k;
+      if (a.sdesc) {  // split plan: one 16-B load, no dependent descriptor loads
+        const uint4 d = a.sdesc[k];
+        const uint64_t pw = (uint64_t)d.x | ((uint64_t)d.y << 32);
+        j = d.z;
+        p = pw & 0xFFFFFFFFFFFFull;
+        l = pw >> 48;
+        sd = d.w;
+        return;
+      }
+      j = k;
       p = reinterpret_cast<uint64_t>(a.ptrs[j]);
       l = a.lens ? a.lens[j] : a.prefix[j + 1] - a.prefix[j];
     }
@@ -132,9 +141,12 @@ __device__ __forceinline__ void small_body(const SmallArgs &a, uint32_t *s_lds, 
     for (int t = 0; t < LOG_NS; t++)
 #pragma unroll
       for (int m = 0; m < NS; m += 2 << t) s[m] ^= comb_apply(s_lds, t, s[m + (1 << t)]);
+    // cross-lane levels inside the group (8 or 16 lanes: within a DPP row)
     uint32_t r = s[0];
-#pragma unroll
-    for (int t = 0; t < LOG_G; t++) r ^= __shfl_down(comb_apply(s_lds, LOG_NS + t, r), 1u << t, 64);
+    r ^= row_shl<1>(comb_apply(s_lds, LOG_NS + 0, r));
+    r ^= row_shl<2>(comb_apply(s_lds, LOG_NS + 1, r));
+    r ^= row_shl<4>(comb_apply(s_lds, LOG_NS + 2, r));
+    if (LOG_G == 4) r ^= row_shl<8>(comb_apply(s_lds, LOG_NS + 3, r));
     const uint32_t tpad = (uint32_t)(span - re), a4 = tpad >> 2;
     if (a4 & 2u) r = comb_apply(s_lds, 1, r);
     if (a4 & 1u) r = comb_apply(s_lds, 0, r);
