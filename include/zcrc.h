@@ -156,13 +156,16 @@ int zcrc_inflate_batch(const void *const *src, const size_t *src_len, void *cons
  *
  * zcrc32_stream_open_registered(seed, segment, bytes) also page-locks the
  * caller's preload segment (ZIPsFS: the entry's textbuffer segment,
- * src/cg_textbuffer.c:103-106) until close(): chunks inside it are DMA'd to
- * the GPU straight from it and update() returns at once, without copying.
+ * src/cg_textbuffer.c:103-106) until close(): the kernels read chunks inside
+ * it over PCIe straight from it, and update() returns at once, without
+ * copying (the update that completes the segment waits for its kernels, so
+ * that final() -- under the caller's lock -- has nothing left to wait for).
  * The segment must stay mapped, and its updated bytes unchanged, until
  * close().  If the segment cannot be registered the stream works as an
  * unregistered one.  Without registration update() copies each piece into a
- * pinned staging slot (never waiting for one: with every slot of the pool
- * leased, the HIP runtime copies from the pageable source itself).  Errors are sticky: after a
+ * pinned staging slot, which the kernel reads over PCIe (never waiting for a
+ * slot: with every slot of the pool leased, the HIP runtime copies from the
+ * pageable source into HBM itself).  Errors are sticky: after a
  * failed update() every later update() and final() return that error until
  * the stream is closed; a partial CRC is never returned. */
 typedef struct zcrc32_stream zcrc32_stream;
@@ -171,10 +174,10 @@ zcrc32_stream *zcrc32_stream_open_registered(uint32_t seed, const void *segment,
 int zcrc32_stream_update(zcrc32_stream *s, const void *data, size_t n_bytes);
 int zcrc32_stream_final(zcrc32_stream *s, uint32_t *crc);      /* stream stays usable */
 void zcrc32_stream_close(zcrc32_stream *s);
-/* How the stream's 4 MiB pieces went to the GPU: DMA from the registered
+/* How the stream's 4 MiB pieces went to the GPU: read from the registered
  * segment / copied through pinned staging / runtime-staged pageable copy (no
  * slot was free).  Every piece is checksummed on the GPU. */
-int zcrc32_stream_stats(const zcrc32_stream *s, uint64_t *dma_pieces, uint64_t *staged_pieces,
+int zcrc32_stream_stats(const zcrc32_stream *s, uint64_t *registered_pieces, uint64_t *staged_pieces,
                         uint64_t *pageable_pieces);
 
 /* Device initialisation plus up to `staging_slots` pinned staging slots,

@@ -105,15 +105,15 @@ for off in range(0, big[2].size, 16 << 20):
     t.update(big[2][off: off + (16 << 20)])
 assert t.final() == zlib.crc32(big[2].tobytes(), 9), "pageable stream pieces"
 st = t.stats()
-assert st["pageable"] == -(-big[2].size // (4 << 20)) and st["staged"] == 0 and st["dma"] == 0, st
+assert st["pageable"] == -(-big[2].size // (4 << 20)) and st["staged"] == 0 and st["registered"] == 0, st
 t.close()
-# a registered segment needs no slot at all: its pieces are DMA'd from it
+# a registered segment needs no slot at all: the kernels read its pieces in place
 seg = big[0].copy()
 r = z.Crc32Stream(segment=seg)
 for off in range(0, seg.size, 16 << 20):
     r.update(seg[off: off + (16 << 20)])
 assert r.final() == exp[0], "registered stream with the pool exhausted"
-assert r.stats() == {"dma": 10, "staged": 0, "pageable": 0}, r.stats()
+assert r.stats() == {"registered": 10, "staged": 0, "pageable": 0}, r.stats()
 r.close()
 assert s.final() == zlib.crc32(big[0][: 1 << 20].tobytes())
 assert s.stats()["staged"] == 1, s.stats()
@@ -129,7 +129,7 @@ def test_staging_pool_with_one_slot(tmp_path):
     launches through it, the waiting GPU path works, and while a stream holds
     the only slot a drop-in call is answered by the host CRC instead of
     waiting (it runs under mutex_fhandle), a second stream copies its pieces
-    from pageable memory, and a registered stream DMAs from its segment."""
+    from pageable memory, and a registered stream reads its segment in place."""
     import os
     import subprocess
     import sys

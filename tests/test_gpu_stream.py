@@ -1,13 +1,13 @@
 """GPU: the streaming CRC of preloadram_now with the
-caller's preload segment registered (zero-copy) and the stream's error
-contract.
+caller's preload segment registered (zero-copy: the kernels read it over
+PCIe) and the stream's error contract.
 
 ZIPsFS reads an entry into one mmap'd segment in <= 16 MiB zip_fread() chunks
 (src/ZIPsFS_preloadfileram.c:284-306, src/cg_textbuffer.c:103-106) and then
 checks the CRC under mutex_fhandle (:309-321).  A stream opened on the
-registered segment (zcrc32_stream_open_registered) DMAs each chunk straight
-from it; chunks outside it go through pinned staging; a failed update makes
-the stream fail until it is closed (never a partial CRC)."""
+registered segment (zcrc32_stream_open_registered) checksums each chunk
+where it lies; chunks outside it go through pinned staging; a failed update
+makes the stream fail until it is closed (never a partial CRC)."""
 import mmap
 import zlib
 
@@ -24,7 +24,7 @@ CHUNK = 16 << 20  # PRELOADRAM_READ_BYTES_NUM (src/ZIPsFS_configuration.h:112)
 
 
 @pytest.mark.parametrize("size,seed", [(64 << 20, 0), ((40 << 20) + 12345, 0xC0DE), (5 << 20, 3), (4096, 0)])
-def test_registered_segment_is_dmad(size, seed):
+def test_registered_segment_is_read_in_place(size, seed):
     seg = o.payload(size, 77)
     exp = zlib.crc32(seg.tobytes(), seed)
     with z.Crc32Stream(seed=seed, segment=seg) as s:
@@ -32,7 +32,7 @@ def test_registered_segment_is_dmad(size, seed):
             s.update(seg[off: off + CHUNK])
         assert s.final() == exp
         st = s.stats()
-    assert st == {"dma": -(-size // (4 << 20)), "staged": 0, "pageable": 0}, st
+    assert st == {"registered": -(-size // (4 << 20)), "staged": 0, "pageable": 0}, st
 
 
 def test_registered_mmap_segment_ragged_chunks_and_outside_data():
@@ -56,7 +56,7 @@ def test_registered_mmap_segment_ragged_chunks_and_outside_data():
     exp = zlib.crc32(other.tobytes(), exp)
     exp = zlib.crc32(seg[7 << 20:].tobytes(), exp)
     assert crc == exp
-    assert st["staged"] == 1 and st["pageable"] == 0 and st["dma"] >= 6, st
+    assert st["staged"] == 1 and st["pageable"] == 0 and st["registered"] >= 6, st
     del seg
     mm.close()
 

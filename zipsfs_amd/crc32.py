@@ -119,7 +119,7 @@ class Crc32Stream:
         """``segment``: optional writable host buffer (numpy array, mmap,
         bytearray) that the updates will come from -- the preload segment.  It
         is page-locked until ``close()`` (zcrc32_stream_open_registered), and
-        updates inside it are DMA'd from it without a copy; it must stay alive
+        updates inside it are read by the kernels in place, without a copy; it must stay alive
         and unchanged until then (this object keeps a reference)."""
         self._seg = None
         if segment is None:
@@ -131,7 +131,7 @@ class Crc32Stream:
         if not self._s:
             msg = lib().zcrc_last_error()
             raise ZcrcError(f"zcrc32_stream_open failed: {msg.decode() if msg else ''}")
-        self._keep = []  # registered updates are read by DMA after update() returns
+        self._keep = []  # registered updates are read by the GPU after update() returns
 
     def update(self, data) -> "Crc32Stream":
         keep, addr, nbytes = _host_view(data)
@@ -142,11 +142,11 @@ class Crc32Stream:
         return self
 
     def stats(self) -> dict:
-        """4 MiB pieces DMA'd from the registered segment / copied through
+        """4 MiB pieces read from the registered segment / copied through
         pinned staging / copied from pageable memory (no staging slot free)."""
         v = [ctypes.c_uint64() for _ in range(3)]
         check(lib().zcrc32_stream_stats(self._s, *[ctypes.byref(x) for x in v]), "zcrc32_stream_stats")
-        return dict(zip(["dma", "staged", "pageable"], [x.value for x in v]))
+        return dict(zip(["registered", "staged", "pageable"], [x.value for x in v]))
 
     def final(self) -> int:
         out = ctypes.c_uint32(0)
