@@ -772,13 +772,18 @@ __global__ __launch_bounds__(kThreads) void crc32_batch_kernel(BatchArgs args) {
   // the same banks: 3.6 us of bank conflicts per launch).
   const uint32_t tid = threadIdx.x;
   uint32_t braid_val[8];
+  uint4 comb0, comb1;
+  auto load_tables = [&]() {
 #pragma unroll
-  for (int k = 0; k < 8; k++) {
-    const uint32_t o = 16u * (tid + 1024u * k);
-    braid_val[k] = tab->braid[(((o >> 16) << 1) | ((o >> 7) & 1u)) * 256u + ((o >> 8) & 255u)];
-  }
-  const uint4 *comb_src = reinterpret_cast<const uint4 *>(tab->comb);
-  const uint4 comb0 = comb_src[tid], comb1 = comb_src[tid + 1024u];
+    for (int k = 0; k < 8; k++) {
+      const uint32_t o = 16u * (tid + 1024u * k);
+      braid_val[k] = tab->braid[(((o >> 16) << 1) | ((o >> 7) & 1u)) * 256u + ((o >> 8) & 255u)];
+    }
+    const uint4 *comb_src = reinterpret_cast<const uint4 *>(tab->comb);
+    comb0 = comb_src[tid];
+    comb1 = comb_src[tid + 1024u];
+  };
+  if (!kFused) load_tables();
 
   // Fused small batch: every workgroup scans the <= kFusedMaxN lengths itself
   // (thread t owns buffers 8t .. 8t+7) while the table loads are in flight,
@@ -789,13 +794,6 @@ __global__ __launch_bounds__(kThreads) void crc32_batch_kernel(BatchArgs args) {
   if (kFused) {
     static_assert(kFusedMaxN == 8u * kThreads, "fused scan: 8 lengths per thread");
     static_assert((kFusedMaxN + 1 + 16) * 8 <= kLdsBytes, "fused scan fits in LDS");
-    uint64_t v[8], sum = 0;
-#pragma unroll
-    for (uint32_t k = 0; k < 8; k++) {
-      const uint64_t idx = 8u * tid + k;
-      v[k] = idx < args.n ? args.lens[idx] : 0;
-      sum += v[k];
-    }
     // Per-buffer mode: no more buffers than waves and none longer than
     // kPerBufMax.  The two-launch path would then give every wave at most one
     // range of whole buffers (W = n, no splits); here wave slot s of workgroup
@@ -805,16 +803,26 @@ __global__ __launch_bounds__(kThreads) void crc32_batch_kernel(BatchArgs args) {
     if (args.n <= (uint64_t)grid * kWaves) {
       const uint32_t lane = tid & 63u, slot = uni32(tid >> 6);
       const uint64_t b = (uint64_t)slot * grid + blockIdx.x;
+      // The decision's lengths first, coalesced (thread t: buffers t + 1024 j),
+      // then the wave's descriptor, the tables and the buffer's first blocks:
+      // vector loads return in issue order, so the barriers below wait for
+      // the lengths alone and the tables arrive meanwhile (tables first, then
+      // 8 strided length loads per thread, put the decision 6 us after entry:
+      // tools/c2_probe, profiles/r03/s10).
+      bool big = false;
+#pragma unroll
+      for (uint32_t j = 0; j < 8; j++) {
+        const uint64_t idx = tid + 1024u * j;
+        if (idx < args.n) big |= args.lens[idx] > kPerBufMax;
+      }
       uint64_t blen = 0, bp = 0;
       uint32_t bseed = 0;
-      if (b < args.n) {  // issued before the decision: in flight with the table loads
+      if (b < args.n) {
         blen = uni64(args.lens[b]);
         bp = uni64(reinterpret_cast<uint64_t>(args.ptrs[b]));
         bseed = args.seeds ? uni32(args.seeds[b]) : 0u;
       }
-      bool big = false;
-#pragma unroll
-      for (uint32_t k = 0; k < 8; k++) big |= v[k] > kPerBufMax;
+      load_tables();
       // the buffer's first 2 kD KiB, in flight across the decision, the LDS
       // fill and the barriers (used only if the mode is taken)
       const uint8_t *bptr = reinterpret_cast<const uint8_t *>(bp);
@@ -828,6 +836,7 @@ __global__ __launch_bounds__(kThreads) void crc32_batch_kernel(BatchArgs args) {
 #pragma unroll
       for (int s = 0; s < kWaves; s++) any_big |= flags[s];
       __syncthreads();  // every wave has read the flags
+      const uint64_t t_decide = kStamp ? __builtin_amdgcn_s_memrealtime() : 0;
       if (!any_big) {
         if (blockIdx.x >= args.n) return;  // whole workgroup idle (uniform: no barrier is skipped)
         uint4 *dst = reinterpret_cast<uint4 *>(s_lds);
@@ -839,6 +848,7 @@ __global__ __launch_bounds__(kThreads) void crc32_batch_kernel(BatchArgs args) {
         cdst[tid + 1024u] = comb1;
         __syncthreads();
         if (b >= args.n) return;  // no barrier after this point
+        const uint64_t t_fill = kStamp ? __builtin_amdgcn_s_memrealtime() : 0;
         // younger wave slots issue first: the SIMDs otherwise serve the
         // oldest waves first and the slots finish in four groups (+0.7% on
         // config 2 against none, -0.4% for the reverse order;
@@ -854,8 +864,24 @@ __global__ __launch_bounds__(kThreads) void crc32_batch_kernel(BatchArgs args) {
           r = piece_raw<kD, kAblate, kAux, false, true>(s_lds, bptr, 0, blen, bseed, lane, nullptr, pre);
         }
         if (lane == 0) args.out[b] = ~r;
+        if (kStamp && lane == 0) {  // diagnostic build (tools/c2_probe): this wave's timeline
+          const uint64_t w = (uint64_t)blockIdx.x * kWaves + slot;
+          args.stamps[8 * w + 0] = t_fill;
+          args.stamps[8 * w + 1] = __builtin_amdgcn_s_memrealtime();
+          args.stamps[8 * w + 4] = t_entry;
+          args.stamps[8 * w + 5] = t_decide;
+        }
         return;
       }
+    } else {
+      load_tables();
+    }
+    uint64_t v[8], sum = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < 8; k++) {
+      const uint64_t idx = 8u * tid + k;
+      v[k] = idx < args.n ? args.lens[idx] : 0;
+      sum += v[k];
     }
     uint64_t tot;
     uint64_t run = block_excl_scan(sum, lds_pre + kFusedMaxN + 8, &tot);
