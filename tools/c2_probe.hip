@@ -199,11 +199,12 @@ int main(int argc, char **argv) {
     uint64_t t0 = ~0ull;
     for (uint64_t w = 0; w < nw; w++)
       if (st[8 * w + 1]) t0 = std::min(t0, st[8 * w + 4]);
-    std::vector<double> entry, search, begin, end;
+    std::vector<double> entry, search, begin, end, lens;
     std::vector<double> slot_end[kWaves];
     for (uint64_t w = 0; w < nw; w++) {
       if (!st[8 * w + 1]) continue;
       entry.push_back((st[8 * w + 4] - t0) * 1e-2);
+      if (fused && st[8 * w + 6]) lens.push_back((st[8 * w + 6] - t0) * 1e-2);  // per-buffer mode: lengths in
       search.push_back((st[8 * w + 5] - t0) * 1e-2);
       begin.push_back((st[8 * w + 0] - t0) * 1e-2);
       end.push_back((st[8 * w + 1] - t0) * 1e-2);
@@ -214,6 +215,7 @@ int main(int argc, char **argv) {
       printf("  %-7s %6.2f %6.2f %6.2f\n", k, pct(v, 0), pct(v, .5), pct(v, 1));
     };
     row("entry", entry);
+    if (!lens.empty()) row("lengths", lens);
     row("search", search);
     row("begin", begin);
     row("end", end);

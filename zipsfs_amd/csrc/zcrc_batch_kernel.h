@@ -830,6 +830,7 @@ __global__ __launch_bounds__(kThreads) void crc32_batch_kernel(BatchArgs args) {
       piece_preload<kD, kAux>(bptr, 0, blen, lane, b < args.n && blen >= 4 && blen <= kPerBufMax, pre);
       uint32_t *flags = s_lds + kLdsCombDword;  // 16 words, overwritten by the fill after the second barrier
       const uint64_t m = __ballot(big);
+      const uint64_t t_lens = kStamp ? __builtin_amdgcn_s_memrealtime() : 0;  // after the lengths arrived
       if (lane == 0) flags[slot] = m ? 1u : 0u;
       __syncthreads();
       uint32_t any_big = 0;
@@ -870,6 +871,7 @@ __global__ __launch_bounds__(kThreads) void crc32_batch_kernel(BatchArgs args) {
           args.stamps[8 * w + 1] = __builtin_amdgcn_s_memrealtime();
           args.stamps[8 * w + 4] = t_entry;
           args.stamps[8 * w + 5] = t_decide;
+          args.stamps[8 * w + 6] = t_lens;
         }
         return;
       }
