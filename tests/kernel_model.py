@@ -424,6 +424,47 @@ def split_plan(lens, grid: int = 256, force: bool = False, small_cost: int = K_S
 K_PER_BUF_MAX = K_MIN_RANGE  # zcrc_internal.h kPerBufMax
 
 
+def braid_lds_loaded() -> np.ndarray:
+    """The batch kernel's LDS braid area (32768 words) as the table fill
+    writes it from TableBlob::braid (zcrc_batch_kernel.h, load_tables):
+    thread t writes the 16-B chunk c = t + 1024 k with 4 copies of
+    braid[j][v], j = 2 (o >> 16) + ((o >> 7) & 1), v = (o >> 8) & 255, o = 16 c."""
+    T = tables()
+    lds = np.zeros(32768, dtype=np.uint32)
+    for c in range(8192):
+        o = 16 * c
+        j = 2 * (o >> 16) + ((o >> 7) & 1)
+        v = (o >> 8) & 255
+        lds[4 * c:4 * c + 4] = T.braid[j, v]
+    return lds
+
+
+def braid_lds_built() -> np.ndarray:
+    """The per-buffer mode's braid (zcrc_batch_kernel.h, braid_gen_lane and
+    the ds_bpermute exchange): lane L of wave w builds entry (j = L >> 4,
+    v = 4 w + (L & 3) + 64 ((L >> 2) & 3)) from the 32 single-bit products
+    q[p] = x^8192 * (1 << p); thread (w, l) then writes chunk 64 w + l +
+    1024 k with lane src = (l >> 4) + 4 (k & 3) + 16 (2 (k >> 2) + ((l >> 3) & 1))'s entry."""
+    q = [gf2_mul(xpow8(1024), 1 << p) for p in range(32)]
+    lds = np.zeros(32768, dtype=np.uint32)
+    for w in range(16):
+        e = []
+        for L in range(64):
+            j, v = L >> 4, 4 * w + (L & 3) + 64 * ((L >> 2) & 3)
+            acc = 0
+            for b in range(8):
+                if (v >> b) & 1:
+                    acc ^= q[8 * j + b]
+            e.append(acc)
+        for l in range(64):
+            t = 64 * w + l
+            for k in range(8):
+                src = (l >> 4) + 4 * (k & 3) + 16 * (2 * (k >> 2) + ((l >> 3) & 1))
+                c = t + 1024 * k
+                lds[4 * c:4 * c + 4] = e[src]
+    return lds
+
+
 def per_buffer_plan(lens, num_cus: int = 256):
     """The one-launch kernel's per-buffer mode (zcrc_batch_kernel.h,
     crc32_batch_kernel, kFused): taken when n <= 16 x grid and no length

@@ -214,3 +214,25 @@ def test_per_buffer_mode_rule_and_mapping():
     assert km.per_buffer_plan([65537]) is None
     assert km.per_buffer_plan([1] * 4097) is None
     assert km.per_buffer_plan([1] * 4097, num_cus=512) is not None
+
+
+def test_per_buffer_braid_build_equals_loaded_fill():
+    """The per-buffer mode builds the braid in registers (no table load ahead
+    of its first barrier); every one of the 32,768 LDS words must equal what
+    the table fill writes from TableBlob::braid."""
+    assert np.array_equal(km.braid_lds_built(), km.braid_lds_loaded())
+
+
+def test_per_buffer_flags_sit_on_zero_combine_words():
+    """The per-buffer mode stores wave s's decision flag in the combine-area
+    word 256 s: the first word of the chunk lane 0 of wave s writes (chunk
+    64 s = table s >> 2, sub-table j = s & 3, v = 0), which is MCT(c)[j][0] =
+    0 in every table -- so an all-clear decision leaves the tables exact."""
+    T = km.tables()
+    comb = np.concatenate([t.reshape(-1) for t in T.comb])  # the kernel's comb area, 8 x 1024 words
+    for s in range(16):
+        chunk = 64 * s
+        assert 4 * chunk == 256 * s
+        c, j, v = chunk >> 8, (chunk >> 6) & 3, 4 * (chunk & 63)
+        assert (c, j, v) == (s >> 2, s & 3, 0)
+        assert comb[256 * s] == 0 and T.comb[c][j, 0] == 0

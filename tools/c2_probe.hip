@@ -13,7 +13,9 @@
 //   crc-fused    the one-launch kernel (scans the lengths itself)
 // and one stamped launch of each CRC form (s_memrealtime, 100 MHz) printed
 // as a timeline: kernel entry, range search done, LDS fill + barrier done,
-// wave end -- percentiles over all waves, relative to the first entry.
+// wave end -- percentiles over all waves, relative to the first entry.  The
+// per-buffer mode (crc-fused) stamps entry, its one barrier ("begin") and
+// its buffer's CRC stored ("end").
 //
 //   make -C tools c2_probe && tools/c2_probe [reps]
 #include <hip/hip_ext.h>
@@ -215,10 +217,15 @@ int main(int argc, char **argv) {
       printf("  %-7s %6.2f %6.2f %6.2f\n", k, pct(v, 0), pct(v, .5), pct(v, 1));
     };
     row("entry", entry);
-    if (!lens.empty()) row("lengths", lens);
-    row("search", search);
-    row("begin", begin);
-    row("end", end);
+    if (fused) {  // per-buffer mode (round 3): tables built and batch decided at its one barrier
+      if (!lens.empty()) row("lengths", lens);
+      row("begin", begin);
+      row("end", end);
+    } else {
+      row("search", search);
+      row("begin", begin);
+      row("end", end);
+    }
     printf("  end p50 by wave slot:");
     for (int s = 0; s < kWaves; s++) printf(" %.1f", slot_end[s].empty() ? 0.0 : pct(slot_end[s], .5));
     printf("\n");

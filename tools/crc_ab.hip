@@ -114,12 +114,25 @@ int main(int argc, char **argv) {
   a.tab = d_tab;
   a.ctr = ctr;
   a.dyn_shift = kDynShift;
+  uint64_t *acc;
+  uint32_t *done;
+  CHECK(hipMalloc(&acc, 8 * kFusedMaxN));
+  CHECK(hipMalloc(&done, 256));
+  CHECK(hipMemset(acc, 0, 8 * kFusedMaxN));
+  CHECK(hipMemset(done, 0, 256));
+  a.acc = acc;  // fused form only (AB_FUSED): split-piece cells and the finished-wave counter
+  a.done = done;
   const double bytes = (double)prefix[nbuf];
   printf("crc_ab: %llu buffers, %.2f GiB (%s), %d CUs, %d rounds\n", (unsigned long long)nbuf, bytes / (1 << 30),
          len ? "uniform" : "zipf", cus, rounds);
   // AB_B_NOWIN: B is the working tree's kernel with the piece-descriptor
   // windows off (kWin = false)
-#ifdef AB_B_NOWIN
+#if defined(AB_FUSED)
+  // AB_FUSED: both one-launch kernels (n <= 16 x CUs; the per-buffer mode
+  // when no buffer exceeds 64 KiB, else the in-kernel scan)
+  kfn ka = va::crc32_batch_kernel<false, 4u, 0, true, false, 1, 2, true>;
+  kfn kb = vb::crc32_batch_kernel<false, 4u, 0, true, false, 1, 2, true>;
+#elif defined(AB_B_NOWIN)
   kfn ka = va::crc32_batch_kernel<false, 4u, 0, true, false, 1, 2>;
   kfn kb = vb::crc32_batch_kernel<false, 4u, 0, true, false, 1, 2, false, false>;
 #else

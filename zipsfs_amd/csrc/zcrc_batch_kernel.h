@@ -46,6 +46,15 @@ namespace zcrc {
 // sustained HBM read rate by ~12% over the default policy on gfx950
 // (tools/hbm_probe, tools/crc_variants).
 constexpr int kLoadNt = 2;
+// per-buffer mode: issue each wave's first 2 kD KiB before its barrier (off:
+// measured no faster on 4096 x 64 KiB and 4-6% slower on 16 KiB and 1 KiB
+// buffers, because the payload then queues in front of the other waves'
+// table and length loads -- tools/crc_ab_fused_np, c2_probe_np,
+// profiles/r03/s15-s16; an A/B knob for those tools)
+#ifndef ZCRC_PERBUF_PRELOAD
+#define ZCRC_PERBUF_PRELOAD 0
+#endif
+constexpr bool kPerBufPreload = ZCRC_PERBUF_PRELOAD;
 
 __device__ __forceinline__ uint32_t lds_u32(const uint32_t *lds, uint32_t byte_addr) {
   return *reinterpret_cast<const uint32_t *>(reinterpret_cast<const char *>(lds) + byte_addr);
@@ -63,6 +72,33 @@ __device__ __forceinline__ uint32_t braid_step(const uint32_t *lds, uint32_t x, 
   const uint32_t a2 = __builtin_amdgcn_perm(x, o2, ZCRC_SEL(2));
   const uint32_t a3 = __builtin_amdgcn_perm(x, o3, ZCRC_SEL(3));
   return lds_u32(lds, a0) ^ lds_u32(lds, a1) ^ lds_u32(lds, a2) ^ lds_u32(lds, a3);
+}
+
+// The braid entry MCT(x^8192)[j][v] this lane builds for wave `w` of the
+// per-buffer mode: j = lane >> 4, v = 4 w + (lane & 3) + 64 ((lane >> 2) & 3),
+// as the xor of the compile-time products q[8j + b] over the set bits b of v
+// (MctBasis, zcrc_gf2.h).  ~40 VALU on immediates, no memory: the braid then
+// needs no load in front of the workgroup's first barrier.  (Selecting among
+// elements of a constexpr array compiled to a select of addresses and a load
+// from a constant table; MctQ makes every product an immediate.)  tests: the
+// per-buffer GPU parity tests read every entry through the hot loop, and
+// tests/test_model.py checks the construction against TableBlob::braid.
+template <int k, int p>
+struct MctQ {
+  static constexpr uint32_t value = MctBasis<k>{}.q[p];
+};
+template <int bit>
+__device__ __forceinline__ uint32_t braid_gen_bit(bool j1, bool j2, uint32_t v) {
+  const uint32_t q = j2 ? (j1 ? MctQ<13, 24 + bit>::value : MctQ<13, 16 + bit>::value)
+                        : (j1 ? MctQ<13, 8 + bit>::value : MctQ<13, bit>::value);
+  return ((v >> bit) & 1u) ? q : 0u;
+}
+__device__ __forceinline__ uint32_t braid_gen_lane(uint32_t lane, uint32_t w) {
+  const bool j1 = lane & 16u, j2 = lane & 32u;  // j = lane >> 4
+  const uint32_t v = 4u * w + (lane & 3u) + 64u * ((lane >> 2) & 3u);
+  return braid_gen_bit<0>(j1, j2, v) ^ braid_gen_bit<1>(j1, j2, v) ^ braid_gen_bit<2>(j1, j2, v) ^
+         braid_gen_bit<3>(j1, j2, v) ^ braid_gen_bit<4>(j1, j2, v) ^ braid_gen_bit<5>(j1, j2, v) ^
+         braid_gen_bit<6>(j1, j2, v) ^ braid_gen_bit<7>(j1, j2, v);
 }
 
 // Lane i gets lane i + d's value, d < 16, inside its 16-lane row (DPP
@@ -800,21 +836,38 @@ __global__ __launch_bounds__(kThreads) void crc32_batch_kernel(BatchArgs args) {
     // g takes buffer s * grid + g whole -- spread over every CU, with no
     // prefix, no range search and no plan.  Every workgroup reads all the
     // lengths, so all of them take the same decision.
+    //
+    // Round 3: one barrier, and nothing in front of it that waits behind the
+    // payload.  At entry each wave issues its share of the decision's
+    // lengths, its chunks of the combine tables and its descriptor; it
+    // builds its braid entries in registers (braid_gen_lane: no table load);
+    // it writes braid, combine tables and its decision flag, and meets the
+    // others at the barrier.  The flags need
+    // no LDS of their own: wave s's flag is the word of combine entry (c, j,
+    // v) = (s >> 2, s & 3, 0), which the same wave writes and which is 0 in
+    // every MCT -- so when no flag is set the tables are already right.
+    // (Round 2 decided first, behind two extra barriers, with the braid and
+    // the lengths loaded after every wave's preload was queued, and the
+    // guarded length loads waited for one at a time: the table fill
+    // completed 7.7 us after entry, now 3.5 us; tools/c2_probe,
+    // profiles/r03/s11, s16.)
     if (args.n <= (uint64_t)grid * kWaves) {
       const uint32_t lane = tid & 63u, slot = uni32(tid >> 6);
       const uint64_t b = (uint64_t)slot * grid + blockIdx.x;
-      // The decision's lengths first, coalesced (thread t: buffers t + 1024 j),
-      // then the wave's descriptor, the tables and the buffer's first blocks:
-      // vector loads return in issue order, so the barriers below wait for
-      // the lengths alone and the tables arrive meanwhile (tables first, then
-      // 8 strided length loads per thread, put the decision 6 us after entry:
-      // tools/c2_probe, profiles/r03/s10).
+      const bool wg_busy = blockIdx.x < args.n;  // workgroup-uniform
+      // the decision's lengths (thread t: buffers t + 1024 j) with clamped
+      // indices and no branch: a guarded load in its own block got its own
+      // vmcnt(0), so the eight round trips ran one after another
       bool big = false;
 #pragma unroll
       for (uint32_t j = 0; j < 8; j++) {
         const uint64_t idx = tid + 1024u * j;
-        if (idx < args.n) big |= args.lens[idx] > kPerBufMax;
+        const uint64_t L = args.lens[idx < args.n ? idx : args.n - 1];
+        big |= (idx < args.n) & (L > kPerBufMax);
       }
+      const uint4 *comb_src = reinterpret_cast<const uint4 *>(tab->comb);
+      const uint4 cm0 = comb_src[tid], cm1 = comb_src[tid + 1024u];  // unconditional: a guarded copy waited for them
+      __builtin_amdgcn_sched_barrier(0);  // issued before the wait for the descriptor below
       uint64_t blen = 0, bp = 0;
       uint32_t bseed = 0;
       if (b < args.n) {
@@ -822,34 +875,40 @@ __global__ __launch_bounds__(kThreads) void crc32_batch_kernel(BatchArgs args) {
         bp = uni64(reinterpret_cast<uint64_t>(args.ptrs[b]));
         bseed = args.seeds ? uni32(args.seeds[b]) : 0u;
       }
-      load_tables();
-      // the buffer's first 2 kD KiB, in flight across the decision, the LDS
-      // fill and the barriers (used only if the mode is taken)
+      const bool own = b < args.n && blen <= kPerBufMax;  // wave-uniform
       const uint8_t *bptr = reinterpret_cast<const uint8_t *>(bp);
       uint4 pre[2 * kD];
-      piece_preload<kD, kAux>(bptr, 0, blen, lane, b < args.n && blen >= 4 && blen <= kPerBufMax, pre);
-      uint32_t *flags = s_lds + kLdsCombDword;  // 16 words, overwritten by the fill after the second barrier
-      const uint64_t m = __ballot(big);
-      const uint64_t t_lens = kStamp ? __builtin_amdgcn_s_memrealtime() : 0;  // after the lengths arrived
-      if (lane == 0) flags[slot] = m ? 1u : 0u;
-      __syncthreads();
-      uint32_t any_big = 0;
-#pragma unroll
-      for (int s = 0; s < kWaves; s++) any_big |= flags[s];
-      __syncthreads();  // every wave has read the flags
-      const uint64_t t_decide = kStamp ? __builtin_amdgcn_s_memrealtime() : 0;
-      if (!any_big) {
-        if (blockIdx.x >= args.n) return;  // whole workgroup idle (uniform: no barrier is skipped)
+      if (kPerBufPreload) piece_preload<kD, kAux>(bptr, 0, blen, lane, own && blen >= 4, pre);
+      if (wg_busy) {
+        // braid chunk t + 1024 k holds entry (j, v) = (2 (k >> 2) + ((lane >> 3) & 1),
+        // 4 slot + (lane >> 4) + 64 (k & 3)) (the layout above): 64 distinct
+        // entries per wave, one built by each lane, exchanged by ds_bpermute
+        const uint32_t e = braid_gen_lane(lane, slot);
         uint4 *dst = reinterpret_cast<uint4 *>(s_lds);
 #pragma unroll
-        for (int k = 0; k < 8; k++)
-          dst[tid + 1024u * k] = make_uint4(braid_val[k], braid_val[k], braid_val[k], braid_val[k]);
+        for (uint32_t k = 0; k < 8; k++) {
+          const uint32_t src = (lane >> 4) + 4u * (k & 3u) + 16u * (2u * (k >> 2) + ((lane >> 3) & 1u));
+          const uint32_t val = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(src * 4u), (int)e);
+          dst[tid + 1024u * k] = make_uint4(val, val, val, val);
+        }
+      }
+      // chunk tid of the combine area is (table tid >> 8, j = (tid >> 6) & 3,
+      // v = 4 (tid & 63) .. +3): lane 0 of wave s holds entry (s >> 2, s & 3, 0)
+      // (the flag is a second write of that word, after the chunk's, by the
+      // same wave: a wave's LDS writes land in order)
+      const uint32_t flag = __ballot(big) ? 1u : 0u;
+      const uint64_t t_lens = kStamp ? __builtin_amdgcn_s_memrealtime() : 0;  // diagnostic: the lengths are in
+      if (wg_busy) {
         uint4 *cdst = reinterpret_cast<uint4 *>(s_lds + kLdsCombDword);
-        cdst[tid] = comb0;
-        cdst[tid + 1024u] = comb1;
-        __syncthreads();
-        if (b >= args.n) return;  // no barrier after this point
-        const uint64_t t_fill = kStamp ? __builtin_amdgcn_s_memrealtime() : 0;
+        cdst[tid] = cm0;
+        cdst[tid + 1024u] = cm1;
+      }
+      if (lane == 0) s_lds[kLdsCombDword + 256u * slot] = flag;
+      __syncthreads();  // the only barrier of the per-buffer mode
+      const uint64_t t_fill = kStamp ? __builtin_amdgcn_s_memrealtime() : 0;
+      const uint32_t fw = lane < (uint32_t)kWaves ? s_lds[kLdsCombDword + 256u * lane] : 0u;
+      if (!__ballot(fw != 0)) {  // workgroup-uniform: every wave read the same 16 words
+        if (b >= args.n || !wg_busy) return;
         // younger wave slots issue first: the SIMDs otherwise serve the
         // oldest waves first and the slots finish in four groups (+0.7% on
         // config 2 against none, -0.4% for the reverse order;
@@ -862,7 +921,7 @@ __global__ __launch_bounds__(kThreads) void crc32_batch_kernel(BatchArgs args) {
           r = ~bseed;
           for (uint32_t p = 0; p < (uint32_t)blen; p++) r = (r >> 8) ^ tab->stdtab[(r ^ bptr[p]) & 0xFFu];
         } else {
-          r = piece_raw<kD, kAblate, kAux, false, true>(s_lds, bptr, 0, blen, bseed, lane, nullptr, pre);
+          r = piece_raw<kD, kAblate, kAux, false, kPerBufPreload>(s_lds, bptr, 0, blen, bseed, lane, nullptr, pre);
         }
         if (lane == 0) args.out[b] = ~r;
         if (kStamp && lane == 0) {  // diagnostic build (tools/c2_probe): this wave's timeline
@@ -870,11 +929,14 @@ __global__ __launch_bounds__(kThreads) void crc32_batch_kernel(BatchArgs args) {
           args.stamps[8 * w + 0] = t_fill;
           args.stamps[8 * w + 1] = __builtin_amdgcn_s_memrealtime();
           args.stamps[8 * w + 4] = t_entry;
-          args.stamps[8 * w + 5] = t_decide;
+          args.stamps[8 * w + 5] = t_fill;
           args.stamps[8 * w + 6] = t_lens;
         }
         return;
       }
+      // some buffer is longer than kPerBufMax: the in-kernel scan below
+      __syncthreads();  // every wave has read the flags before the scan overwrites LDS
+      load_tables();
     } else {
       load_tables();
     }

@@ -33,7 +33,7 @@ constexpr uint32_t kPolyReflected = 0xEDB88320u;  // src/cg_crc32.c:11
 constexpr uint32_t kOne = 0x80000000u;            // x^0 in reflected order
 
 // r * x (one zero bit through the register).
-ZCRC_HD uint32_t gf2_times_x(uint32_t r) { return (r >> 1) ^ (kPolyReflected & (0u - (r & 1u))); }
+ZCRC_HD constexpr uint32_t gf2_times_x(uint32_t r) { return (r >> 1) ^ (kPolyReflected & (0u - (r & 1u))); }
 
 // r * x^-1.  Exact because P(0) = 1: the reflected polynomial has bit 31 set,
 // so a set bit 31 after the forward step can only come from the reduction.
@@ -42,7 +42,7 @@ ZCRC_HD uint32_t gf2_times_xinv(uint32_t r) {
 }
 
 // a * b mod P.
-ZCRC_HD uint32_t gf2_mul(uint32_t a, uint32_t b) {
+ZCRC_HD constexpr uint32_t gf2_mul(uint32_t a, uint32_t b) {
   uint32_t p = 0;
 #if defined(__HIP_DEVICE_COMPILE__)
 #pragma unroll
@@ -92,6 +92,19 @@ inline void build_mct(uint32_t c, uint32_t *table /* 4*256 */) {
   for (int j = 0; j < 4; j++)
     for (uint32_t v = 0; v < 256; v++) table[j * 256 + v] = gf2_mul(c, v << (8 * j));
 }
+
+// Compile-time products for building an MCT in registers (the per-buffer
+// mode's braid, zcrc_batch_kernel.h) for c = x^(2^k): q[p] = c * (1 << p),
+// so that MCT(c)[j][v] = xor over the set bits b of v of q[8j + b].
+template <int k>
+struct MctBasis {
+  uint32_t q[32];
+  constexpr MctBasis() : q{} {
+    uint32_t c = kOne >> 1;  // x
+    for (int i = 0; i < k; i++) c = gf2_mul(c, c);
+    for (int p = 0; p < 32; p++) q[p] = gf2_mul(c, 1u << p);
+  }
+};
 
 // Standard reflected byte table T[v] = raw CRC of the single byte v.
 inline void build_std_table(uint32_t *table /* 256 */) {
