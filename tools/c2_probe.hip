@@ -9,6 +9,10 @@
 //                workgroup per CU, wave w reads buffer w (nt 16-B loads,
 //                two groups of 4 KiB in flight), xor into one word
 //   probe-grid   pure-read grid-stride sweep, 8 workgroups of 256 per CU
+//   probe-pb     pure read in the per-buffer mode's mapping and 2 x 4 KiB
+//                ping-pong, slot priorities as the product; -rot: each wave
+//                starts at a hashed block of its buffer and wraps; -np:
+//                no slot priorities
 //   crc          the product kernel (prefix precomputed: the plan's output)
 //   crc-fused    the one-launch kernel (scans the lengths itself)
 // and one stamped launch of each CRC form (s_memrealtime, 100 MHz) printed
@@ -61,6 +65,50 @@ __global__ __launch_bounds__(1024) void probe_wave(const uint8_t *base, uint64_t
 #pragma unroll
     for (int u = 0; u < 8; u++) acc ^= v[u][0] ^ v[u][1] ^ v[u][2] ^ v[u][3];
   }
+  if (acc == 0x12345678u) out[w] = acc;  // keep the loads
+}
+
+// The per-buffer mode's mapping (wave slot s of workgroup g reads buffer
+// s * grid + g), 2 x 4 KiB ping-pong like the CRC loop; kRot: each wave
+// starts at a hashed block of its buffer and wraps (the pure-read cost of a
+// de-phased visit order)
+template <bool kRot, bool kPrio = true>
+__global__ __launch_bounds__(1024) void probe_pb(const uint8_t *base, uint64_t per, uint32_t *out) {
+  const uint32_t lane = threadIdx.x & 63u, slot = threadIdx.x >> 6;
+  const uint64_t w = (uint64_t)slot * gridDim.x + blockIdx.x;
+  if (kPrio) {
+    if (slot >= 12) __builtin_amdgcn_s_setprio(3);
+    else if (slot >= 8) __builtin_amdgcn_s_setprio(2);
+    else if (slot >= 4) __builtin_amdgcn_s_setprio(1);
+  }
+  __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc((void *)(base + w * per), (short)0, (int)per, 0x00020000);
+  const uint32_t blocks = (uint32_t)(per >> 10);
+  const uint32_t rot = kRot ? (uint32_t)((w * 0x9E3779B1u) >> 7) % blocks & ~3u : 0u;
+  uint32_t acc = 0;
+  uint32_t ga[4][4], gb[4][4];
+  auto ld = [&](uint32_t (*G)[4], uint32_t g) {
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+      const uint32_t blk = (rot + 4 * g + u) % blocks;
+      auto x = __builtin_amdgcn_raw_buffer_load_b128(r, 1024u * blk + 16u * lane, 0, 2);
+      G[u][0] = x[0], G[u][1] = x[1], G[u][2] = x[2], G[u][3] = x[3];
+    }
+  };
+  auto use = [&](uint32_t (*G)[4]) {
+#pragma unroll
+    for (int u = 0; u < 4; u++) acc ^= G[u][0] ^ G[u][1] ^ G[u][2] ^ G[u][3];
+  };
+  const uint32_t ng = blocks / 4;
+  ld(ga, 0);
+  ld(gb, 1);
+  for (uint32_t g = 0; g + 2 < ng; g += 2) {
+    use(ga);
+    ld(ga, g + 2);
+    use(gb);
+    if (g + 3 < ng) ld(gb, g + 3);
+  }
+  use(ga);
+  use(gb);
   if (acc == 0x12345678u) out[w] = acc;  // keep the loads
 }
 
@@ -132,8 +180,8 @@ int main(int argc, char **argv) {
   };
   std::vector<hipEvent_t> ev(2 * kBatches);
   for (auto &e : ev) CHECK(hipEventCreate(&e));
-  enum { kProbeWave, kProbeGrid, kCrc, kCrcFused, kNumV };
-  const char *names[kNumV] = {"probe-wave", "probe-grid", "crc", "crc-fused"};
+  enum { kProbeWave, kProbeGrid, kCrc, kCrcFused, kProbePb, kProbePbRot, kProbePbNoPrio, kNumV };
+  const char *names[kNumV] = {"probe-wave", "probe-grid", "crc", "crc-fused", "probe-pb", "probe-pb-rot", "probe-pb-np"};
   auto launch = [&](int v, int b, hipEvent_t e0, hipEvent_t e1) {
     const uint8_t *base = data + b * kBatchBytes;
     switch (v) {
@@ -142,6 +190,15 @@ int main(int argc, char **argv) {
         break;
       case kProbeGrid:
         hipExtLaunchKernelGGL(probe_grid, dim3(cus * 8), dim3(256), 0, 0, e0, e1, 0, base, kBatchBytes, out);
+        break;
+      case kProbePb:
+        hipExtLaunchKernelGGL(probe_pb<false>, dim3(cus), dim3(1024), 0, 0, e0, e1, 0, base, kLen, out);
+        break;
+      case kProbePbRot:
+        hipExtLaunchKernelGGL(probe_pb<true>, dim3(cus), dim3(1024), 0, 0, e0, e1, 0, base, kLen, out);
+        break;
+      case kProbePbNoPrio:
+        hipExtLaunchKernelGGL((probe_pb<false, false>), dim3(cus), dim3(1024), 0, 0, e0, e1, 0, base, kLen, out);
         break;
       case kCrc:
         hipExtLaunchKernelGGL((crc32_batch_kernel<false, kDepth, 0>), dim3(cus), dim3(kThreads), 0, 0, e0, e1, 0,
