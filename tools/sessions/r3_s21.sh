@@ -1,8 +1,8 @@
 #!/bin/bash
-# Round 3, sessions 19-21: per-buffer mode variants against fc529b5 (s19: decide late,
+# Round 3, session 19/20: per-buffer mode variants against fc529b5 (s20: the preload
 # barrier waits only for the combine-table loads) against fc529b5.
 set -e -o pipefail
-O=gpurun_out/s19; mkdir -p $O
+O=gpurun_out/s21; mkdir -p $O
 timeout -k 10 400 python3 -u -m pytest -x -v --timeout 120 --timeout-method thread -m gpu \
   tests/test_gpu_parity.py tests/test_gpu_small_kernel.py > $O/pytest_parity.log 2>&1
 for shape in "4096 65536 40" "4096 16384 40" "1000 65536 40" "4096 4096 40" "4096 1024 40" "4096 0 20" "2048 65537 20"; do
