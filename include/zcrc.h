@@ -137,6 +137,20 @@ int zcrc32_batch_device_strided(const void *d_base, uint64_t stride, uint64_t le
 int zcrc_inflate_batch_device(const void *const *d_src, const uint64_t *d_src_len, void *const *d_dst,
                               const uint64_t *d_cap, uint64_t *d_out_len, int32_t *d_status, size_t n,
                               void *stream);
+/* ONE raw-DEFLATE stream in device memory, decoded by many waves at once
+ * (block-parallel, speculative: DESIGN.md section 11b).  ZIPsFS preloads one
+ * deflated entry at a time (zip_fread() in preloadram_now,
+ * src/ZIPsFS_preloadfileram.c:286-306), which the batch call above would
+ * decode on a single wave.  The compressed bytes are cut into chunks of
+ * chunk_bytes (0: 16 KiB, grown so that there are at most 16,384); each chunk
+ * decodes from the first valid block header in it with an unknown history,
+ * the chunks reachable from the stream's start are stitched together, and
+ * when that fails (corrupt data, a chunk's output far above the average
+ * ratio) the stream is decoded serially, with zlib's status.  Same results
+ * as zcrc_inflate_batch_device for one stream (*d_out_len, *d_status).
+ * Scratch: about 4 x cap bytes of HBM, kept per HIP stream.  Asynchronous. */
+int zcrc_inflate_device(const void *d_src, uint64_t src_len, void *d_dst, uint64_t cap, uint64_t *d_out_len,
+                        int32_t *d_status, uint64_t chunk_bytes, void *stream);
 /* Same for host memory, plus the CRC-32 of every output: the preload of a
  * deflated entry (raw stream via libzip ZIP_FL_COMPRESSED) inflated and
  * checksummed in one call.  Streams are packed into pinned staging, inflated

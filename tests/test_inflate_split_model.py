@@ -1,0 +1,109 @@
+"""CPU tests of the block-parallel inflate model (tests/inflate_split_model.py),
+the specification of zcrc_inflate_split.hip: the model's bytes equal
+zlib.decompress (zlib 1.2.11, the library libzip inflates ZIPsFS entries with)
+on streams cut into many small chunks, and its fall-backs trigger where the
+GPU path falls back to the serial decoder.  Sizes are kept small: the model
+decodes in pure Python."""
+import zlib
+
+import pytest
+
+import inflate_split_model as M
+import inflate_streams as S
+
+
+def _zlib(comp: bytes) -> bytes:
+    return zlib.decompress(comp, -15)
+
+
+@pytest.mark.parametrize("kind,level,strategy", [
+    ("text", 6, "default"), ("spectrum", 6, "default"), ("text", 1, "default"), ("spectrum", 9, "filtered"),
+    ("random", 6, "default"), ("far", 6, "default"), ("runs", 6, "rle"), ("text", 6, "huffman"),
+    ("text", 6, "fixed"),
+])
+def test_model_equals_zlib(kind, level, strategy):
+    data = S.PAYLOADS[kind](96 << 10, 11)
+    comp = S.deflate(data, level, strategy)
+    st, out, stats = M.inflate_split(comp, len(data), 1024)
+    assert stats["fallback"] is None, stats
+    assert st == M.OK and out == _zlib(comp)
+
+
+def test_model_flush_blocks_and_many_chunks():
+    """Sync/full flushes put empty stored blocks and byte-aligned block starts
+    between dynamic blocks; 512-byte chunks make most chunks candidate-less."""
+    data = S.text_payload(80 << 10, 3) + S.spectrum_payload(40 << 10, 4)
+    comp = S.deflate_chunked(data, 9000)
+    st, out, stats = M.inflate_split(comp, len(data), 512)
+    assert st == M.OK and out == data, stats
+    assert stats["chain"] >= 3
+
+
+def test_model_history_markers_cross_chunks():
+    """Matches reaching 32 KiB back across every chunk boundary (markers
+    resolved through the chain of tails)."""
+    data = S.far_repeat_payload(200 << 10, 5)
+    comp = S.deflate(data, 9)
+    st, out, stats = M.inflate_split(comp, len(data), 700)
+    assert st == M.OK and out == data, stats
+
+
+def test_model_header_check_passes_every_true_block_start():
+    data = S.text_payload(200 << 10, 9) + S.spectrum_payload(100 << 10, 9)
+    comp = S.deflate(data, 6)
+    starts = _block_starts(comp)
+    dyn = [p for p, t in starts if t == 2]
+    assert len(dyn) >= 3
+    assert all(M.header_ok(comp, p) for p in dyn)
+
+
+def _block_starts(comp: bytes):
+    """(bit position, BTYPE) of every block, by an exact decode."""
+    out, res = [], []
+    br = M.Bits(comp, 0)
+    while True:
+        res.append((br.pos, (br.peek(3) >> 1) & 3))
+        last = br.get(1)
+        typ = br.get(2)
+        if typ == 0:
+            br.pos = (br.pos + 7) & ~7
+            ln = br.get(16)
+            br.get(16)
+            br.pos += 8 * ln
+        else:
+            if typ == 1:
+                ll, dd = M.fixed_codes()
+            else:
+                _, ll, dd = M.read_dynamic(br)
+            assert M.codes(br, ll, dd, out, M.ChunkResult(0), False) == M.OK
+        if last:
+            return res
+
+
+def test_model_corrupt_stream_falls_back():
+    data = S.text_payload(60 << 10, 2)
+    comp = bytearray(S.deflate(data, 6))
+    comp[len(comp) // 2] ^= 0x5A
+    st, out, stats = M.inflate_split(bytes(comp), len(data), 2048)
+    if st is None:
+        assert stats["fallback"]
+    else:  # the flip may leave a valid stream: then it must be zlib's
+        try:
+            want = _zlib(bytes(comp))
+        except zlib.error:
+            want = None
+        assert out == want
+
+
+def test_model_output_cap_falls_back():
+    data = S.spectrum_payload(64 << 10, 1)
+    comp = S.deflate(data, 6)
+    st, _, stats = M.inflate_split(comp, len(data) - 1, 1024)
+    assert st is None and stats["fallback"] == "output"
+
+
+def test_model_truncated_stream_falls_back():
+    data = S.spectrum_payload(64 << 10, 1)
+    comp = S.deflate(data, 6)[:-3]
+    st, _, stats = M.inflate_split(comp, len(data), 1024)
+    assert st is None and stats["fallback"]

@@ -41,6 +41,7 @@ _SIGNATURES = {
     "zcrc32_combine": (_c_u32, [_c_u32, _c_u32, _c_u64]),
     "zcrc_inflate_batch_device": (_c_int, [_c_p] * 6 + [_c_sz, _c_p]),
     "zcrc_inflate_batch": (_c_int, [_c_p] * 7 + [_c_sz, ctypes.c_uint]),
+    "zcrc_inflate_device": (_c_int, [_c_p, ctypes.c_uint64, _c_p, ctypes.c_uint64, _c_p, _c_p, ctypes.c_uint64, _c_p]),
     "zcrc32_stream_open": (_c_p, [_c_u32]),
     "zcrc32_stream_update": (_c_int, [_c_p, _c_p, _c_sz]),
     "zcrc32_stream_final": (_c_int, [_c_p, ctypes.POINTER(_c_u32)]),

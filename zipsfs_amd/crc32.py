@@ -27,7 +27,7 @@ __all__ = [
     "ZcrcError", "Crc32Stream", "cg_crc32", "crc32_batch", "crc32_batch_device", "crc32_batch_device_ws",
     "crc32_batch_strided", "crc32_tensors", "crc32_combine", "fhandle_check_crc32",
     "verify_entries", "fill_synthetic", "profile", "device_info", "version",
-    "inflate_batch_device", "inflate_to_device", "inflate_batch", "INFLATE_STATUS",
+    "inflate_batch_device", "inflate_to_device", "inflate_batch", "inflate_device", "INFLATE_STATUS",
 ]
 
 
@@ -319,6 +319,28 @@ def inflate_batch_device(src_ptrs, src_lens, dst_ptrs, caps, out_lens=None, stat
                                           caps.data_ptr(), out_lens.data_ptr(), status.data_ptr(), n,
                                           _stream_ptr(stream)), "zcrc_inflate_batch_device")
     return out_lens, status
+
+
+def inflate_device(src, dst, src_len: int = None, cap: int = None, chunk_bytes: int = 0, stream=None):
+    """ONE raw-DEFLATE stream, block-parallel on the GPU (zcrc_inflate_device).
+
+    src: uint8 device tensor holding the compressed stream (src_len bytes,
+    default all of it); dst: uint8 device tensor for the output (cap bytes,
+    default its size).  Returns (out_len, status) as 1-element device tensors
+    (int64, int32); asynchronous on `stream`.  chunk_bytes: the split
+    granularity (0: the library's default)."""
+    torch = _torch()
+    _check_dev(src, "src", torch.uint8)
+    _check_dev(dst, "dst", torch.uint8)
+    src_len = src.numel() if src_len is None else int(src_len)
+    cap = dst.numel() if cap is None else int(cap)
+    if src_len > src.numel() or cap > dst.numel():
+        raise ValueError("src_len / cap beyond the tensors")
+    out_len = torch.zeros(1, dtype=torch.int64, device=src.device)
+    status = torch.full((1,), -99, dtype=torch.int32, device=src.device)
+    check(lib().zcrc_inflate_device(src.data_ptr(), src_len, dst.data_ptr(), cap, out_len.data_ptr(),
+                                    status.data_ptr(), int(chunk_bytes), _stream_ptr(stream)), "zcrc_inflate_device")
+    return out_len, status
 
 
 def inflate_batch(streams: Sequence, caps: Sequence[int]):

@@ -63,6 +63,15 @@ namespace w32 {  // the whole 32 KiB window in LDS: four streams per CU
 #include "zcrc_inflate_impl.h"
 #undef ZI_WIN
 }  // namespace w32
+namespace sp {  // speculative chunk decode (16-bit elements, zcrc_inflate_split.hip): 16 Ki-element ring
+#define ZI_WIN 16384u
+#define ZI_SPEC 1
+#include "zcrc_inflate_impl.h"
+#undef ZI_SPEC
+#undef ZI_WIN
+}  // namespace sp
+
+hipError_t launch_inflate_spec(const SpecArgs &args, hipStream_t stream) { return sp::launch_spec(args, stream); }
 
 // Longest-first dispatch.  Workgroups start in index order, so when a batch
 // has more streams than can be resident, a slow stream that happens to sit

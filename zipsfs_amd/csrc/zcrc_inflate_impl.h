@@ -1,7 +1,31 @@
 // zcrc_inflate_impl.h -- the batched inflate kernel, parameterised by the
-// LDS window size ZI_WIN.  Included twice by zcrc_inflate.hip (namespaces w16
-// and w32); not a standalone header.
+// LDS window size ZI_WIN.  Included by zcrc_inflate.hip once per variant
+// (namespaces w16, w8, w32, and sp: ZI_SPEC = 1, the speculative chunk
+// decoder of zcrc_inflate_split.hip); not a standalone header.
+//
+// ZI_SPEC: output elements are 16-bit -- a byte, or a marker kMarker + w for
+// byte w of the unknown 32 KiB history before the chunk (a back-reference
+// past the chunk's first output) -- written to the chunk's region of split
+// scratch; the decode starts at a candidate bit position and stops at the
+// next candidate it reaches (tests/inflate_split_model.py is the spec).
+#ifndef ZI_SPEC
+#define ZI_SPEC 0
+#define ZI_SPEC_DEFAULTED
+#endif
 namespace {
+
+#if ZI_SPEC
+typedef uint16_t elem_t;
+#define ZI_DSW "ds_write_b16"
+#define ZI_DSR "ds_read_u16"
+#define ZI_ESH "1"
+#else
+typedef uint8_t elem_t;
+#define ZI_DSW "ds_write_b8"
+#define ZI_DSR "ds_read_u8"
+#define ZI_ESH "0"
+#endif
+constexpr uint32_t kEsh = ZI_SPEC ? 1u : 0u;  // log2(bytes per output element)
 
 
 // The LDS ring holds the last kWin bytes (ZI_WIN, set by zcrc_inflate.hip).
@@ -103,7 +127,7 @@ struct CodeMeta {
 // literal instead of ~30).
 constexpr uint32_t kDummy = kWin;
 struct Lds {
-  uint8_t ring[kWin + 256];
+  elem_t ring[kWin + 256];
   uint16_t llsym[288], ddsym[32], clsym[20];
   CodeMeta llm, ddm;
   uint8_t lens[320];  // litlen lengths [0, nlen), distance lengths [nlen, nlen + ndist)
@@ -315,16 +339,21 @@ __device__ __forceinline__ int32_t bad_symbol(Reader &r, uint32_t e, int32_t err
   return err;
 }
 
-// Output: bytes [fl, pos) are decoded but still only in the ring.  `room`
-// counts the literals/match bytes that may be added before something must
-// happen: min(cap - pos, kFlushLag - (pos - fl)).
+// Output: elements [fl, pos) are decoded but still only in the ring.  `room`
+// counts the literals/match elements that may be added before something must
+// happen: min(cap - pos, kFlushLag - (pos - fl)).  (Elements are bytes, or
+// 16-bit values under ZI_SPEC.)
 struct Out {
-  uint8_t *dst;
+  elem_t *dst;
   uint64_t cap;
-  uint64_t pos;  // bytes produced
-  uint64_t fl;   // bytes flushed to dst (a multiple of 1024 until the end)
+  uint64_t pos;  // elements produced
+  uint64_t fl;   // elements flushed to dst (a multiple of kFlushStep until the end)
   uint32_t room;
   bool al16;     // dst 16-byte aligned
+#if ZI_SPEC
+  uint32_t reach;  // furthest back-reference before the chunk's first element
+  bool spec;       // the history is unknown (every chunk but the first)
+#endif
   __device__ void set_room() {
     const uint64_t c = cap - pos;
     const uint32_t f = kFlushLag - (uint32_t)(pos - fl);
@@ -332,18 +361,31 @@ struct Out {
   }
 };
 
+// one element through a buffer resource (bytes, or 16-bit under ZI_SPEC),
+// sc1: from L2, never a stale L1 line (reads of flushed output)
+__device__ __forceinline__ uint32_t load_elem_sc1(__amdgpu_buffer_rsrc_t r, uint32_t idx) {
+  if (kEsh) return __builtin_amdgcn_raw_buffer_load_b16(r, idx << kEsh, 0, 16);
+  return __builtin_amdgcn_raw_buffer_load_b8(r, idx, 0, 16);
+}
+__device__ __forceinline__ void store_elem(uint32_t v, __amdgpu_buffer_rsrc_t r, uint32_t idx) {
+  if (kEsh) __builtin_amdgcn_raw_buffer_store_b16((uint16_t)v, r, idx << kEsh, 0, 0);
+  else __builtin_amdgcn_raw_buffer_store_b8((uint8_t)v, r, idx, 0, 0);
+}
+
 // ring [fl, upto) -> dst, 1 KiB per step: one 16-B LDS read and one 16-B
-// store per lane when dst is 16-B aligned, else 16 coalesced byte steps.
+// store per lane when dst is 16-B aligned, else coalesced element steps.
 // Stores go through a buffer resource sized to the bytes due, so the
 // hardware drops the lanes past `upto` (no divergent branch).
+constexpr uint32_t kFlushStep = 1024u >> kEsh;  // elements per 1 KiB step
 __device__ __forceinline__ void flush_to(Lds &s, Out &o, uint64_t upto) {
   const uint32_t lane = lane_id();
   while (o.fl < upto) {
     const uint32_t roff = (uint32_t)(o.fl & kWinMask);
-    const uint32_t m = (upto - o.fl < 1024u) ? (uint32_t)(upto - o.fl) : 1024u;
-    const __amdgpu_buffer_rsrc_t d = __builtin_amdgcn_make_buffer_rsrc(o.dst + o.fl, (short)0, (int)m, 0x00020000);
-    if (o.al16 && m == 1024u) {
-      const uint4 v = *reinterpret_cast<const uint4 *>(&s.ring[roff + 16u * lane]);
+    const uint32_t m = (upto - o.fl < kFlushStep) ? (uint32_t)(upto - o.fl) : kFlushStep;
+    const __amdgpu_buffer_rsrc_t d =
+        __builtin_amdgcn_make_buffer_rsrc(o.dst + o.fl, (short)0, (int)(m << kEsh), 0x00020000);
+    if (o.al16 && m == kFlushStep) {
+      const uint4 v = *reinterpret_cast<const uint4 *>(&s.ring[roff + (16u >> kEsh) * lane]);
       typedef uint32_t v4w __attribute__((ext_vector_type(4)));
       v4w w;
       w.x = v.x;
@@ -353,12 +395,11 @@ __device__ __forceinline__ void flush_to(Lds &s, Out &o, uint64_t upto) {
       __builtin_amdgcn_raw_buffer_store_b128(w, d, 16u * lane, 0, 0);
     } else {
 #pragma unroll
-      for (uint32_t k = 0; k < 16; k++)
-        __builtin_amdgcn_raw_buffer_store_b8(s.ring[roff + 64u * k + lane], d, 64u * k + lane, 0, 0);
+      for (uint32_t k = 0; k < (16u >> kEsh); k++) store_elem(s.ring[roff + 64u * k + lane], d, 64u * k + lane);
     }
     o.fl += m;
   }
-  // far matches read flushed bytes back with sc1 (L2) loads: let these
+  // far matches read flushed elements back with sc1 (L2) loads: let these
   // stores reach L2 first (once per kFlushLag batch)
   __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
 }
@@ -372,7 +413,7 @@ __device__ __forceinline__ void settle(Lds &s, Out &o) {
   o.set_room();
 }
 
-// lane-parallel copy of `len` bytes from `dist` back (dist <= pos checked);
+// lane-parallel copy of `len` elements from `dist` back (dist <= pos checked);
 // lanes past `len` write to the dummy tail.  Sources older than the ring
 // (dist > kWin) are flushed already (pos - fl < kFlushLag + 1024 + 258 <
 // kWin) and are read back from dst with sc1 loads, which bypass the CU's
@@ -382,36 +423,59 @@ __device__ __forceinline__ void copy_match(Lds &s, const Out &o, uint32_t p0, ui
   const uint32_t src = p0 - dist;
   if (dist > kWin) {
     const __amdgpu_buffer_rsrc_t far =
-        __builtin_amdgcn_make_buffer_rsrc(o.dst + (o.pos - dist), (short)0, (int)len, 0x00020000);
+        __builtin_amdgcn_make_buffer_rsrc(o.dst + (o.pos - dist), (short)0, (int)(len << kEsh), 0x00020000);
     uint32_t v[5];  // len <= 258
 #pragma unroll
-    for (uint32_t k = 0; k < 5; k++)
-      v[k] = (64u * k < len) ? __builtin_amdgcn_raw_buffer_load_b8(far, 64u * k + lane, 0, 16) : 0u;
+    for (uint32_t k = 0; k < 5; k++) v[k] = (64u * k < len) ? load_elem_sc1(far, 64u * k + lane) : 0u;
 #pragma unroll
     for (uint32_t k = 0; k < 5; k++) {
       const uint32_t i = 64u * k + lane;
-      if (64u * k < len) s.ring[i < len ? (p0 + i) & kWinMask : kDummy + 4u * lane] = (uint8_t)v[k];
+      if (64u * k < len) s.ring[i < len ? (p0 + i) & kWinMask : kDummy + 4u * lane] = (elem_t)v[k];
     }
   } else if (dist >= 64u || len <= dist) {
-    // every source byte precedes the 64-byte step that writes it
+    // every source element precedes the 64-element step that writes it
     for (uint32_t i0 = 0; i0 < len; i0 += 64) {
       const uint32_t i = i0 + lane;
-      const uint8_t v = s.ring[(src + i) & kWinMask];
+      const elem_t v = s.ring[(src + i) & kWinMask];
       s.ring[i < len ? (p0 + i) & kWinMask : kDummy + 4u * lane] = v;
     }
   } else {
-    // short period: byte i repeats byte i mod dist
+    // short period: element i repeats element i mod dist
     const float rcp = 1.0f / (float)dist;
     for (uint32_t i0 = 0; i0 < len; i0 += 64) {
       const uint32_t i = i0 + lane;
       uint32_t m = i - (uint32_t)((float)i * rcp) * dist;
       m = (int32_t)m < 0 ? m + dist : m;
       m = m >= dist ? m - dist : m;
-      const uint8_t v = s.ring[(src + m) & kWinMask];
+      const elem_t v = s.ring[(src + m) & kWinMask];
       s.ring[i < len ? (p0 + i) & kWinMask : kDummy + 4u * lane] = v;
     }
   }
 }
+
+#if ZI_SPEC
+// A back-reference reaching before the chunk's first element (dist > p0,
+// dist <= p0 + 32 KiB): element i takes source p0 - dist + (i mod dist) --
+// the same element the sequential copy would -- which is either a marker
+// (source < 0: byte 32768 + source of the history) or an element produced
+// earlier (in the ring, or flushed to dst when older than the ring).  Every
+// source precedes the copy, so the 64-lane steps are independent.
+__device__ __noinline__ void copy_spec(Lds &s, const Out &o, uint32_t p0, uint32_t len, uint32_t dist) {
+  const uint32_t lane = lane_id();
+  // flushed elements [0, p0 - kWin) are read back from dst (sc1)
+  const uint32_t nfar = p0 > kWin ? p0 - kWin : 0u;
+  const __amdgpu_buffer_rsrc_t far = __builtin_amdgcn_make_buffer_rsrc(o.dst, (short)0, (int)(nfar << kEsh), 0x00020000);
+  for (uint32_t i0 = 0; i0 < len; i0 += 64) {
+    const uint32_t i = i0 + lane;
+    const uint32_t m = i % dist;
+    const int32_t sidx = (int32_t)p0 - (int32_t)dist + (int32_t)m;
+    const uint32_t fv = load_elem_sc1(far, sidx < 0 ? 0x3FFFFFFFu : (uint32_t)sidx);  // out of range: 0
+    const uint32_t nv = s.ring[(uint32_t)sidx & kWinMask];
+    const uint32_t v = sidx < 0 ? kInflateMarker + (uint32_t)((int32_t)kInflateHist + sidx) : ((uint32_t)sidx < nfar ? fv : nv);
+    s.ring[i < len ? (p0 + i) & kWinMask : kDummy + 4u * lane] = (elem_t)v;
+  }
+}
+#endif
 
 // Literal runs, the hot path of poorly compressible data (~93% of the
 // symbols of the spectrum payloads), as one hand-scheduled loop, unrolled
@@ -467,7 +531,7 @@ __device__ __forceinline__ uint32_t literal_run(Reader &r, uint32_t &p, uint32_t
       "s_lshr_b64 s[60:61], s[60:61], %[t0]\n\t"
       "s_sub_u32 %[nb], %[nb], %[t0]\n\t"
       "v_lshrrev_b32_e64 v57, 11, %[t1]\n\t"
-      "ds_write_b8 v58, v57\n\t"
+      ZI_DSW " v58, v57\n\t"
       "s_add_u32 %[p], %[p], 1\n\t"
       "s_cmp_le_u32 %[nb], 32\n\t"
       "s_cbranch_scc1 L_ref_%=\n\t"
@@ -486,7 +550,7 @@ __device__ __forceinline__ uint32_t literal_run(Reader &r, uint32_t &p, uint32_t
       "s_lshr_b64 s[60:61], s[60:61], %[t0]\n\t"
       "s_sub_u32 %[nb], %[nb], %[t0]\n\t"
       "v_lshrrev_b32_e64 v57, 11, %[t1]\n\t"
-      "ds_write_b8 v58, v57\n\t"
+      ZI_DSW " v58, v57\n\t"
       "s_add_u32 %[p], %[p], 1\n\t"
       "s_branch L_top_%=\n\t"
       // refill 32 bits: exit (0) if past the end or into the next block
@@ -570,16 +634,16 @@ __device__ __forceinline__ uint32_t literal_run(Reader &r, uint32_t &p, uint32_t
       "s_sub_u32 %[t2], %[p], %[md]\n\t"
       "v_add_u32 v59, %[t2], %[vl]\n\t"
       "v_and_b32 v59, %[wm], v59\n\t"
-      "v_add_u32 v59, %[rl], v59\n\t"
-      "ds_read_u8 v57, v59\n\t"
+      "v_lshl_add_u32 v59, v59, " ZI_ESH ", %[rl]\n\t"
+      ZI_DSR " v57, v59\n\t"
       "v_add_u32 v58, %[p], %[vl]\n\t"
       "v_and_b32 v58, %[wm], v58\n\t"
-      "v_add_u32 v58, %[rl], v58\n\t"
+      "v_lshl_add_u32 v58, v58, " ZI_ESH ", %[rl]\n\t"
       "v_cmp_gt_u32 vcc, %[ml], %[vl]\n\t"
       "s_nop 1\n\t"
       "v_cndmask_b32 v58, %[vdm], v58, vcc\n\t"
       "s_waitcnt lgkmcnt(0)\n\t"
-      "ds_write_b8 v58, v57\n\t"
+      ZI_DSW " v58, v57\n\t"
       "s_add_u32 %[p], %[p], %[ml]\n\t"
       "s_sub_u32 %[room], %[room], %[ml]\n\t"
       "s_branch L_top_%=\n\t"
@@ -607,9 +671,9 @@ __device__ int32_t codes(Lds &s, Reader &r, Out &o, const LLTab &ll, const DTab 
   const uint32_t lane = threadIdx.x;
   const uint32_t ring_lds = (uint32_t)reinterpret_cast<uintptr_t>(
       (__attribute__((address_space(3))) uint8_t *)(&s.ring[0]));
-  const uint32_t vsel = lane == 0 ? 1u : 0u;
-  const uint32_t vdum = ring_lds + (lane == 0 ? 0u : kDummy + 4u * lane);
-  const uint32_t vdm = ring_lds + kDummy + 4u * lane;
+  const uint32_t vsel = lane == 0 ? (1u << kEsh) : 0u;
+  const uint32_t vdum = ring_lds + (lane == 0 ? 0u : (kDummy + 4u * lane) << kEsh);
+  const uint32_t vdm = ring_lds + ((kDummy + 4u * lane) << kEsh);
   int32_t st = ZCRC_INFLATE_OK;
   for (;;) {
     uint32_t len, dist;
@@ -657,7 +721,7 @@ __device__ int32_t codes(Lds &s, Reader &r, Out &o, const LLTab &ll, const DTab 
         settle(s, o);
       }
 #ifndef ZI_ABL_NOLIT
-      s.ring[lane == 0 ? (uint32_t)o.pos & kWinMask : kDummy + 4u * lane] = (uint8_t)e_val(e);
+      s.ring[lane == 0 ? (uint32_t)o.pos & kWinMask : kDummy + 4u * lane] = (elem_t)e_val(e);
 #endif
       o.pos++;
       o.room--;
@@ -690,7 +754,11 @@ __device__ int32_t codes(Lds &s, Reader &r, Out &o, const LLTab &ll, const DTab 
     r.drop(e_extra(d));
     }
   have_pair:
+#if ZI_SPEC
+    if (dist > o.pos && (!o.spec || dist > o.pos + kInflateHist)) {
+#else
     if (dist > o.pos) {
+#endif
       st = ZCRC_INFLATE_ERR_DIST;
       break;
     }
@@ -698,7 +766,15 @@ __device__ int32_t codes(Lds &s, Reader &r, Out &o, const LLTab &ll, const DTab 
       st = ZCRC_INFLATE_ERR_OUTPUT;
       break;
     }
-#ifndef ZI_ABL_NOCOPY
+#if ZI_SPEC
+    if (dist > o.pos) {  // into the unknown history: markers
+      const uint32_t back = dist - (uint32_t)o.pos;
+      o.reach = back > o.reach ? back : o.reach;
+      copy_spec(s, o, (uint32_t)o.pos, len, dist);
+    } else {
+      copy_match(s, o, (uint32_t)o.pos, len, dist);
+    }
+#elif !defined(ZI_ABL_NOCOPY)
     copy_match(s, o, (uint32_t)o.pos, len, dist);
 #endif
     o.pos += len;
@@ -729,7 +805,7 @@ __device__ int32_t stored(Lds &s, Reader &r, Out &o) {
 #pragma unroll
     for (int k = 0; k < 16; k++) {
       const uint32_t j = 64u * k + lane;
-      s.ring[i0 + j < len ? (p0 + j) & kWinMask : kDummy + 4u * lane] = (uint8_t)v[k];
+      s.ring[i0 + j < len ? (p0 + j) & kWinMask : kDummy + 4u * lane] = (elem_t)v[k];
     }
     o.pos += (len - i0 < 1024u) ? len - i0 : 1024u;
     settle(s, o);
@@ -826,10 +902,12 @@ __device__ void fixed_tables(Lds &s, LLTab &ll, DTab &dd) {
 #define ZI_WPE 1
 #define ZI_WPE_DEFAULTED
 #endif
+#if !ZI_SPEC
 __global__ __launch_bounds__(64, ZI_WPE) void inflate_kernel(InflateArgs a) {
   __shared__ __attribute__((aligned(16))) Lds s;
   if (blockIdx.x >= a.n) return;
   const uint64_t i = a.order ? a.order[blockIdx.x] : blockIdx.x;
+  if (a.run_if && a.run_if[i] == 0) return;  // the block-parallel decode succeeded (zcrc_inflate_split.hip)
   const uint8_t *src = a.src[i];
   const uint64_t src_len = a.src_len[i];
   Out o;
@@ -892,14 +970,115 @@ __global__ __launch_bounds__(64, ZI_WPE) void inflate_kernel(InflateArgs a) {
     a.status[i] = st;
   }
 }
+#else
+// Speculative decode of chunk k of one stream (zcrc_inflate_split.hip,
+// tests/inflate_split_model.py spec_decode): from candidate bit a.cand[k]
+// (chunk 0: bit 0, history known) to the first block start equal to a later
+// candidate (link), the end of the final block, or an error.  Elements go
+// to the chunk's region, which extends over the following chunks that have
+// no candidate (no decode of theirs writes there).
+__global__ __launch_bounds__(64, ZI_WPE) void inflate_spec_kernel(SpecArgs a) {
+  __shared__ __attribute__((aligned(16))) Lds s;
+  const uint64_t k = blockIdx.x;
+  const uint64_t c = a.cand[k];
+  SpecRec *rec = a.rec + k;
+  if (c == kSplitNone) {
+    if (threadIdx.x == 0) *rec = SpecRec{0, 0, kSpecSkipped, -1, 0, 0};
+    return;
+  }
+  uint64_t nxt = k + 1;
+  while (nxt < a.nchunks && a.cand[nxt] == kSplitNone) nxt++;
+  Out o;
+  o.dst = a.region + k * a.region_elems;
+  o.cap = (nxt - k) * a.region_elems;
+  o.pos = 0;
+  o.fl = 0;
+  o.al16 = (reinterpret_cast<uint64_t>(o.dst) & 15u) == 0;
+  o.reach = 0;
+  o.spec = k > 0;
+  o.set_room();
+  int32_t st = ZCRC_INFLATE_OK;
+  int32_t link = -1;
+  uint32_t last = 0;
+  Reader r;
+  const uint64_t base = reinterpret_cast<uint64_t>(a.src) & ~(uint64_t)15;
+  r.lead = (uint32_t)(reinterpret_cast<uint64_t>(a.src) - base);
+  r.end = r.lead + (uint32_t)a.src_len;
+  r.limit = r.end + 16u;
+  r.rsrc = __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void *>(base), (short)0, (int)((r.end + 15u) & ~15u),
+                                             0x00020000);
+  r.seek(r.lead + (uint32_t)(c >> 3));
+  if (!r.ensure()) st = ZCRC_INFLATE_ERR_INPUT;
+  else r.drop((uint32_t)(c & 7u));
+  LLTab ll;
+  DTab dd;
+  uint64_t j = k + 1;  // the next candidate at or past the decode position
+  while (st == ZCRC_INFLATE_OK) {
+    if (!r.ensure()) {
+      st = ZCRC_INFLATE_ERR_INPUT;
+      break;
+    }
+    const uint64_t bit = ((uint64_t)(r.P - r.lead) << 3) - r.nb;
+    while (j < a.nchunks) {
+      const uint64_t cj = a.cand[j];
+      if (cj != kSplitNone && cj >= bit) break;
+      j++;
+    }
+    if (j < a.nchunks && a.cand[j] == bit) {
+      link = (int32_t)j;
+      break;
+    }
+    last = r.peek(1);
+    const uint32_t type = (uint32_t)(r.bb >> 1) & 3u;
+    r.drop(3);
+    if (type == 0) {
+      st = stored(s, r, o);
+    } else if (type == 1) {
+      fixed_tables(s, ll, dd);
+      st = codes(s, r, o, ll, dd);
+    } else if (type == 2) {
+      st = dynamic_tables(s, r, ll, dd);
+      if (st == ZCRC_INFLATE_OK) st = codes(s, r, o, ll, dd);
+    } else {
+      st = ZCRC_INFLATE_ERR_BLOCK_TYPE;
+    }
+    st = (int32_t)uni((uint32_t)st);
+    if (last) break;
+  }
+  if (st == ZCRC_INFLATE_OK && link < 0 && r.consumed() > a.src_len) st = ZCRC_INFLATE_ERR_INPUT;
+  if (st == ZCRC_INFLATE_OK) flush_to(s, o, o.pos);
+  if (threadIdx.x == 0) {
+    rec->out_len = o.pos;
+    rec->end_bit = ((uint64_t)(r.P - r.lead) << 3) - r.nb;
+    rec->status = st;
+    rec->link = link;
+    rec->reach = o.reach;
+    rec->final_ = (st == ZCRC_INFLATE_OK && link < 0 && last) ? 1u : 0u;
+  }
+}
+#endif
 
 }  // namespace
 
+#if !ZI_SPEC
 hipError_t launch(const InflateArgs &args, hipStream_t stream) {
   hipLaunchKernelGGL(inflate_kernel, dim3((unsigned)args.n), dim3(64), 0, stream, args);
   return hipGetLastError();
 }
+#else
+hipError_t launch_spec(const SpecArgs &args, hipStream_t stream) {
+  hipLaunchKernelGGL(inflate_spec_kernel, dim3((unsigned)args.nchunks), dim3(64), 0, stream, args);
+  return hipGetLastError();
+}
+#endif
 #ifdef ZI_WPE_DEFAULTED
 #undef ZI_WPE
 #undef ZI_WPE_DEFAULTED
 #endif
+#ifdef ZI_SPEC_DEFAULTED
+#undef ZI_SPEC
+#undef ZI_SPEC_DEFAULTED
+#endif
+#undef ZI_DSW
+#undef ZI_DSR
+#undef ZI_ESH

@@ -1,0 +1,501 @@
+// zcrc_inflate_split.hip -- block-parallel inflate of ONE raw-DEFLATE stream
+// on MI355X (gfx950).  SURVEY.md 8(f) rank 4, DESIGN.md section 11b.
+//
+// ZIPsFS preloads one deflated entry at a time: zip_fread() in 16 MiB calls
+// inside preloadram_now (src/ZIPsFS_preloadfileram.c:286-306), libzip
+// inflating with zlib, and then the CRC check (:243).  The batched inflate
+// (zcrc_inflate.hip) gives each stream one wave, so a single entry decodes at
+// one wave's speed.  Here one stream is cut into chunks that decode at once:
+//
+//   1. inflate_find_kernel: for every chunk of the compressed bytes, the first
+//      bit position whose dynamic-Huffman block header is valid by zlib's
+//      rules (quick filter on every position, full header check on the ~0.1%
+//      that pass it).  A true block start always passes; a false one only
+//      costs work.
+//   2. sp::inflate_spec_kernel (zcrc_inflate_impl.h, ZI_SPEC): every chunk
+//      decodes from its candidate with an unknown history into 16-bit
+//      elements (byte or history marker) and stops where it reaches a later
+//      candidate (a link) or the final block's end.
+//   3. inflate_chain_kernel: follows the links from chunk 0 (a true start, so
+//      every chunk it reaches started at a true block boundary), checks the
+//      chain (statuses, history reach, capacity) and lays the chunks out.
+//   4. inflate_tails_kernel: the last 32 KiB of each chain chunk resolved in
+//      chain order through an LDS window; inflate_body_kernel: all other
+//      elements in parallel, from the resolved tails in dst.
+//   5. When the chain fails, the serial kernel (one wave) decodes the stream
+//      and reports zlib's exact status: launch_inflate with run_if.
+//
+// The CPU model tests/inflate_split_model.py is the specification; its tests
+// and the GPU tests compare the bytes with zlib.decompress.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/zcrc.h"
+#include "zcrc_internal.h"
+
+namespace zcrc {
+namespace {
+
+constexpr uint32_t kFindThreads = 1024;
+constexpr uint32_t kFindWin = 16384;     // compressed bytes staged per finder window
+constexpr uint32_t kFindLook = 1024;     // + look-ahead: a dynamic header is at most ~563 bytes
+constexpr uint32_t kFindWords = (kFindWin + kFindLook) / 4 + 4;
+constexpr uint32_t kFindSurv = 1024;     // survivors of the quick filter checked per window
+
+// 64 bits of the staged window starting at bit q (LSB first)
+__device__ __forceinline__ uint64_t bits64(const uint32_t *w, uint32_t q) {
+  const uint32_t i = q >> 5, s = q & 31u;
+  const uint64_t lo = (((uint64_t)w[i + 1] << 32) | w[i]) >> s;
+  const uint64_t hi = s ? ((uint64_t)w[i + 2] << (64 - s)) : 0ull;
+  return lo | hi;
+}
+
+// Quick filter at bit q: BTYPE = 2, HLIT <= 29, HDIST <= 29, and a complete
+// code-length code (zlib rejects an incomplete one).  ~0.1% of the positions
+// of compressed data pass (tests/test_inflate_split.py measures it).
+__device__ __forceinline__ bool quick_ok(const uint32_t *w, uint32_t q) {
+  const uint64_t v = bits64(w, q);
+  if (((v >> 1) & 3u) != 2u) return false;
+  if (((v >> 3) & 31u) > 29u || ((v >> 8) & 31u) > 29u) return false;
+  const uint32_t hclen = (uint32_t)((v >> 13) & 15u) + 4u;
+  uint64_t cl = bits64(w, q + 17);
+  cl &= (hclen == 19u) ? ((1ull << 57) - 1) : ((1ull << (3 * hclen)) - 1);
+  uint32_t kraft = 0;
+#pragma unroll
+  for (uint32_t i = 0; i < 19; i++) {
+    const uint32_t l = (uint32_t)(cl >> (3 * i)) & 7u;
+    kraft += l ? (128u >> l) : 0u;
+  }
+  return kraft == 128u;
+}
+
+// The full dynamic-header check at bit q (lane-parallel: each thread its own
+// position): decode the literal/length and distance code lengths with the
+// code-length code and apply zlib 1.2.11's acceptance rules (as
+// oracle/inflate_port.c dynamic(); the code-length code lengths come in the
+// order 16 17 18 0 8 7 9 6 10 5 11 4 12 3 13 2 14 1 15, RFC 1951 3.2.7).
+// `avail`: staged bits from q.  sorted:
+// this thread's 19-byte scratch for the canonical symbol order.
+__device__ __forceinline__ bool full_ok(const uint32_t *w, uint32_t q, uint32_t avail, uint8_t *sorted) {
+  const uint64_t v = bits64(w, q);
+  const uint32_t nlen = (uint32_t)((v >> 3) & 31u) + 257u, ndist = (uint32_t)((v >> 8) & 31u) + 1u;
+  const uint32_t hclen = (uint32_t)((v >> 13) & 15u) + 4u;
+  const uint64_t cl = bits64(w, q + 17);
+  uint32_t len_of[19];
+#define ZCL(i) ((i) < hclen ? (uint32_t)(cl >> (3 * (i))) & 7u : 0u)
+  len_of[16] = ZCL(0);
+  len_of[17] = ZCL(1);
+  len_of[18] = ZCL(2);
+  len_of[0] = ZCL(3);
+  len_of[8] = ZCL(4);
+  len_of[7] = ZCL(5);
+  len_of[9] = ZCL(6);
+  len_of[6] = ZCL(7);
+  len_of[10] = ZCL(8);
+  len_of[5] = ZCL(9);
+  len_of[11] = ZCL(10);
+  len_of[4] = ZCL(11);
+  len_of[12] = ZCL(12);
+  len_of[3] = ZCL(13);
+  len_of[13] = ZCL(14);
+  len_of[2] = ZCL(15);
+  len_of[14] = ZCL(16);
+  len_of[1] = ZCL(17);
+  len_of[15] = ZCL(18);
+#undef ZCL
+  uint32_t cnt[8];
+#pragma unroll
+  for (uint32_t L = 0; L < 8; L++) cnt[L] = 0;
+  uint32_t k = 0;
+#pragma unroll
+  for (uint32_t L = 1; L < 8; L++) {
+#pragma unroll
+    for (uint32_t s = 0; s < 19; s++) {
+      if (len_of[s] == L) {
+        sorted[k] = (uint8_t)s;
+        k++;
+        cnt[L]++;
+      }
+    }
+  }
+  uint32_t p = q + 17 + 3 * hclen;  // next bit
+  const uint32_t total = nlen + ndist, end = q + avail;
+  uint32_t idx = 0, prev = 0, kll = 0, kd = 0, mll = 0, md = 0;
+  bool eob = false;
+  while (idx < total) {
+    if (p + 32 > end) return false;  // the header would run past the staged bytes
+    const uint32_t b = (uint32_t)bits64(w, p);
+    // canonical decode, bit by bit (codes of at most 7 bits)
+    uint32_t code = 0, first = 0, index = 0, sym = 32, used = 0;
+#pragma unroll
+    for (uint32_t L = 1; L < 8; L++) {
+      if (sym == 32) {
+        code |= (b >> (L - 1)) & 1u;
+        const uint32_t c = cnt[L];
+        if (code - first < c) {
+          sym = sorted[index + code - first];
+          used = L;
+        } else {
+          index += c;
+          first = (first + c) << 1;
+          code <<= 1;
+        }
+      }
+    }
+    if (sym == 32) return false;
+    p += used;
+    const uint32_t x = b >> used;
+    uint32_t val, rep;
+    if (sym < 16) {
+      val = sym;
+      rep = 1;
+      prev = sym;
+    } else if (sym == 16) {
+      if (idx == 0) return false;
+      val = prev;
+      rep = 3 + (x & 3u);
+      p += 2;
+    } else if (sym == 17) {
+      val = 0;
+      rep = 3 + (x & 7u);
+      p += 3;
+      prev = 0;
+    } else {
+      val = 0;
+      rep = 11 + (x & 127u);
+      p += 7;
+      prev = 0;
+    }
+    if (idx + rep > total) return false;
+    if (val) {
+      // split the run at the literal/length | distance boundary
+      const uint32_t in_ll = idx < nlen ? (nlen - idx < rep ? nlen - idx : rep) : 0u;
+      kll += in_ll << (15 - val);
+      kd += (rep - in_ll) << (15 - val);
+      if (in_ll) mll = val > mll ? val : mll;
+      if (rep > in_ll) md = val > md ? val : md;
+      if (idx <= 256 && 256 < idx + rep) eob = true;
+    }
+    idx += rep;
+  }
+  if (!eob) return false;
+  if (kll > 32768u || (kll < 32768u && mll != 1u)) return false;
+  if (kd > 32768u || (kd < 32768u && md > 1u)) return false;
+  return true;
+}
+
+struct FindArgs {
+  const uint8_t *src;
+  uint64_t src_len;
+  uint64_t chunk;  // compressed bytes per chunk
+  uint64_t nchunks;
+  uint64_t *cand;
+};
+
+// One workgroup per chunk k >= 1: the first bit position in [8 k chunk,
+// 8 (k+1) chunk) that passes full_ok, in windows of kFindWin bytes.
+__global__ __launch_bounds__(kFindThreads) void inflate_find_kernel(FindArgs a) {
+  __shared__ uint32_t w[kFindWords];
+  __shared__ uint32_t surv[kFindSurv];
+  __shared__ uint8_t sorted[kFindSurv][20];
+  __shared__ uint32_t nsurv, best;
+  const uint32_t tid = threadIdx.x;
+  const uint64_t k = blockIdx.x;
+  if (k == 0) {
+    if (tid == 0) a.cand[0] = 0;
+    return;
+  }
+  const uint64_t lo = k * a.chunk;
+  const uint64_t hi = lo + a.chunk < a.src_len ? lo + a.chunk : a.src_len;
+  uint64_t found = kSplitNone;
+  for (uint64_t wlo = lo; wlo < hi && found == kSplitNone; wlo += kFindWin) {
+    const uint64_t whi = wlo + kFindWin < hi ? wlo + kFindWin : hi;  // positions [wlo, whi)
+    const uint64_t send = whi + kFindLook < a.src_len ? whi + kFindLook : a.src_len;
+    const uint32_t nbytes = (uint32_t)(send - wlo);
+    if (tid == 0) nsurv = 0, best = 0xFFFFFFFFu;
+    // stage [wlo, send) as little-endian words, zeros past the end
+    for (uint32_t i = tid; i < kFindWords; i += kFindThreads) {
+      uint32_t v = 0;
+#pragma unroll
+      for (uint32_t b = 0; b < 4; b++) {
+        const uint32_t o = 4 * i + b;
+        if (o < nbytes) v |= (uint32_t)a.src[wlo + o] << (8 * b);
+      }
+      w[i] = v;
+    }
+    __syncthreads();
+    const uint32_t npos = 8u * (uint32_t)(whi - wlo);
+    for (uint32_t q = tid; q < npos; q += kFindThreads) {
+      if (quick_ok(w, q)) {
+        const uint32_t i = atomicAdd(&nsurv, 1u);
+        if (i < kFindSurv) surv[i] = q;
+      }
+    }
+    __syncthreads();
+    const uint32_t ns = nsurv < kFindSurv ? nsurv : kFindSurv;  // more: the rest go unchecked (only parallelism is lost)
+    for (uint32_t i = tid; i < ns; i += kFindThreads) {
+      const uint32_t q = surv[i];
+      if (full_ok(w, q, 8u * nbytes - q, sorted[i])) atomicMin(&best, q);
+    }
+    __syncthreads();
+    if (best != 0xFFFFFFFFu) found = 8 * wlo + best;
+    __syncthreads();  // before the next window overwrites w / nsurv
+  }
+  if (tid == 0) a.cand[k] = found;
+}
+
+struct ChainArgs {
+  const SpecRec *rec;
+  uint64_t nchunks;
+  uint64_t cap;
+  uint32_t *chain;     // chain chunks in order; chain[nchunks] = their count
+  uint64_t *off;       // output offset of chunk k (valid on the chain)
+  uint32_t *run_serial;
+  uint64_t *out_len;   // the caller's (1 stream)
+  int32_t *status;
+  // the serial fall-back's one-stream argument arrays
+  const uint8_t **fb_src;
+  uint64_t *fb_src_len;
+  uint8_t **fb_dst;
+  uint64_t *fb_cap;
+  const uint8_t *src;
+  uint64_t src_len;
+  uint8_t *dst;
+};
+
+constexpr uint32_t kChainLds = 16384;  // chunks whose links are staged in LDS (the host keeps nchunks <= this)
+
+// Follow the links from chunk 0 (LDS walk by one thread), then give every
+// chain chunk its output offset (block scan in index order: links only go
+// forward).  Failure -> run_serial = 1.
+__global__ __launch_bounds__(1024) void inflate_chain_kernel(ChainArgs a) {
+  __shared__ uint32_t nxt[kChainLds];
+  __shared__ uint64_t part[16];
+  __shared__ uint32_t ok_s;
+  const uint32_t tid = threadIdx.x;
+  const uint32_t n = (uint32_t)a.nchunks;
+  // successor: the next chunk, kFinal, or kFail (an error, or neither linked
+  // nor final); kOn marks the chain
+  constexpr uint32_t kFinal = 0xFFFFFEu, kFail = 0xFFFFFFu, kOn = 0x80000000u;
+  for (uint32_t k = tid; k < n; k += 1024) {
+    const SpecRec r = a.rec[k];
+    uint32_t s = kFail;
+    if (r.status == ZCRC_INFLATE_OK) s = r.final_ ? kFinal : (r.link > (int32_t)k ? (uint32_t)r.link : kFail);
+    nxt[k] = s;
+  }
+  if (tid == 0) {
+    *a.fb_src = a.src;
+    *a.fb_src_len = a.src_len;
+    *a.fb_dst = a.dst;
+    *a.fb_cap = a.cap;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    // mark the chain: on-chain chunks get bit 30 set in their entry
+    uint32_t k = 0;
+    bool ok = true;
+    for (;;) {  // links only go forward: this ends
+      const uint32_t s = nxt[k];
+      nxt[k] = s | kOn;
+      if (s == kFinal) break;
+      if (s == kFail) {
+        ok = false;
+        break;
+      }
+      k = s;
+    }
+    ok_s = ok;
+  }
+  __syncthreads();
+  if (!ok_s) {
+    if (tid == 0) {
+      *a.run_serial = 1;
+      a.chain[a.nchunks] = 0;
+    }
+    return;
+  }
+  // exclusive scan of out_len over the chain, in index order; then checks
+  const uint32_t per = (n + 1023) / 1024;
+  const uint32_t k0 = tid * per, k1 = k0 + per < n ? k0 + per : n;
+  uint64_t sum = 0;
+  for (uint32_t k = k0; k < k1; k++)
+    if (nxt[k] & kOn) sum += a.rec[k].out_len;
+  // block scan of the per-thread sums (wave scan, then wave totals)
+  const uint32_t lane = tid & 63u, wv = tid >> 6;
+  uint64_t inc = sum;
+  for (uint32_t d = 1; d < 64; d <<= 1) {
+    const uint64_t t = __shfl_up(inc, d, 64);
+    if (lane >= d) inc += t;
+  }
+  if (lane == 63) part[wv] = inc;
+  __syncthreads();
+  uint64_t base = 0, tot = 0;
+  for (uint32_t i = 0; i < 16; i++) {
+    if (i < wv) base += part[i];
+    tot += part[i];
+  }
+  uint64_t run = base + inc - sum;
+  bool good = true;
+  for (uint32_t k = k0; k < k1; k++) {
+    if (nxt[k] & kOn) {
+      const SpecRec r = a.rec[k];
+      if (r.reach > run) good = false;  // a back-reference before the stream start
+      a.off[k] = run;
+      run += r.out_len;
+    }
+  }
+  if (!good) ok_s = 0;  // benign race: every writer writes 0
+  __syncthreads();
+  if (tid == 0) {
+    const bool fine = ok_s && tot <= a.cap;
+    *a.run_serial = fine ? 0u : 1u;
+    if (fine) {
+      *a.out_len = tot;
+      *a.status = ZCRC_INFLATE_OK;
+    }
+    // chain list in order (only read when fine)
+    uint32_t m = 0;
+    for (uint32_t k = 0; k < n; k++)
+      if (nxt[k] & kOn) a.chain[m++] = k;
+    a.chain[a.nchunks] = fine ? m : 0u;
+  }
+}
+
+struct ResolveArgs {
+  const uint16_t *region;
+  uint64_t region_elems;
+  const SpecRec *rec;
+  const uint32_t *chain;  // chain[nchunks] = count (0: the serial decode runs instead)
+  const uint64_t *off;
+  uint64_t nchunks;
+  uint8_t *dst;
+};
+
+// element -> byte: a marker is byte (v - kInflateMarker) of the kInflateHist
+// bytes before the chunk at output offset `off`.  (One helper shared by an
+// LDS-ring and a global-memory caller crashed the compiler's inliner: two.)
+__device__ __forceinline__ uint8_t resolve_ring(uint32_t v, const uint8_t *ring, uint64_t off) {
+  return v < kInflateMarker ? (uint8_t)v : ring[(off - kInflateHist + (v - kInflateMarker)) & (kInflateHist - 1)];
+}
+__device__ __forceinline__ uint8_t resolve_dst(uint32_t v, const uint8_t *dst, uint64_t off) {
+  return v < kInflateMarker ? (uint8_t)v : dst[off - kInflateHist + (v - kInflateMarker)];
+}
+
+// The last 32 KiB of every chain chunk, in chain order, through an LDS ring
+// of the last 32 KiB of output: chunk m's markers read bytes of chunks
+// before it, all in the ring when its turn comes.
+__global__ __launch_bounds__(1024) void inflate_tails_kernel(ResolveArgs a) {
+  __shared__ uint8_t ring[kInflateHist];
+  const uint32_t tid = threadIdx.x;
+  const uint32_t m_end = a.chain[a.nchunks];
+  constexpr uint32_t kPer = kInflateHist / 1024;
+  for (uint32_t m = 0; m < m_end; m++) {
+    const uint32_t k = a.chain[m];
+    const uint64_t len = a.rec[k].out_len, off = a.off[k];
+    const uint64_t t0 = len > kInflateHist ? len - kInflateHist : 0;
+    const uint16_t *el = a.region + k * a.region_elems;
+    uint8_t v[kPer];
+#pragma unroll
+    for (uint32_t j = 0; j < kPer; j++) {
+      const uint64_t e = t0 + tid + 1024u * j;
+      v[j] = e < len ? resolve_ring(el[e], ring, off) : 0;
+    }
+    __syncthreads();  // every marker read its history before the ring moves on
+#pragma unroll
+    for (uint32_t j = 0; j < kPer; j++) {
+      const uint64_t e = t0 + tid + 1024u * j;
+      if (e < len) {
+        ring[(off + e) & (kInflateHist - 1)] = v[j];
+        a.dst[off + e] = v[j];
+      }
+    }
+    __syncthreads();
+  }
+}
+
+// Every chain chunk's elements before its last 32 KiB: markers from the
+// resolved tails in dst (written by the previous launch).
+__global__ __launch_bounds__(256) void inflate_body_kernel(ResolveArgs a) {
+  const uint32_t m_end = a.chain[a.nchunks];
+  constexpr uint32_t kTile = 256 * 16;
+  for (uint32_t m = blockIdx.y; m < m_end; m += gridDim.y) {
+    const uint32_t k = a.chain[m];
+    const uint64_t len = a.rec[k].out_len, off = a.off[k];
+    const uint64_t body = len > kInflateHist ? len - kInflateHist : 0;
+    const uint16_t *el = a.region + k * a.region_elems;
+    for (uint64_t t = (uint64_t)blockIdx.x * kTile; t < body; t += (uint64_t)gridDim.x * kTile) {
+#pragma unroll
+      for (uint32_t j = 0; j < 16; j++) {
+        const uint64_t e = t + threadIdx.x + 256u * j;
+        if (e < body) a.dst[off + e] = resolve_dst(el[e], a.dst, off);
+      }
+    }
+  }
+}
+
+}  // namespace
+
+uint64_t inflate_split_chunk(uint64_t src_len, uint64_t want) {
+  uint64_t c = want ? want : kInflateSplitChunk;
+  const uint64_t need = (src_len + kChainLds - 1) / kChainLds;  // at most kChainLds chunks
+  return c < need ? need : c;
+}
+
+uint64_t inflate_split_scratch_bytes(uint64_t src_len, uint64_t cap, uint64_t chunk) {
+  const uint64_t nch = src_len ? (src_len + chunk - 1) / chunk : 1;
+  const uint64_t relems = ((2 * cap) / nch + kInflateSplitSlack + 7) & ~7ull;
+  return 256 + nch * (8 + sizeof(SpecRec) + 4 + 8) + 8 + 64 + nch * relems * 2 + 64;
+}
+
+// One stream: find, speculative decode, chain, resolve, serial fall-back.
+hipError_t launch_inflate_split(const uint8_t *src, uint64_t src_len, uint8_t *dst, uint64_t cap,
+                                uint64_t *out_len, int32_t *status, uint64_t chunk, void *scratch, int num_cus,
+                                hipStream_t stream) {
+  const uint64_t nch = src_len ? (src_len + chunk - 1) / chunk : 1;
+  const uint64_t relems = ((2 * cap) / nch + kInflateSplitSlack + 7) & ~7ull;
+  uint8_t *p = static_cast<uint8_t *>(scratch);
+  auto take = [&](uint64_t bytes) {
+    uint8_t *r = p;
+    p += (bytes + 63) & ~63ull;
+    return r;
+  };
+  uint32_t *run_serial = reinterpret_cast<uint32_t *>(take(64));
+  const uint8_t **fb_src = reinterpret_cast<const uint8_t **>(take(8));
+  uint64_t *fb_src_len = reinterpret_cast<uint64_t *>(take(8));
+  uint8_t **fb_dst = reinterpret_cast<uint8_t **>(take(8));
+  uint64_t *fb_cap = reinterpret_cast<uint64_t *>(take(8));
+  uint64_t *cand = reinterpret_cast<uint64_t *>(take(8 * nch));
+  SpecRec *rec = reinterpret_cast<SpecRec *>(take(sizeof(SpecRec) * nch));
+  uint32_t *chain = reinterpret_cast<uint32_t *>(take(4 * (nch + 1)));
+  uint64_t *off = reinterpret_cast<uint64_t *>(take(8 * nch));
+  uint16_t *region = reinterpret_cast<uint16_t *>(take(2 * nch * relems));
+
+  FindArgs fa{src, src_len, chunk, nch, cand};
+  hipLaunchKernelGGL(inflate_find_kernel, dim3((unsigned)nch), dim3(kFindThreads), 0, stream, fa);
+  SpecArgs sa{src, src_len, cand, rec, region, relems, nch};
+  hipError_t e = launch_inflate_spec(sa, stream);
+  if (e != hipSuccess) return e;
+  ChainArgs ca{rec, nch, cap, chain, off, run_serial, out_len, status, fb_src, fb_src_len, fb_dst, fb_cap,
+               src, src_len, dst};
+  hipLaunchKernelGGL(inflate_chain_kernel, dim3(1), dim3(1024), 0, stream, ca);
+  ResolveArgs ra{region, relems, rec, chain, off, nch, dst};
+  hipLaunchKernelGGL(inflate_tails_kernel, dim3(1), dim3(1024), 0, stream, ra);
+  const unsigned gy = (unsigned)(nch < 4096 ? nch : 4096);
+  const unsigned gx = (unsigned)((4u * (unsigned)num_cus + gy - 1) / gy) + 1u;
+  hipLaunchKernelGGL(inflate_body_kernel, dim3(gx, gy), dim3(256), 0, stream, ra);
+  e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  // the serial decode, run only when the chain failed
+  InflateArgs ia{};
+  ia.src = fb_src;
+  ia.src_len = fb_src_len;
+  ia.dst = fb_dst;
+  ia.cap = fb_cap;
+  ia.out_len = out_len;
+  ia.status = status;
+  ia.n = 1;
+  ia.run_if = run_serial;
+  return launch_inflate(ia, num_cus, stream, nullptr);
+}
+
+}  // namespace zcrc

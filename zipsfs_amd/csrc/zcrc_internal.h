@@ -120,13 +120,52 @@ struct InflateArgs {
   // optional dispatch order (workgroup b decodes stream order[b]); nullptr:
   // stream b.  launch_inflate fills it longest-first when streams queue.
   const uint32_t *order;
+  // optional: stream i is decoded only when run_if[i] != 0 (the serial
+  // fall-back of the block-parallel decode, zcrc_inflate_split.hip)
+  const uint32_t *run_if;
+};
+// Block-parallel (speculative) inflate of one stream (zcrc_inflate_split.hip;
+// the spec is tests/inflate_split_model.py).  Chunk k's decode writes 16-bit
+// elements: a byte, or kInflateMarker + w = byte w of the kInflateHist bytes
+// before the chunk's first element.
+constexpr uint32_t kInflateMarker = 0x8000u;
+constexpr uint32_t kInflateHist = 32768u;
+constexpr uint64_t kSplitNone = ~0ull;  // no candidate block start in the chunk
+constexpr int32_t kSpecSkipped = -1;    // SpecRec::status of a chunk without a candidate
+struct SpecRec {
+  uint64_t out_len;  // elements produced
+  uint64_t end_bit;  // bit position where the decode stopped
+  int32_t status;    // ZCRC_INFLATE_*, or kSpecSkipped
+  int32_t link;      // the chunk whose candidate it stopped at, -1: none
+  uint32_t reach;    // furthest back-reference before its first element (bytes)
+  uint32_t final_;   // 1: it decoded the final block
+};
+struct SpecArgs {
+  const uint8_t *src;
+  uint64_t src_len;
+  const uint64_t *cand;  // per chunk: candidate bit position, or kSplitNone
+  SpecRec *rec;
+  uint16_t *region;      // chunk k's elements start at region + k * region_elems
+  uint64_t region_elems;
+  uint64_t nchunks;
 };
 constexpr uint64_t kInflateMaxSrc = 0xF0000000ull;  // 32-bit buffer range and block arithmetic
 // order_scratch: >= 4 * n bytes of device memory for the dispatch order
 // (used when the batch exceeds the streams resident at once; may be null)
 hipError_t launch_inflate(const InflateArgs &args, int num_cus, hipStream_t stream, uint32_t *order_scratch);
+hipError_t launch_inflate_spec(const SpecArgs &args, hipStream_t stream);
+constexpr uint64_t kInflateSplitChunk = 16384;  // compressed bytes per chunk (at most 16,384 chunks)
+constexpr uint64_t kInflateSplitSlack = 16384;  // elements added to each chunk's region
+constexpr uint64_t kInflateSplitMinSrc = 65536; // smaller streams decode serially
+// chunk size for a stream (want = 0: the default), the scratch the split
+// decode of one stream needs, and the launch chain (zcrc_inflate_split.hip)
+uint64_t inflate_split_chunk(uint64_t src_len, uint64_t want);
+uint64_t inflate_split_scratch_bytes(uint64_t src_len, uint64_t cap, uint64_t chunk);
+hipError_t launch_inflate_split(const uint8_t *src, uint64_t src_len, uint8_t *dst, uint64_t cap,
+                                uint64_t *out_len, int32_t *status, uint64_t chunk, void *scratch, int num_cus,
+                                hipStream_t stream);
 // purposes of the runtime's per-stream scratch cache (zcrc_runtime.hip)
-enum ScratchUse { kScratchBatch = 0, kScratchInflateOrder = 1, kScratchFused = 2 };
+enum ScratchUse { kScratchBatch = 0, kScratchInflateOrder = 1, kScratchFused = 2, kScratchInflateSplit = 3 };
 
 inline uint64_t plan_tiles(uint64_t n) { return n == 0 ? 1 : (n + kPlanTile - 1) / kPlanTile; }
 const char *product_kernel_name();

@@ -1526,6 +1526,32 @@ int zcrc_inflate_batch_device(const void *const *d_src, const uint64_t *d_src_le
   return ZCRC_OK;
 }
 
+int zcrc_inflate_device(const void *d_src, uint64_t src_len, void *d_dst, uint64_t cap, uint64_t *d_out_len,
+                        int32_t *d_status, uint64_t chunk_bytes, void *stream) {
+  if (!d_out_len || !d_status || (src_len && !d_src) || (cap && !d_dst)) return fail(ZCRC_ERR_ARG, "null argument");
+  if (src_len >= kInflateMaxSrc) return fail(ZCRC_ERR_TOO_BIG, "compressed stream of 3.75 GiB or more");
+  DeviceCtx *dc = nullptr;
+  int rc = device_ctx(&dc);
+  if (rc) return rc;
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  if (src_len == 0) {  // nothing to read (d_src may be null): input exhausted, as the batch kernel reports
+    ZCRC_HIP_TRY(hipMemsetAsync(d_out_len, 0, sizeof(uint64_t), st));
+    ZCRC_HIP_TRY(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(d_status), ZCRC_INFLATE_ERR_INPUT, 1, st));
+    return ZCRC_OK;
+  }
+  // streams below kInflateSplitMinSrc: one chunk (the same kernels, no split)
+  const uint64_t chunk = src_len < kInflateSplitMinSrc ? src_len : inflate_split_chunk(src_len, chunk_bytes);
+  const size_t need = inflate_split_scratch_bytes(src_len, cap, chunk);
+  void *scratch = nullptr;
+  size_t have = 0;
+  std::unique_lock<std::mutex> lk;
+  rc = stream_scratch(st, kScratchInflateSplit, need, &scratch, &have, &lk);
+  if (rc) return rc;
+  ZCRC_HIP_TRY(launch_inflate_split(static_cast<const uint8_t *>(d_src), src_len, static_cast<uint8_t *>(d_dst), cap,
+                                    d_out_len, d_status, chunk, scratch, dc->num_cus, st));
+  return ZCRC_OK;
+}
+
 namespace zcrc {
 namespace {
 
