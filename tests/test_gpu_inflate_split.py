@@ -133,3 +133,19 @@ def test_split_inflate_repeated_calls_reuse_scratch():
         for comp, data in streams:
             st, out = _run(comp, len(data), 4096 if rep else 0)
             assert st == 0 and out == data
+
+
+def test_host_batch_routes_large_entries_through_split():
+    """zcrc_inflate_batch (host memory, the preload of deflated entries):
+    one large entry (split path), a few large ones next to many small ones
+    (the cost model splits the large and batches the rest) -- bytes, status
+    and CRC-32 equal zlib's either way."""
+    one = S.text_payload(3 << 20, 50)
+    res = z.inflate_batch([S.deflate(one, 6)], [len(one)])
+    assert res[0][0] == 0 and res[0][1] == one and res[0][2] == zlib.crc32(one)
+    datas = [S.spectrum_payload(2 << 20, 60), S.text_payload(5 << 20, 61)]
+    datas += [S.PAYLOADS["text" if i % 2 else "spectrum"](20000 + 977 * i, 70 + i) for i in range(40)]
+    comps = [S.deflate(d, 6) for d in datas]
+    res = z.inflate_batch(comps, [len(d) for d in datas])
+    for (st, out, crc), d in zip(res, datas):
+        assert st == 0 and out == d and crc == zlib.crc32(d)

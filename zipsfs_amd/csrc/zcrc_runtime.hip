@@ -1493,9 +1493,13 @@ int zcrc32_batch_device_strided(const void *d_base, uint64_t stride, uint64_t le
   return rc;
 }
 
-int zcrc_inflate_batch_device(const void *const *d_src, const uint64_t *d_src_len, void *const *d_dst,
+namespace zcrc {
+namespace {
+// the batched inflate; d_run_if (device, optional): stream i is decoded only
+// when d_run_if[i] != 0 (the others go through zcrc_inflate_device)
+int inflate_batch_device_impl(const void *const *d_src, const uint64_t *d_src_len, void *const *d_dst,
                               const uint64_t *d_cap, uint64_t *d_out_len, int32_t *d_status, size_t n,
-                              void *stream) {
+                              void *stream, const uint32_t *d_run_if) {
   if (n == 0) return ZCRC_OK;
   if (!d_src || !d_src_len || !d_dst || !d_cap || !d_out_len || !d_status) return fail(ZCRC_ERR_ARG, "null argument");
   if (n > 0x7FFFFFFFu) return fail(ZCRC_ERR_ARG, "too many streams for one launch");
@@ -1510,6 +1514,7 @@ int zcrc_inflate_batch_device(const void *const *d_src, const uint64_t *d_src_le
   a.out_len = d_out_len;
   a.status = d_status;
   a.n = n;
+  a.run_if = d_run_if;
   hipStream_t st = static_cast<hipStream_t>(stream);
   hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
   ZCRC_HIP_TRY(hipStreamIsCapturing(st, &cap));
@@ -1524,6 +1529,14 @@ int zcrc_inflate_batch_device(const void *const *d_src, const uint64_t *d_src_le
   if (rc) return rc;
   ZCRC_HIP_TRY(launch_inflate(a, dc->num_cus, st, static_cast<uint32_t *>(order)));
   return ZCRC_OK;
+}
+}  // namespace
+}  // namespace zcrc
+
+int zcrc_inflate_batch_device(const void *const *d_src, const uint64_t *d_src_len, void *const *d_dst,
+                              const uint64_t *d_cap, uint64_t *d_out_len, int32_t *d_status, size_t n,
+                              void *stream) {
+  return inflate_batch_device_impl(d_src, d_src_len, d_dst, d_cap, d_out_len, d_status, n, stream, nullptr);
 }
 
 int zcrc_inflate_device(const void *d_src, uint64_t src_len, void *d_dst, uint64_t cap, uint64_t *d_out_len,
@@ -1582,6 +1595,12 @@ struct InflateStage {
   }
 };
 thread_local InflateStage t_inflate;
+// cost model of the host batch's split choice (inflate_host_group; measured
+// in DESIGN.md 11b)
+constexpr double kSplitCallUs = 6000.0;        // one zcrc_inflate_device call on a text-like entry
+constexpr double kWaveCompressedBps = 8.0e6;   // compressed bytes per second one wave decodes
+constexpr size_t kSplitMaxPerGroup = 64;
+constexpr uint64_t kSplitMaxCap = 1ull << 32;  // split scratch is ~4 x cap of HBM
 constexpr size_t kInflateGroupBytes = 1ull << 30;  // in + out bytes staged per group
 
 // streams [a, b): pack, one H2D, inflate, CRC, one D2H, unpack
@@ -1604,10 +1623,32 @@ int inflate_host_group(const void *const *src, const size_t *src_len, void *cons
     pi += src_len[i];
     po += cap[i];
   }
+  // Streams worth decoding block-parallel (zcrc_inflate_device), one after
+  // another, while the batch kernel decodes the rest at once: with the
+  // streams sorted by size, split the first k where k split latencies plus
+  // the (k+1)-th stream's one-wave decode time is least (cost model,
+  // kSplitCallUs per split call, kWaveCompressedBps for one
+  // wave).  ZIPsFS's preload of one entry takes the split path from ~40 KB of
+  // compressed bytes.
+  std::vector<uint32_t> run_if(m, 1u);
+  {
+    std::vector<size_t> ord(m);
+    for (size_t j = 0; j < m; j++) ord[j] = j;
+    std::sort(ord.begin(), ord.end(), [&](size_t x, size_t y) { return src_len[a + x] > src_len[a + y]; });
+    auto wave_us = [&](size_t r) { return r < m ? (double)src_len[a + ord[r]] / kWaveCompressedBps * 1e6 : 0.0; };
+    size_t best_k = 0;
+    double best = wave_us(0);
+    for (size_t k = 1; k <= m && k <= kSplitMaxPerGroup; k++) {
+      if (src_len[a + ord[k - 1]] < kInflateSplitMinSrc || cap[a + ord[k - 1]] > kSplitMaxCap) break;
+      const double t = kSplitCallUs * (double)k + wave_us(k);
+      if (t < best) best = t, best_k = k;
+    }
+    for (size_t r = 0; r < best_k; r++) run_if[ord[r]] = 0u;
+  }
   void *d_in = nullptr, *d_out = nullptr, *d_desc = nullptr;
   ZCRC_HIP_TRY(hipMallocAsync(&d_in, in + 16, st));
   ZCRC_HIP_TRY(hipMallocAsync(&d_out, out + 16, st));
-  ZCRC_HIP_TRY(hipMallocAsync(&d_desc, 8 * 5 * m + 8 * m, st));
+  ZCRC_HIP_TRY(hipMallocAsync(&d_desc, 8 * 5 * m + 8 * m + 4 * m, st));
   for (size_t j = 0; j < m; j++) {
     h[j] += reinterpret_cast<uint64_t>(d_in);
     h[2 * m + j] += reinterpret_cast<uint64_t>(d_out);
@@ -1615,13 +1656,25 @@ int inflate_host_group(const void *const *src, const size_t *src_len, void *cons
   uint64_t *dd = static_cast<uint64_t *>(d_desc);
   int32_t *d_status = reinterpret_cast<int32_t *>(dd + 5 * m);
   uint32_t *d_crc = reinterpret_cast<uint32_t *>(d_status + m);
+  uint32_t *d_run_if = d_crc + m;
   std::vector<uint64_t> olen(m);
   std::vector<int32_t> stv(m);
   std::vector<uint32_t> crcv(m);
   ZCRC_HIP_TRY(hipMemcpyAsync(d_in, t_inflate.h_in, in, hipMemcpyHostToDevice, st));
   ZCRC_HIP_TRY(hipMemcpyAsync(dd, h.data(), 8 * 4 * m, hipMemcpyHostToDevice, st));
-  rc = zcrc_inflate_batch_device(reinterpret_cast<const void *const *>(dd), dd + m,
-                                 reinterpret_cast<void *const *>(dd + 2 * m), dd + 3 * m, dd + 4 * m, d_status, m, st);
+  ZCRC_HIP_TRY(hipMemcpyAsync(d_run_if, run_if.data(), 4 * m, hipMemcpyHostToDevice, st));
+  bool any_batch = false;
+  for (size_t j = 0; j < m; j++) any_batch |= run_if[j] != 0;
+  rc = any_batch ? inflate_batch_device_impl(reinterpret_cast<const void *const *>(dd), dd + m,
+                                             reinterpret_cast<void *const *>(dd + 2 * m), dd + 3 * m, dd + 4 * m,
+                                             d_status, m, st, d_run_if)
+                 : ZCRC_OK;
+  for (size_t j = 0; j < m && !rc; j++) {
+    if (run_if[j]) continue;
+    rc = zcrc_inflate_device(reinterpret_cast<const uint8_t *>(d_in) + (h[j] - reinterpret_cast<uint64_t>(d_in)),
+                             src_len[a + j], reinterpret_cast<uint8_t *>(h[2 * m + j]), cap[a + j], dd + 4 * m + j,
+                             d_status + j, 0, st);
+  }
   if (!rc)
     rc = zcrc32_batch_device(reinterpret_cast<const void *const *>(dd + 2 * m), dd + 4 * m, nullptr, d_crc, m, st);
   if (!rc) {
