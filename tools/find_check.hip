@@ -1,0 +1,23 @@
+// tools/find_check.hip -- host build of the block-parallel inflate's block-
+// start test (zipsfs_amd/csrc/zcrc_inflate_find.h) for the CPU test
+// tests/test_inflate_find.py: flags[q] = quick_ok(q) | full_ok(q) << 1 for
+// every bit position q of a stream, with the stream staged as the finder
+// kernel stages it (little-endian words, zeros past the end).  Test tooling.
+#include <stdint.h>
+#include <string.h>
+
+#include <vector>
+
+#include "../zipsfs_amd/csrc/zcrc_inflate_find.h"
+
+extern "C" int find_flags(const uint8_t *data, size_t n, uint8_t *flags) {
+  std::vector<uint32_t> w((n + 3) / 4 + 8, 0u);
+  memcpy(w.data(), data, n);
+  uint8_t sorted[20];
+  for (size_t q = 0; q < 8 * n; q++) {
+    const bool a = zcrc::find::quick_ok(w.data(), (uint32_t)q);
+    const bool b = a && zcrc::find::full_ok(w.data(), (uint32_t)q, (uint32_t)(8 * n - q), sorted);
+    flags[q] = (uint8_t)(a | (b << 1));
+  }
+  return 0;
+}

@@ -31,6 +31,7 @@
 #include <stdint.h>
 
 #include "../../include/zcrc.h"
+#include "zcrc_inflate_find.h"
 #include "zcrc_internal.h"
 
 namespace zcrc {
@@ -41,148 +42,6 @@ constexpr uint32_t kFindWin = 16384;     // compressed bytes staged per finder w
 constexpr uint32_t kFindLook = 1024;     // + look-ahead: a dynamic header is at most ~563 bytes
 constexpr uint32_t kFindWords = (kFindWin + kFindLook) / 4 + 4;
 constexpr uint32_t kFindSurv = 1024;     // survivors of the quick filter checked per window
-
-// 64 bits of the staged window starting at bit q (LSB first)
-__device__ __forceinline__ uint64_t bits64(const uint32_t *w, uint32_t q) {
-  const uint32_t i = q >> 5, s = q & 31u;
-  const uint64_t lo = (((uint64_t)w[i + 1] << 32) | w[i]) >> s;
-  const uint64_t hi = s ? ((uint64_t)w[i + 2] << (64 - s)) : 0ull;
-  return lo | hi;
-}
-
-// Quick filter at bit q: BTYPE = 2, HLIT <= 29, HDIST <= 29, and a complete
-// code-length code (zlib rejects an incomplete one).  ~0.1% of the positions
-// of compressed data pass (tests/test_inflate_split.py measures it).
-__device__ __forceinline__ bool quick_ok(const uint32_t *w, uint32_t q) {
-  const uint64_t v = bits64(w, q);
-  if (((v >> 1) & 3u) != 2u) return false;
-  if (((v >> 3) & 31u) > 29u || ((v >> 8) & 31u) > 29u) return false;
-  const uint32_t hclen = (uint32_t)((v >> 13) & 15u) + 4u;
-  uint64_t cl = bits64(w, q + 17);
-  cl &= (hclen == 19u) ? ((1ull << 57) - 1) : ((1ull << (3 * hclen)) - 1);
-  uint32_t kraft = 0;
-#pragma unroll
-  for (uint32_t i = 0; i < 19; i++) {
-    const uint32_t l = (uint32_t)(cl >> (3 * i)) & 7u;
-    kraft += l ? (128u >> l) : 0u;
-  }
-  return kraft == 128u;
-}
-
-// The full dynamic-header check at bit q (lane-parallel: each thread its own
-// position): decode the literal/length and distance code lengths with the
-// code-length code and apply zlib 1.2.11's acceptance rules (as
-// oracle/inflate_port.c dynamic(); the code-length code lengths come in the
-// order 16 17 18 0 8 7 9 6 10 5 11 4 12 3 13 2 14 1 15, RFC 1951 3.2.7).
-// `avail`: staged bits from q.  sorted:
-// this thread's 19-byte scratch for the canonical symbol order.
-__device__ __forceinline__ bool full_ok(const uint32_t *w, uint32_t q, uint32_t avail, uint8_t *sorted) {
-  const uint64_t v = bits64(w, q);
-  const uint32_t nlen = (uint32_t)((v >> 3) & 31u) + 257u, ndist = (uint32_t)((v >> 8) & 31u) + 1u;
-  const uint32_t hclen = (uint32_t)((v >> 13) & 15u) + 4u;
-  const uint64_t cl = bits64(w, q + 17);
-  uint32_t len_of[19];
-#define ZCL(i) ((i) < hclen ? (uint32_t)(cl >> (3 * (i))) & 7u : 0u)
-  len_of[16] = ZCL(0);
-  len_of[17] = ZCL(1);
-  len_of[18] = ZCL(2);
-  len_of[0] = ZCL(3);
-  len_of[8] = ZCL(4);
-  len_of[7] = ZCL(5);
-  len_of[9] = ZCL(6);
-  len_of[6] = ZCL(7);
-  len_of[10] = ZCL(8);
-  len_of[5] = ZCL(9);
-  len_of[11] = ZCL(10);
-  len_of[4] = ZCL(11);
-  len_of[12] = ZCL(12);
-  len_of[3] = ZCL(13);
-  len_of[13] = ZCL(14);
-  len_of[2] = ZCL(15);
-  len_of[14] = ZCL(16);
-  len_of[1] = ZCL(17);
-  len_of[15] = ZCL(18);
-#undef ZCL
-  uint32_t cnt[8];
-#pragma unroll
-  for (uint32_t L = 0; L < 8; L++) cnt[L] = 0;
-  uint32_t k = 0;
-#pragma unroll
-  for (uint32_t L = 1; L < 8; L++) {
-#pragma unroll
-    for (uint32_t s = 0; s < 19; s++) {
-      if (len_of[s] == L) {
-        sorted[k] = (uint8_t)s;
-        k++;
-        cnt[L]++;
-      }
-    }
-  }
-  uint32_t p = q + 17 + 3 * hclen;  // next bit
-  const uint32_t total = nlen + ndist, end = q + avail;
-  uint32_t idx = 0, prev = 0, kll = 0, kd = 0, mll = 0, md = 0;
-  bool eob = false;
-  while (idx < total) {
-    if (p + 32 > end) return false;  // the header would run past the staged bytes
-    const uint32_t b = (uint32_t)bits64(w, p);
-    // canonical decode, bit by bit (codes of at most 7 bits)
-    uint32_t code = 0, first = 0, index = 0, sym = 32, used = 0;
-#pragma unroll
-    for (uint32_t L = 1; L < 8; L++) {
-      if (sym == 32) {
-        code |= (b >> (L - 1)) & 1u;
-        const uint32_t c = cnt[L];
-        if (code - first < c) {
-          sym = sorted[index + code - first];
-          used = L;
-        } else {
-          index += c;
-          first = (first + c) << 1;
-          code <<= 1;
-        }
-      }
-    }
-    if (sym == 32) return false;
-    p += used;
-    const uint32_t x = b >> used;
-    uint32_t val, rep;
-    if (sym < 16) {
-      val = sym;
-      rep = 1;
-      prev = sym;
-    } else if (sym == 16) {
-      if (idx == 0) return false;
-      val = prev;
-      rep = 3 + (x & 3u);
-      p += 2;
-    } else if (sym == 17) {
-      val = 0;
-      rep = 3 + (x & 7u);
-      p += 3;
-      prev = 0;
-    } else {
-      val = 0;
-      rep = 11 + (x & 127u);
-      p += 7;
-      prev = 0;
-    }
-    if (idx + rep > total) return false;
-    if (val) {
-      // split the run at the literal/length | distance boundary
-      const uint32_t in_ll = idx < nlen ? (nlen - idx < rep ? nlen - idx : rep) : 0u;
-      kll += in_ll << (15 - val);
-      kd += (rep - in_ll) << (15 - val);
-      if (in_ll) mll = val > mll ? val : mll;
-      if (rep > in_ll) md = val > md ? val : md;
-      if (idx <= 256 && 256 < idx + rep) eob = true;
-    }
-    idx += rep;
-  }
-  if (!eob) return false;
-  if (kll > 32768u || (kll < 32768u && mll != 1u)) return false;
-  if (kd > 32768u || (kd < 32768u && md > 1u)) return false;
-  return true;
-}
 
 struct FindArgs {
   const uint8_t *src;
@@ -226,7 +85,7 @@ __global__ __launch_bounds__(kFindThreads) void inflate_find_kernel(FindArgs a) 
     __syncthreads();
     const uint32_t npos = 8u * (uint32_t)(whi - wlo);
     for (uint32_t q = tid; q < npos; q += kFindThreads) {
-      if (quick_ok(w, q)) {
+      if (find::quick_ok(w, q)) {
         const uint32_t i = atomicAdd(&nsurv, 1u);
         if (i < kFindSurv) surv[i] = q;
       }
@@ -235,7 +94,7 @@ __global__ __launch_bounds__(kFindThreads) void inflate_find_kernel(FindArgs a) 
     const uint32_t ns = nsurv < kFindSurv ? nsurv : kFindSurv;  // more: the rest go unchecked (only parallelism is lost)
     for (uint32_t i = tid; i < ns; i += kFindThreads) {
       const uint32_t q = surv[i];
-      if (full_ok(w, q, 8u * nbytes - q, sorted[i])) atomicMin(&best, q);
+      if (find::full_ok(w, q, 8u * nbytes - q, sorted[i])) atomicMin(&best, q);
     }
     __syncthreads();
     if (best != 0xFFFFFFFFu) found = 8 * wlo + best;
