@@ -4,7 +4,6 @@
 # then single-entry timings; then the GPU suite, smoke and default bench.
 set -e -o pipefail
 O=gpurun_out/s25; mkdir -p $O
-: skip (s24 passed) timeout -k 10 300 python3 -u -m pytest tests/test_gpu_inflate.py -x -v --timeout 120 --timeout-method thread > $O/pytest_inflate.log 2>&1
 timeout -k 10 400 python3 -u -m pytest tests/test_gpu_inflate_split.py -x -v --timeout 120 --timeout-method thread > $O/pytest_split.log 2>&1
 timeout -k 10 300 python3 -u tools/bench_inflate_one.py --sizes 1,16,64 --reps 5 > $O/bench_inflate_one.jsonl 2> $O/bench_inflate_one.err
 timeout -k 10 900 python3 -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > $O/pytest_gpu.log 2>&1
