@@ -14,8 +14,13 @@ extern "C" int find_flags(const uint8_t *data, size_t n, uint8_t *flags) {
   std::vector<uint32_t> w((n + 3) / 4 + 8, 0u);
   memcpy(w.data(), data, n);
   uint8_t sorted[20];
+  uint16_t lut[512];
+  for (uint32_t t = 0; t < 512; t++) lut[t] = (uint16_t)zcrc::find::kraft3(t);
   for (size_t q = 0; q < 8 * n; q++) {
-    const bool a = zcrc::find::quick_ok(w.data(), (uint32_t)q);
+    const size_t i = q >> 5;
+    uint32_t x0, x1, x2;
+    zcrc::find::window96(w[i], w[i + 1], w[i + 2], w[i + 3], (uint32_t)(q & 31), x0, x1, x2);
+    const bool a = zcrc::find::quick_ok3(x0, x1, x2, lut);
     const bool b = a && zcrc::find::full_ok(w.data(), (uint32_t)q, (uint32_t)(8 * n - q), sorted);
     flags[q] = (uint8_t)(a | (b << 1));
   }

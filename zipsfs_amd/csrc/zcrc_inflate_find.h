@@ -19,23 +19,40 @@ __host__ __device__ inline uint64_t bits64(const uint32_t *w, uint32_t q) {
   return lo | hi;
 }
 
-// Quick filter at bit q: BTYPE = 2, HLIT <= 29, HDIST <= 29, and a complete
-// code-length code (zlib rejects an incomplete one).  ~0.1% of the positions
-// of compressed data pass (tests/test_inflate_split.py measures it).
-__host__ __device__ inline bool quick_ok(const uint32_t *w, uint32_t q) {
-  const uint64_t v = bits64(w, q);
-  if (((v >> 1) & 3u) != 2u) return false;
-  if (((v >> 3) & 31u) > 29u || ((v >> 8) & 31u) > 29u) return false;
-  const uint32_t hclen = (uint32_t)((v >> 13) & 15u) + 4u;
-  uint64_t cl = bits64(w, q + 17);
-  cl &= (hclen == 19u) ? ((1ull << 57) - 1) : ((1ull << (3 * hclen)) - 1);
+// Kraft contribution (units of 2^-7) of the three 3-bit code lengths packed
+// in t (9 bits): the finder keeps these 512 values in LDS.
+__host__ __device__ inline uint32_t kraft3(uint32_t t) {
+  uint32_t s = 0;
+  for (uint32_t f = 0; f < 3; f++) {
+    const uint32_t l = (t >> (3 * f)) & 7u;
+    s += l ? (128u >> l) : 0u;
+  }
+  return s;
+}
+
+// Quick filter on the 96 bits x0 | x1 << 32 | x2 << 64 that start at the
+// candidate position: BTYPE = 2, HLIT <= 29, HDIST <= 29, and a complete
+// code-length code (zlib rejects an incomplete one; its HCLEN + 4 lengths of
+// 3 bits follow the 17 header bits), summed from `lut` (kraft3 of every
+// 9-bit triple).  ~0.1% of the positions of compressed data pass
+// (tests/test_inflate_find.py).
+__host__ __device__ inline bool quick_ok3(uint32_t x0, uint32_t x1, uint32_t x2, const uint16_t *lut) {
+  const bool head = ((x0 >> 1) & 3u) == 2u && ((x0 >> 3) & 31u) <= 29u && ((x0 >> 8) & 31u) <= 29u;
+  const uint32_t hclen = ((x0 >> 13) & 15u) + 4u;
+  uint64_t cl = (uint64_t)(x0 >> 17) | ((uint64_t)x1 << 15) | ((uint64_t)x2 << 47);
+  cl &= (1ull << (3 * hclen)) - 1;  // 3 hclen <= 57
   uint32_t kraft = 0;
 #pragma unroll
-  for (uint32_t i = 0; i < 19; i++) {
-    const uint32_t l = (uint32_t)(cl >> (3 * i)) & 7u;
-    kraft += l ? (128u >> l) : 0u;
-  }
-  return kraft == 128u;
+  for (uint32_t g = 0; g < 7; g++) kraft += lut[(uint32_t)(cl >> (9 * g)) & 511u];
+  return head && kraft == 128u;
+}
+
+// the 96 bits from bit b (< 32) of the words w0..w3
+__host__ __device__ inline void window96(uint32_t w0, uint32_t w1, uint32_t w2, uint32_t w3, uint32_t b, uint32_t &x0,
+                                         uint32_t &x1, uint32_t &x2) {
+  x0 = (uint32_t)((((uint64_t)w1 << 32) | w0) >> b);
+  x1 = (uint32_t)((((uint64_t)w2 << 32) | w1) >> b);
+  x2 = (uint32_t)((((uint64_t)w3 << 32) | w2) >> b);
 }
 
 // The full dynamic-header check at bit q (lane-parallel: each thread its own

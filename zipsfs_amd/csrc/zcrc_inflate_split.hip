@@ -52,18 +52,28 @@ struct FindArgs {
 };
 
 // One workgroup per chunk k >= 1: the first bit position in [8 k chunk,
-// 8 (k+1) chunk) that passes full_ok, in windows of kFindWin bytes.
+// 8 (k+1) chunk) that passes full_ok.  The chunk is staged in windows of
+// kFindWin bytes; each thread tests the 32 positions of one staged word at a
+// time (a 96-bit funnel of four words per position, the code-length Kraft
+// sum from a 512-entry LDS table), in sub-windows of 4 KiB, and the
+// survivors of a sub-window get the full check before the next one starts:
+// the search stops at the first sub-window with a true start.
+constexpr uint32_t kFindSub = kFindThreads;  // words per sub-window (32 positions each)
 __global__ __launch_bounds__(kFindThreads) void inflate_find_kernel(FindArgs a) {
   __shared__ uint32_t w[kFindWords];
+  __shared__ uint16_t lut[512];
   __shared__ uint32_t surv[kFindSurv];
   __shared__ uint8_t sorted[kFindSurv][20];
-  __shared__ uint32_t nsurv, best;
+  // per sub-window parity: its survivor count and best position (double-
+  // buffered: a count is reset one sub-window after it was last read)
+  __shared__ uint32_t nsurv[2], best[2];
   const uint32_t tid = threadIdx.x;
   const uint64_t k = blockIdx.x;
   if (k == 0) {
     if (tid == 0) a.cand[0] = 0;
     return;
   }
+  if (tid < 512) lut[tid] = (uint16_t)find::kraft3(tid);
   const uint64_t lo = k * a.chunk;
   const uint64_t hi = lo + a.chunk < a.src_len ? lo + a.chunk : a.src_len;
   uint64_t found = kSplitNone;
@@ -71,7 +81,6 @@ __global__ __launch_bounds__(kFindThreads) void inflate_find_kernel(FindArgs a) 
     const uint64_t whi = wlo + kFindWin < hi ? wlo + kFindWin : hi;  // positions [wlo, whi)
     const uint64_t send = whi + kFindLook < a.src_len ? whi + kFindLook : a.src_len;
     const uint32_t nbytes = (uint32_t)(send - wlo);
-    if (tid == 0) nsurv = 0, best = 0xFFFFFFFFu;
     // stage [wlo, send) as little-endian words, zeros past the end
     for (uint32_t i = tid; i < kFindWords; i += kFindThreads) {
       uint32_t v = 0;
@@ -82,23 +91,38 @@ __global__ __launch_bounds__(kFindThreads) void inflate_find_kernel(FindArgs a) 
       }
       w[i] = v;
     }
-    __syncthreads();
+    if (tid == 0) nsurv[0] = nsurv[1] = 0, best[0] = best[1] = 0xFFFFFFFFu;
+    __syncthreads();  // staged; counters reset
     const uint32_t npos = 8u * (uint32_t)(whi - wlo);
-    for (uint32_t q = tid; q < npos; q += kFindThreads) {
-      if (find::quick_ok(w, q)) {
-        const uint32_t i = atomicAdd(&nsurv, 1u);
-        if (i < kFindSurv) surv[i] = q;
+    for (uint32_t sub = 0; sub * 32u * kFindSub < npos; sub++) {
+      const uint32_t p = sub & 1u;
+      const uint32_t i = sub * kFindSub + tid;  // this thread's word: positions 32 i .. 32 i + 31
+      if (32u * i < npos) {
+        const uint32_t w0 = w[i], w1 = w[i + 1], w2 = w[i + 2], w3 = w[i + 3];
+        for (uint32_t b = 0; b < 32; b++) {
+          uint32_t x0, x1, x2;
+          find::window96(w0, w1, w2, w3, b, x0, x1, x2);
+          if (find::quick_ok3(x0, x1, x2, lut) && 32u * i + b < npos) {
+            const uint32_t j = atomicAdd(&nsurv[p], 1u);
+            if (j < kFindSurv) surv[j] = 32u * i + b;
+          }
+        }
+      }
+      __syncthreads();  // every thread has also read the other parity's counters of the last sub-window
+      if (tid == 0) nsurv[p ^ 1u] = 0, best[p ^ 1u] = 0xFFFFFFFFu;
+      const uint32_t ns = nsurv[p] < kFindSurv ? nsurv[p] : kFindSurv;  // more: the rest go unchecked (parallelism lost, never correctness)
+      for (uint32_t j = tid; j < ns; j += kFindThreads) {
+        const uint32_t q = surv[j];
+        if (find::full_ok(w, q, 8u * nbytes - q, sorted[j])) atomicMin(&best[p], q);
+      }
+      __syncthreads();
+      const uint32_t bq = best[p];  // workgroup-uniform
+      if (bq != 0xFFFFFFFFu) {
+        found = 8 * wlo + bq;
+        break;
       }
     }
-    __syncthreads();
-    const uint32_t ns = nsurv < kFindSurv ? nsurv : kFindSurv;  // more: the rest go unchecked (only parallelism is lost)
-    for (uint32_t i = tid; i < ns; i += kFindThreads) {
-      const uint32_t q = surv[i];
-      if (find::full_ok(w, q, 8u * nbytes - q, sorted[i])) atomicMin(&best, q);
-    }
-    __syncthreads();
-    if (best != 0xFFFFFFFFu) found = 8 * wlo + best;
-    __syncthreads();  // before the next window overwrites w / nsurv
+    __syncthreads();  // before the next window overwrites w
   }
   if (tid == 0) a.cand[k] = found;
 }
@@ -231,44 +255,77 @@ struct ResolveArgs {
 };
 
 // element -> byte: a marker is byte (v - kInflateMarker) of the kInflateHist
-// bytes before the chunk at output offset `off`.  (One helper shared by an
-// LDS-ring and a global-memory caller crashed the compiler's inliner: two.)
-__device__ __forceinline__ uint8_t resolve_ring(uint32_t v, const uint8_t *ring, uint64_t off) {
-  return v < kInflateMarker ? (uint8_t)v : ring[(off - kInflateHist + (v - kInflateMarker)) & (kInflateHist - 1)];
-}
+// bytes before the chunk at output offset `off`.  (A helper shared with the
+// tails kernel's LDS-ring form crashed the compiler's inliner.)
 __device__ __forceinline__ uint8_t resolve_dst(uint32_t v, const uint8_t *dst, uint64_t off) {
   return v < kInflateMarker ? (uint8_t)v : dst[off - kInflateHist + (v - kInflateMarker)];
 }
 
 // The last 32 KiB of every chain chunk, in chain order, through an LDS ring
 // of the last 32 KiB of output: chunk m's markers read bytes of chunks
-// before it, all in the ring when its turn comes.
+// before it, all in the ring when its turn comes.  The only sequential
+// step of the scheme: the next chunk's elements (and the metadata two steps
+// ahead) are loaded while the current one is resolved, so a step costs its
+// LDS work and two barriers, not a memory round trip.
 __global__ __launch_bounds__(1024) void inflate_tails_kernel(ResolveArgs a) {
   __shared__ uint8_t ring[kInflateHist];
   const uint32_t tid = threadIdx.x;
   const uint32_t m_end = a.chain[a.nchunks];
   constexpr uint32_t kPer = kInflateHist / 1024;
-  for (uint32_t m = 0; m < m_end; m++) {
-    const uint32_t k = a.chain[m];
-    const uint64_t len = a.rec[k].out_len, off = a.off[k];
-    const uint64_t t0 = len > kInflateHist ? len - kInflateHist : 0;
-    const uint16_t *el = a.region + k * a.region_elems;
-    uint8_t v[kPer];
-#pragma unroll
-    for (uint32_t j = 0; j < kPer; j++) {
-      const uint64_t e = t0 + tid + 1024u * j;
-      v[j] = e < len ? resolve_ring(el[e], ring, off) : 0;
+  constexpr uint32_t kMask = kInflateHist - 1;
+  // step m: the chunk's tail through buffer resources (thread t's element j
+  // is tail element t + 1024 j; the range check, which covers voffset but
+  // not soffset, drops what lies past the tail -- no 64-bit addresses)
+  struct Step {
+    uint32_t hist;  // (chunk's output offset) mod 32 Ki: marker w is ring[(hist + w) mod 32 Ki]
+    uint32_t pos;   // (tail's output offset) mod 32 Ki
+    uint32_t n;     // tail elements
+    __amdgpu_buffer_rsrc_t src, dst;
+  };
+  auto step_of = [&](uint32_t m) {
+    uint64_t off = 0, t0 = 0, n = 0;
+    const uint16_t *el = a.region;
+    if (m < m_end) {
+      const uint32_t k = a.chain[m];
+      const uint64_t len = a.rec[k].out_len;
+      t0 = len > kInflateHist ? len - kInflateHist : 0;
+      n = len - t0;
+      off = a.off[k];
+      el = a.region + k * a.region_elems + t0;
     }
+    Step st;
+    st.hist = (uint32_t)off & kMask;
+    st.pos = (uint32_t)(off + t0) & kMask;
+    st.n = (uint32_t)n;
+    st.src = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t *>(el), (short)0, (int)(2 * n), 0x00020000);
+    st.dst = __builtin_amdgcn_make_buffer_rsrc(a.dst + off + t0, (short)0, (int)n, 0x00020000);
+    return st;
+  };
+  auto load = [&](const Step &st, uint32_t *raw) {
+#pragma unroll
+    for (uint32_t j = 0; j < kPer; j++) raw[j] = __builtin_amdgcn_raw_buffer_load_b16(st.src, 2 * (tid + 1024u * j), 0, 0);
+  };
+  Step cur = step_of(0), nxt = step_of(1);
+  uint32_t raw[kPer];
+  load(cur, raw);
+  for (uint32_t m = 0; m < m_end; m++) {
+    uint32_t v[kPer];
+#pragma unroll
+    for (uint32_t j = 0; j < kPer; j++)
+      v[j] = raw[j] < kInflateMarker ? raw[j] : ring[(cur.hist + raw[j] - kInflateMarker) & kMask];
+    const Step after = step_of(m + 2);
+    load(nxt, raw);  // step m + 1's elements, in flight during the rest of this step
     __syncthreads();  // every marker read its history before the ring moves on
+    // (stores past the tail are dropped by the range check; ring slots past
+    // it hold the next chunk's history and are not touched)
 #pragma unroll
     for (uint32_t j = 0; j < kPer; j++) {
-      const uint64_t e = t0 + tid + 1024u * j;
-      if (e < len) {
-        ring[(off + e) & (kInflateHist - 1)] = v[j];
-        a.dst[off + e] = v[j];
-      }
+      __builtin_amdgcn_raw_buffer_store_b8((uint8_t)v[j], cur.dst, tid + 1024u * j, 0, 0);
+      if (tid + 1024u * j < cur.n) ring[(cur.pos + tid + 1024u * j) & kMask] = (uint8_t)v[j];
     }
     __syncthreads();
+    cur = nxt;
+    nxt = after;
   }
 }
 
@@ -294,8 +351,17 @@ __global__ __launch_bounds__(256) void inflate_body_kernel(ResolveArgs a) {
 
 }  // namespace
 
-uint64_t inflate_split_chunk(uint64_t src_len, uint64_t want) {
-  uint64_t c = want ? want : kInflateSplitChunk;
+uint64_t inflate_split_chunk(uint64_t src_len, uint64_t want, int num_cus) {
+  // Default: kInflateSplitChunk, or larger so that the chunks just fill the
+  // speculative decoder's resident workgroups (kSpecPerCu per CU): more
+  // chunks than that only queue (the decode time stays ~src_len / (resident
+  // x rate)) and lengthen the tails kernel's chain.
+  uint64_t c = want;
+  if (!c) {
+    const uint64_t resident = (uint64_t)kSpecPerCu * (uint64_t)(num_cus > 0 ? num_cus : 1);
+    c = (src_len + resident - 1) / resident;
+    if (c < kInflateSplitChunk) c = kInflateSplitChunk;
+  }
   const uint64_t need = (src_len + kChainLds - 1) / kChainLds;  // at most kChainLds chunks
   return c < need ? need : c;
 }

@@ -159,7 +159,8 @@ constexpr uint64_t kInflateSplitSlack = 16384;  // elements added to each chunk'
 constexpr uint64_t kInflateSplitMinSrc = 65536; // smaller streams decode serially
 // chunk size for a stream (want = 0: the default), the scratch the split
 // decode of one stream needs, and the launch chain (zcrc_inflate_split.hip)
-uint64_t inflate_split_chunk(uint64_t src_len, uint64_t want);
+uint64_t inflate_split_chunk(uint64_t src_len, uint64_t want, int num_cus);
+constexpr uint32_t kSpecPerCu = 4;  // sp::inflate_spec_kernel workgroups per CU (34.5 KB of LDS each)
 uint64_t inflate_split_scratch_bytes(uint64_t src_len, uint64_t cap, uint64_t chunk);
 hipError_t launch_inflate_split(const uint8_t *src, uint64_t src_len, uint8_t *dst, uint64_t cap,
                                 uint64_t *out_len, int32_t *status, uint64_t chunk, void *scratch, int num_cus,

@@ -1553,7 +1553,7 @@ int zcrc_inflate_device(const void *d_src, uint64_t src_len, void *d_dst, uint64
     return ZCRC_OK;
   }
   // streams below kInflateSplitMinSrc: one chunk (the same kernels, no split)
-  const uint64_t chunk = src_len < kInflateSplitMinSrc ? src_len : inflate_split_chunk(src_len, chunk_bytes);
+  const uint64_t chunk = src_len < kInflateSplitMinSrc ? src_len : inflate_split_chunk(src_len, chunk_bytes, dc->num_cus);
   const size_t need = inflate_split_scratch_bytes(src_len, cap, chunk);
   void *scratch = nullptr;
   size_t have = 0;
