@@ -84,7 +84,7 @@ def main():
                     "split_ms": round(t_split, 3), "split_gbs": round(size / t_split / 1e6, 2),
                     "one_wave_ms": None if t_serial is None else round(t_serial, 3),
                     "zlib_1core_ms": round(t_cpu, 3), "zlib_1core_gbs": round(size / t_cpu / 1e6, 3),
-                    "speedup_vs_1core": round(t_cpu / t_split, 2), "chunk": args.chunk or 16384}
+                    "speedup_vs_1core": round(t_cpu / t_split, 2), "chunk": args.chunk or "auto"}
             print(json.dumps(line), flush=True)
 
 

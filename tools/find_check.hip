@@ -1,6 +1,6 @@
 // tools/find_check.hip -- host build of the block-parallel inflate's block-
 // start test (zipsfs_amd/csrc/zcrc_inflate_find.h) for the CPU test
-// tests/test_inflate_find.py: flags[q] = quick_ok(q) | full_ok(q) << 1 for
+// tests/test_inflate_find.py: flags[q] = quick filter (head_ok && cl_ok) | full_ok << 1 for
 // every bit position q of a stream, with the stream staged as the finder
 // kernel stages it (little-endian words, zeros past the end).  Test tooling.
 #include <stdint.h>
@@ -14,13 +14,11 @@ extern "C" int find_flags(const uint8_t *data, size_t n, uint8_t *flags) {
   std::vector<uint32_t> w((n + 3) / 4 + 8, 0u);
   memcpy(w.data(), data, n);
   uint8_t sorted[20];
-  uint16_t lut[512];
-  for (uint32_t t = 0; t < 512; t++) lut[t] = (uint16_t)zcrc::find::kraft3(t);
   for (size_t q = 0; q < 8 * n; q++) {
     const size_t i = q >> 5;
     uint32_t x0, x1, x2;
     zcrc::find::window96(w[i], w[i + 1], w[i + 2], w[i + 3], (uint32_t)(q & 31), x0, x1, x2);
-    const bool a = zcrc::find::quick_ok3(x0, x1, x2, lut);
+    const bool a = zcrc::find::head_ok(x0) && zcrc::find::cl_ok(x0, x1, x2);
     const bool b = a && zcrc::find::full_ok(w.data(), (uint32_t)q, (uint32_t)(8 * n - q), sorted);
     flags[q] = (uint8_t)(a | (b << 1));
   }

@@ -19,32 +19,27 @@ __host__ __device__ inline uint64_t bits64(const uint32_t *w, uint32_t q) {
   return lo | hi;
 }
 
-// Kraft contribution (units of 2^-7) of the three 3-bit code lengths packed
-// in t (9 bits): the finder keeps these 512 values in LDS.
-__host__ __device__ inline uint32_t kraft3(uint32_t t) {
-  uint32_t s = 0;
-  for (uint32_t f = 0; f < 3; f++) {
-    const uint32_t l = (t >> (3 * f)) & 7u;
-    s += l ? (128u >> l) : 0u;
-  }
-  return s;
+// Quick filter, in two parts, on the 96 bits x0 | x1 << 32 | x2 << 64 that
+// start at the candidate position.  head_ok: BTYPE = 2, HLIT <= 29, HDIST
+// <= 29 (~22% of the positions of compressed data pass).  cl_ok: the
+// HCLEN + 4 code-length code lengths (3 bits each, after the 17 header bits)
+// form a complete code -- zlib rejects an incomplete one (~0.4% of those
+// pass; tests/test_inflate_find.py).  The finder runs cl_ok only on the
+// positions head_ok kept.
+__host__ __device__ inline bool head_ok(uint32_t x0) {
+  return ((x0 >> 1) & 3u) == 2u && ((x0 >> 3) & 31u) <= 29u && ((x0 >> 8) & 31u) <= 29u;
 }
-
-// Quick filter on the 96 bits x0 | x1 << 32 | x2 << 64 that start at the
-// candidate position: BTYPE = 2, HLIT <= 29, HDIST <= 29, and a complete
-// code-length code (zlib rejects an incomplete one; its HCLEN + 4 lengths of
-// 3 bits follow the 17 header bits), summed from `lut` (kraft3 of every
-// 9-bit triple).  ~0.1% of the positions of compressed data pass
-// (tests/test_inflate_find.py).
-__host__ __device__ inline bool quick_ok3(uint32_t x0, uint32_t x1, uint32_t x2, const uint16_t *lut) {
-  const bool head = ((x0 >> 1) & 3u) == 2u && ((x0 >> 3) & 31u) <= 29u && ((x0 >> 8) & 31u) <= 29u;
+__host__ __device__ inline bool cl_ok(uint32_t x0, uint32_t x1, uint32_t x2) {
   const uint32_t hclen = ((x0 >> 13) & 15u) + 4u;
   uint64_t cl = (uint64_t)(x0 >> 17) | ((uint64_t)x1 << 15) | ((uint64_t)x2 << 47);
   cl &= (1ull << (3 * hclen)) - 1;  // 3 hclen <= 57
-  uint32_t kraft = 0;
+  uint32_t kraft = 0;  // units of 2^-7
 #pragma unroll
-  for (uint32_t g = 0; g < 7; g++) kraft += lut[(uint32_t)(cl >> (9 * g)) & 511u];
-  return head && kraft == 128u;
+  for (uint32_t i = 0; i < 19; i++) {
+    const uint32_t l = (uint32_t)(cl >> (3 * i)) & 7u;
+    kraft += (128u >> l) & (0u - (uint32_t)(l != 0));
+  }
+  return kraft == 128u;
 }
 
 // the 96 bits from bit b (< 32) of the words w0..w3

@@ -54,14 +54,15 @@ struct FindArgs {
 // One workgroup per chunk k >= 1: the first bit position in [8 k chunk,
 // 8 (k+1) chunk) that passes full_ok.  The chunk is staged in windows of
 // kFindWin bytes; each thread tests the 32 positions of one staged word at a
-// time (a 96-bit funnel of four words per position, the code-length Kraft
-// sum from a 512-entry LDS table), in sub-windows of 4 KiB, and the
-// survivors of a sub-window get the full check before the next one starts:
-// the search stops at the first sub-window with a true start.
+// time (a 96-bit funnel of four words per position): the cheap header test
+// on all 32 gives a mask, the code-length Kraft sum runs only on its set bits
+// (a 512-entry LDS table of triple contributions, read at random addresses, cost more
+// than the arithmetic: bank conflicts).  Sub-windows of 4 KiB; the survivors
+// of a sub-window get the full check before the next one starts, and the
+// search stops at the first sub-window with a true start.
 constexpr uint32_t kFindSub = kFindThreads;  // words per sub-window (32 positions each)
 __global__ __launch_bounds__(kFindThreads) void inflate_find_kernel(FindArgs a) {
   __shared__ uint32_t w[kFindWords];
-  __shared__ uint16_t lut[512];
   __shared__ uint32_t surv[kFindSurv];
   __shared__ uint8_t sorted[kFindSurv][20];
   // per sub-window parity: its survivor count and best position (double-
@@ -73,7 +74,6 @@ __global__ __launch_bounds__(kFindThreads) void inflate_find_kernel(FindArgs a) 
     if (tid == 0) a.cand[0] = 0;
     return;
   }
-  if (tid < 512) lut[tid] = (uint16_t)find::kraft3(tid);
   const uint64_t lo = k * a.chunk;
   const uint64_t hi = lo + a.chunk < a.src_len ? lo + a.chunk : a.src_len;
   uint64_t found = kSplitNone;
@@ -99,10 +99,19 @@ __global__ __launch_bounds__(kFindThreads) void inflate_find_kernel(FindArgs a) 
       const uint32_t i = sub * kFindSub + tid;  // this thread's word: positions 32 i .. 32 i + 31
       if (32u * i < npos) {
         const uint32_t w0 = w[i], w1 = w[i + 1], w2 = w[i + 2], w3 = w[i + 3];
+        uint32_t mask = 0;
+#pragma unroll
         for (uint32_t b = 0; b < 32; b++) {
+          const uint32_t x0 = (uint32_t)((((uint64_t)w1 << 32) | w0) >> b);
+          mask |= (uint32_t)find::head_ok(x0) << b;
+        }
+        if (32u * i + 32u > npos) mask &= (1u << (npos - 32u * i)) - 1u;  // npos is a multiple of 8
+        while (mask) {
+          const uint32_t b = (uint32_t)__builtin_ctz(mask);
+          mask &= mask - 1u;
           uint32_t x0, x1, x2;
           find::window96(w0, w1, w2, w3, b, x0, x1, x2);
-          if (find::quick_ok3(x0, x1, x2, lut) && 32u * i + b < npos) {
+          if (find::cl_ok(x0, x1, x2)) {
             const uint32_t j = atomicAdd(&nsurv[p], 1u);
             if (j < kFindSurv) surv[j] = 32u * i + b;
           }

@@ -154,7 +154,7 @@ constexpr uint64_t kInflateMaxSrc = 0xF0000000ull;  // 32-bit buffer range and b
 // (used when the batch exceeds the streams resident at once; may be null)
 hipError_t launch_inflate(const InflateArgs &args, int num_cus, hipStream_t stream, uint32_t *order_scratch);
 hipError_t launch_inflate_spec(const SpecArgs &args, hipStream_t stream);
-constexpr uint64_t kInflateSplitChunk = 16384;  // compressed bytes per chunk (at most 16,384 chunks)
+constexpr uint64_t kInflateSplitChunk = 8192;   // compressed bytes per chunk (at least; at most 16,384 chunks)
 constexpr uint64_t kInflateSplitSlack = 16384;  // elements added to each chunk's region
 constexpr uint64_t kInflateSplitMinSrc = 65536; // smaller streams decode serially
 // chunk size for a stream (want = 0: the default), the scratch the split
