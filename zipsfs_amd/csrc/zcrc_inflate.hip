@@ -63,15 +63,29 @@ namespace w32 {  // the whole 32 KiB window in LDS: four streams per CU
 #include "zcrc_inflate_impl.h"
 #undef ZI_WIN
 }  // namespace w32
-namespace sp {  // speculative chunk decode (16-bit elements, zcrc_inflate_split.hip): 16 Ki-element ring
+// speculative chunk decode (16-bit elements, zcrc_inflate_split.hip): the
+// whole 32 Ki-element history in LDS (two streams per CU, no reads of older
+// output back from HBM -- on text ~13% of the matches reach past 16 Ki), or
+// a 16 Ki-element ring at four per CU for streams with more chunks than
+// that many resident decoders
+namespace sp32 {
+#define ZI_WIN 32768u
+#define ZI_SPEC 1
+#include "zcrc_inflate_impl.h"
+#undef ZI_SPEC
+#undef ZI_WIN
+}  // namespace sp32
+namespace sp16 {
 #define ZI_WIN 16384u
 #define ZI_SPEC 1
 #include "zcrc_inflate_impl.h"
 #undef ZI_SPEC
 #undef ZI_WIN
-}  // namespace sp
+}  // namespace sp16
 
-hipError_t launch_inflate_spec(const SpecArgs &args, hipStream_t stream) { return sp::launch_spec(args, stream); }
+hipError_t launch_inflate_spec(const SpecArgs &args, bool wide, hipStream_t stream) {
+  return wide ? sp32::launch_spec(args, stream) : sp16::launch_spec(args, stream);
+}
 
 // Longest-first dispatch.  Workgroups start in index order, so when a batch
 // has more streams than can be resident, a slow stream that happens to sit

@@ -19,9 +19,10 @@
 //   3. inflate_chain_kernel: follows the links from chunk 0 (a true start, so
 //      every chunk it reaches started at a true block boundary), checks the
 //      chain (statuses, history reach, capacity) and lays the chunks out.
-//   4. inflate_tails_kernel: the last 32 KiB of each chain chunk resolved in
-//      chain order through an LDS window; inflate_body_kernel: all other
-//      elements in parallel, from the resolved tails in dst.
+//   4. inflate_win_*_kernel: the 32 KiB window after each chain chunk, as
+//      bytes and references to the previous window, resolved by pointer
+//      jumping in log2(chunks) parallel rounds, its tail stored to dst;
+//      inflate_body_kernel: all other elements in parallel, from the tails.
 //   5. When the chain fails, the serial kernel (one wave) decodes the stream
 //      and reports zlib's exact status: launch_inflate with run_if.
 //
@@ -29,6 +30,7 @@
 // and the GPU tests compare the bytes with zlib.decompress.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include "../../include/zcrc.h"
 #include "zcrc_inflate_find.h"
@@ -264,78 +266,73 @@ struct ResolveArgs {
 };
 
 // element -> byte: a marker is byte (v - kInflateMarker) of the kInflateHist
-// bytes before the chunk at output offset `off`.  (A helper shared with the
-// tails kernel's LDS-ring form crashed the compiler's inliner.)
+// bytes before the chunk at output offset `off`.
 __device__ __forceinline__ uint8_t resolve_dst(uint32_t v, const uint8_t *dst, uint64_t off) {
   return v < kInflateMarker ? (uint8_t)v : dst[off - kInflateHist + (v - kInflateMarker)];
 }
 
-// The last 32 KiB of every chain chunk, in chain order, through an LDS ring
-// of the last 32 KiB of output: chunk m's markers read bytes of chunks
-// before it, all in the ring when its turn comes.  The only sequential
-// step of the scheme: the next chunk's elements (and the metadata two steps
-// ahead) are loaded while the current one is resolved, so a step costs its
-// LDS work and two barriers, not a memory round trip.
-__global__ __launch_bounds__(1024) void inflate_tails_kernel(ResolveArgs a) {
-  __shared__ uint8_t ring[kInflateHist];
-  const uint32_t tid = threadIdx.x;
-  const uint32_t m_end = a.chain[a.nchunks];
-  constexpr uint32_t kPer = kInflateHist / 1024;
-  constexpr uint32_t kMask = kInflateHist - 1;
-  // step m: the chunk's tail through buffer resources (thread t's element j
-  // is tail element t + 1024 j; the range check, which covers voffset but
-  // not soffset, drops what lies past the tail -- no 64-bit addresses)
-  struct Step {
-    uint32_t hist;  // (chunk's output offset) mod 32 Ki: marker w is ring[(hist + w) mod 32 Ki]
-    uint32_t pos;   // (tail's output offset) mod 32 Ki
-    uint32_t n;     // tail elements
-    __amdgpu_buffer_rsrc_t src, dst;
-  };
-  auto step_of = [&](uint32_t m) {
-    uint64_t off = 0, t0 = 0, n = 0;
-    const uint16_t *el = a.region;
-    if (m < m_end) {
-      const uint32_t k = a.chain[m];
-      const uint64_t len = a.rec[k].out_len;
-      t0 = len > kInflateHist ? len - kInflateHist : 0;
-      n = len - t0;
-      off = a.off[k];
-      el = a.region + k * a.region_elems + t0;
-    }
-    Step st;
-    st.hist = (uint32_t)off & kMask;
-    st.pos = (uint32_t)(off + t0) & kMask;
-    st.n = (uint32_t)n;
-    st.src = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t *>(el), (short)0, (int)(2 * n), 0x00020000);
-    st.dst = __builtin_amdgcn_make_buffer_rsrc(a.dst + off + t0, (short)0, (int)n, 0x00020000);
-    return st;
-  };
-  auto load = [&](const Step &st, uint32_t *raw) {
-#pragma unroll
-    for (uint32_t j = 0; j < kPer; j++) raw[j] = __builtin_amdgcn_raw_buffer_load_b16(st.src, 2 * (tid + 1024u * j), 0, 0);
-  };
-  Step cur = step_of(0), nxt = step_of(1);
-  uint32_t raw[kPer];
-  load(cur, raw);
-  for (uint32_t m = 0; m < m_end; m++) {
-    uint32_t v[kPer];
-#pragma unroll
-    for (uint32_t j = 0; j < kPer; j++)
-      v[j] = raw[j] < kInflateMarker ? raw[j] : ring[(cur.hist + raw[j] - kInflateMarker) & kMask];
-    const Step after = step_of(m + 2);
-    load(nxt, raw);  // step m + 1's elements, in flight during the rest of this step
-    __syncthreads();  // every marker read its history before the ring moves on
-    // (stores past the tail are dropped by the range check; ring slots past
-    // it hold the next chunk's history and are not touched)
-#pragma unroll
-    for (uint32_t j = 0; j < kPer; j++) {
-      __builtin_amdgcn_raw_buffer_store_b8((uint8_t)v[j], cur.dst, tid + 1024u * j, 0, 0);
-      if (tid + 1024u * j < cur.n) ring[(cur.pos + tid + 1024u * j) & kMask] = (uint8_t)v[j];
-    }
-    __syncthreads();
-    cur = nxt;
-    nxt = after;
+// The 32 KiB windows: W_m = the last 32 KiB of output through the end of
+// chain chunk m, one 32-bit entry per byte -- the byte (kWinByte | value) or
+// a reference (c << 15 | p) to byte p of W_c.  Built from the chunk's last
+// 32 Ki elements (a marker w of chunk m refers to byte w of W_{m-1}; when the
+// chunk is shorter than 32 KiB the window's front refers to W_{m-1} shifted),
+// then resolved by pointer jumping: each round replaces a reference by what
+// it points at, so after round r every remaining reference reaches 2^r
+// chunks back, and ceil(log2 chunks) rounds leave bytes only (W_0 has no
+// reference).  Each round is one parallel pass -- the chain's one
+// sequential dependency costs log2(chunks) launches, not a step per chunk
+// (the first form, an LDS ring walked chunk by chunk, took 3-7 us per chunk:
+// 6.8 ms on a 64 MiB entry).
+constexpr uint32_t kWinByte = 0x80000000u;
+struct WinArgs {
+  const uint16_t *region;
+  uint64_t region_elems;
+  const SpecRec *rec;
+  const uint32_t *chain;  // chain[nchunks] = count (0: the serial decode runs instead)
+  const uint64_t *off;
+  uint64_t nchunks;
+  const uint32_t *win_in;  // jump: the previous round's windows
+  uint32_t *win;           // nchunks x kInflateHist entries, by chain position
+  uint8_t *dst;
+};
+
+// grid: (kInflateHist / 1024, nchunks); block (x, m) builds entries
+// [1024 x, 1024 x + 1024) of W_m
+__global__ __launch_bounds__(1024) void inflate_win_build_kernel(WinArgs a) {
+  const uint32_t m = blockIdx.y;
+  if (m >= a.chain[a.nchunks]) return;
+  const uint32_t k = a.chain[m];
+  const uint64_t len = a.rec[k].out_len;
+  const uint32_t n = len < kInflateHist ? (uint32_t)len : kInflateHist;
+  const uint32_t i = blockIdx.x * 1024u + threadIdx.x;
+  uint32_t v;
+  if (i >= kInflateHist - n) {
+    const uint32_t e = a.region[k * a.region_elems + (len - kInflateHist + i)];
+    v = e < kInflateMarker ? (kWinByte | e) : (m ? ((m - 1) << 15) | (e - kInflateMarker) : kWinByte);
+  } else {
+    v = m ? ((m - 1) << 15) | (i + n) : kWinByte;  // W_0's front: before the stream, never referenced
   }
+  a.win[(uint64_t)m * kInflateHist + i] = v;
+}
+
+__global__ __launch_bounds__(1024) void inflate_win_jump_kernel(WinArgs a) {
+  const uint32_t m = blockIdx.y;
+  if (m >= a.chain[a.nchunks]) return;
+  const uint64_t at = (uint64_t)m * kInflateHist + blockIdx.x * 1024u + threadIdx.x;
+  uint32_t v = a.win_in[at];
+  if (!(v & kWinByte)) v = a.win_in[(uint64_t)(v >> 15) * kInflateHist + (v & (kInflateHist - 1))];
+  a.win[at] = v;
+}
+
+// each chunk's last (up to) 32 KiB of output, from its resolved window
+__global__ __launch_bounds__(1024) void inflate_win_store_kernel(WinArgs a) {
+  const uint32_t m = blockIdx.y;
+  if (m >= a.chain[a.nchunks]) return;
+  const uint32_t k = a.chain[m];
+  const uint64_t len = a.rec[k].out_len;
+  const uint32_t n = len < kInflateHist ? (uint32_t)len : kInflateHist;
+  const uint32_t i = blockIdx.x * 1024u + threadIdx.x;
+  if (i >= kInflateHist - n) a.dst[a.off[k] + len - kInflateHist + i] = (uint8_t)a.win[(uint64_t)m * kInflateHist + i];
 }
 
 // Every chain chunk's elements before its last 32 KiB: markers from the
@@ -360,31 +357,43 @@ __global__ __launch_bounds__(256) void inflate_body_kernel(ResolveArgs a) {
 
 }  // namespace
 
-uint64_t inflate_split_chunk(uint64_t src_len, uint64_t want, int num_cus) {
-  // Default: kInflateSplitChunk, or larger so that the chunks just fill the
-  // speculative decoder's resident workgroups (kSpecPerCu per CU): more
-  // chunks than that only queue (the decode time stays ~src_len / (resident
-  // x rate)) and lengthen the tails kernel's chain.
+// Default: chunks of kInflateSplitChunk, or larger so that the chunks just
+// fill the speculative decoder's resident workgroups -- more chunks than
+// that only queue (the decode time stays ~src_len / (resident x rate)) and
+// add pointer-jumping rounds.  The 32 Ki-history decoder (two per CU, no
+// reads of old output back from HBM) while its residents suffice, else the
+// 16 Ki ring (four per CU).  ZCRC_SPLIT_RING=16|32 forces one (measurement).
+InflateSplitShape inflate_split_shape(uint64_t src_len, uint64_t want, int num_cus) {
+  static const int force = [] {
+    const char *e = getenv("ZCRC_SPLIT_RING");
+    return e ? atoi(e) : 0;
+  }();
+  const uint64_t cus = (uint64_t)(num_cus > 0 ? num_cus : 1);
+  InflateSplitShape sh;
+  sh.wide = force ? force == 32 : (src_len + kInflateSplitChunk - 1) / kInflateSplitChunk <= kSpecPerCuWide * cus;
   uint64_t c = want;
   if (!c) {
-    const uint64_t resident = (uint64_t)kSpecPerCu * (uint64_t)(num_cus > 0 ? num_cus : 1);
+    const uint64_t resident = (sh.wide ? kSpecPerCuWide : kSpecPerCu) * cus;
     c = (src_len + resident - 1) / resident;
     if (c < kInflateSplitChunk) c = kInflateSplitChunk;
   }
   const uint64_t need = (src_len + kChainLds - 1) / kChainLds;  // at most kChainLds chunks
-  return c < need ? need : c;
+  sh.chunk = c < need ? need : c;
+  return sh;
 }
 
 uint64_t inflate_split_scratch_bytes(uint64_t src_len, uint64_t cap, uint64_t chunk) {
   const uint64_t nch = src_len ? (src_len + chunk - 1) / chunk : 1;
   const uint64_t relems = ((2 * cap) / nch + kInflateSplitSlack + 7) & ~7ull;
-  return 256 + nch * (8 + sizeof(SpecRec) + 4 + 8) + 8 + 64 + nch * relems * 2 + 64;
+  return 256 + nch * (8 + sizeof(SpecRec) + 4 + 8) + 8 + 64 + nch * relems * 2 + 2 * 4ull * kInflateHist * nch +
+         64 * 12;
 }
 
 // One stream: find, speculative decode, chain, resolve, serial fall-back.
 hipError_t launch_inflate_split(const uint8_t *src, uint64_t src_len, uint8_t *dst, uint64_t cap,
-                                uint64_t *out_len, int32_t *status, uint64_t chunk, void *scratch, int num_cus,
-                                hipStream_t stream) {
+                                uint64_t *out_len, int32_t *status, InflateSplitShape shape, void *scratch,
+                                int num_cus, hipStream_t stream) {
+  const uint64_t chunk = shape.chunk;
   const uint64_t nch = src_len ? (src_len + chunk - 1) / chunk : 1;
   const uint64_t relems = ((2 * cap) / nch + kInflateSplitSlack + 7) & ~7ull;
   uint8_t *p = static_cast<uint8_t *>(scratch);
@@ -403,17 +412,30 @@ hipError_t launch_inflate_split(const uint8_t *src, uint64_t src_len, uint8_t *d
   uint32_t *chain = reinterpret_cast<uint32_t *>(take(4 * (nch + 1)));
   uint64_t *off = reinterpret_cast<uint64_t *>(take(8 * nch));
   uint16_t *region = reinterpret_cast<uint16_t *>(take(2 * nch * relems));
+  uint32_t *win[2] = {reinterpret_cast<uint32_t *>(take(4ull * kInflateHist * nch)),
+                      reinterpret_cast<uint32_t *>(take(4ull * kInflateHist * nch))};
 
   FindArgs fa{src, src_len, chunk, nch, cand};
   hipLaunchKernelGGL(inflate_find_kernel, dim3((unsigned)nch), dim3(kFindThreads), 0, stream, fa);
   SpecArgs sa{src, src_len, cand, rec, region, relems, nch};
-  hipError_t e = launch_inflate_spec(sa, stream);
+  hipError_t e = launch_inflate_spec(sa, shape.wide, stream);
   if (e != hipSuccess) return e;
   ChainArgs ca{rec, nch, cap, chain, off, run_serial, out_len, status, fb_src, fb_src_len, fb_dst, fb_cap,
                src, src_len, dst};
   hipLaunchKernelGGL(inflate_chain_kernel, dim3(1), dim3(1024), 0, stream, ca);
+  // windows: build, ceil(log2 nch) pointer-jumping rounds, store the tails
+  uint32_t rounds = 0;
+  while ((1ull << rounds) < nch) rounds++;
+  WinArgs wa{region, relems, rec, chain, off, nch, nullptr, win[0], dst};
+  const dim3 wgrid(kInflateHist / 1024, (unsigned)nch);
+  hipLaunchKernelGGL(inflate_win_build_kernel, wgrid, dim3(1024), 0, stream, wa);
+  for (uint32_t r = 0; r < rounds; r++) {
+    wa.win_in = win[r & 1];
+    wa.win = win[(r + 1) & 1];
+    hipLaunchKernelGGL(inflate_win_jump_kernel, wgrid, dim3(1024), 0, stream, wa);
+  }
+  hipLaunchKernelGGL(inflate_win_store_kernel, wgrid, dim3(1024), 0, stream, wa);
   ResolveArgs ra{region, relems, rec, chain, off, nch, dst};
-  hipLaunchKernelGGL(inflate_tails_kernel, dim3(1), dim3(1024), 0, stream, ra);
   const unsigned gy = (unsigned)(nch < 4096 ? nch : 4096);
   const unsigned gx = (unsigned)((4u * (unsigned)num_cus + gy - 1) / gy) + 1u;
   hipLaunchKernelGGL(inflate_body_kernel, dim3(gx, gy), dim3(256), 0, stream, ra);

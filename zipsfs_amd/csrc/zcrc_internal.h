@@ -153,18 +153,25 @@ constexpr uint64_t kInflateMaxSrc = 0xF0000000ull;  // 32-bit buffer range and b
 // order_scratch: >= 4 * n bytes of device memory for the dispatch order
 // (used when the batch exceeds the streams resident at once; may be null)
 hipError_t launch_inflate(const InflateArgs &args, int num_cus, hipStream_t stream, uint32_t *order_scratch);
-hipError_t launch_inflate_spec(const SpecArgs &args, hipStream_t stream);
+// wide: the 32 Ki-element-history decoder (kSpecPerCuWide per CU), else the
+// 16 Ki-element ring (kSpecPerCu per CU)
+hipError_t launch_inflate_spec(const SpecArgs &args, bool wide, hipStream_t stream);
 constexpr uint64_t kInflateSplitChunk = 8192;   // compressed bytes per chunk (at least; at most 16,384 chunks)
 constexpr uint64_t kInflateSplitSlack = 16384;  // elements added to each chunk's region
 constexpr uint64_t kInflateSplitMinSrc = 65536; // smaller streams decode serially
 // chunk size for a stream (want = 0: the default), the scratch the split
 // decode of one stream needs, and the launch chain (zcrc_inflate_split.hip)
-uint64_t inflate_split_chunk(uint64_t src_len, uint64_t want, int num_cus);
-constexpr uint32_t kSpecPerCu = 4;  // sp::inflate_spec_kernel workgroups per CU (34.5 KB of LDS each)
+struct InflateSplitShape {
+  uint64_t chunk;  // compressed bytes per chunk
+  bool wide;       // the 32 Ki-element-history decoder
+};
+InflateSplitShape inflate_split_shape(uint64_t src_len, uint64_t want, int num_cus);
+constexpr uint32_t kSpecPerCu = 4;      // sp16::inflate_spec_kernel workgroups per CU (34.5 KB of LDS each)
+constexpr uint32_t kSpecPerCuWide = 2;  // sp32:: (67 KB each)
 uint64_t inflate_split_scratch_bytes(uint64_t src_len, uint64_t cap, uint64_t chunk);
 hipError_t launch_inflate_split(const uint8_t *src, uint64_t src_len, uint8_t *dst, uint64_t cap,
-                                uint64_t *out_len, int32_t *status, uint64_t chunk, void *scratch, int num_cus,
-                                hipStream_t stream);
+                                uint64_t *out_len, int32_t *status, InflateSplitShape shape, void *scratch,
+                                int num_cus, hipStream_t stream);
 // purposes of the runtime's per-stream scratch cache (zcrc_runtime.hip)
 enum ScratchUse { kScratchBatch = 0, kScratchInflateOrder = 1, kScratchFused = 2, kScratchInflateSplit = 3 };
 

@@ -1553,15 +1553,16 @@ int zcrc_inflate_device(const void *d_src, uint64_t src_len, void *d_dst, uint64
     return ZCRC_OK;
   }
   // streams below kInflateSplitMinSrc: one chunk (the same kernels, no split)
-  const uint64_t chunk = src_len < kInflateSplitMinSrc ? src_len : inflate_split_chunk(src_len, chunk_bytes, dc->num_cus);
-  const size_t need = inflate_split_scratch_bytes(src_len, cap, chunk);
+  InflateSplitShape shape = inflate_split_shape(src_len, chunk_bytes, dc->num_cus);
+  if (src_len < kInflateSplitMinSrc) shape.chunk = src_len;
+  const size_t need = inflate_split_scratch_bytes(src_len, cap, shape.chunk);
   void *scratch = nullptr;
   size_t have = 0;
   std::unique_lock<std::mutex> lk;
   rc = stream_scratch(st, kScratchInflateSplit, need, &scratch, &have, &lk);
   if (rc) return rc;
   ZCRC_HIP_TRY(launch_inflate_split(static_cast<const uint8_t *>(d_src), src_len, static_cast<uint8_t *>(d_dst), cap,
-                                    d_out_len, d_status, chunk, scratch, dc->num_cus, st));
+                                    d_out_len, d_status, shape, scratch, dc->num_cus, st));
   return ZCRC_OK;
 }
 
