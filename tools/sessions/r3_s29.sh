@@ -9,3 +9,6 @@ timeout -k 10 400 python3 -u -m pytest tests/test_gpu_inflate_split.py -x -v --t
 for k in text spectrum; do
   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/kt_$k -o run -- python3 tools/bench_inflate_one.py --kinds $k --sizes 1,16,64 --reps 3 --no-serial > $O/bench_$k.jsonl 2> $O/bench_$k.err
 done
+for r in 16 32; do
+  ZCRC_SPLIT_RING=$r timeout -k 10 300 python3 tools/bench_inflate_one.py --sizes 1,4,16,64 --reps 5 --no-serial > $O/bench_ring$r.jsonl 2> $O/bench_ring$r.err
+done
