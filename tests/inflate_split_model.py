@@ -357,3 +357,217 @@ def inflate_split(data: bytes, cap: int, chunk_bytes: int, region=None):
             v = el[t]
             dst[base + t] = v if v < MARKER else dst[base - WINDOW + (v - MARKER)]
     return OK, bytes(dst), stats
+
+
+# ------------------------------------------------------------------ parts
+# Round 3, second level: a chunk whose candidate starts a long block is cut
+# into `parts` items.  Item (k, j >= 1) starts at b_j, a token boundary found
+# by a probe: decode `probe_tokens` tokens of chunk k's first block (tables
+# from the header at c_k) from the guess g_j = c_k + j |R_k| / parts and take
+# the position after them -- Huffman codes resynchronise, usually within a
+# few dozen tokens, so b_j is a true token boundary with high probability.
+# It is only trusted once an earlier item lands on it exactly: while inside
+# chunk k's first block an item checks every token boundary against the
+# later b_m of its chunk (landing -> link to item (k, m)); one it steps over
+# is skipped (that item's work is wasted).  Past that block only candidates
+# are targets, at block starts, as above.
+
+
+def probe(data: bytes, c: int, guess: int, ntok: int):
+    """Position after ntok tokens decoded from `guess` with the tables of the
+    block whose header is at c; None when the decode meets an end of block
+    or an invalid code first (the guess is not inside that block's codes)."""
+    br = Bits(data, c)
+    br.get(3)
+    st, ll, dd = read_dynamic(br)
+    if st != OK or guess < br.pos:
+        return None
+    br.pos = guess
+    for _ in range(ntok):
+        sym = decode_sym(br, ll)
+        if sym < 0 or sym == 256 or sym >= 286 or br.over:
+            return None
+        if sym > 256:
+            k = sym - 257
+            br.get(LEN_EXTRA[k])
+            ds = decode_sym(br, dd)
+            if ds < 0 or ds >= 30:
+                return None
+            br.get(DIST_EXTRA[ds])
+        if br.over:
+            return None
+    return br.pos
+
+
+def part_decode(data: bytes, start: int, hdr, targets, cand, me_chunk: int, spec: bool):
+    """Decode item from `start`: a block header when hdr is None (item j =
+    0), else a token boundary inside the block whose header is at hdr.
+    targets: [(b_m, m)] of the later items of this chunk, checked at every
+    token boundary while in that first block; candidates of later chunks are
+    checked at block starts.  Returns (ChunkResult, link), link = ("part", m)
+    or ("chunk", k') or None."""
+    br = Bits(data, start)
+    res = ChunkResult(start=start)
+    out = res.out
+    ti, j = 0, me_chunk + 1
+    in_first = True
+    if hdr is not None:
+        hb = Bits(data, hdr)
+        bfinal = hb.get(1)
+        hb.get(2)
+        _, ll, dd = read_dynamic(hb)
+        st, landed, ti = codes_targets(br, ll, dd, out, res, spec, targets, ti)
+        in_first = False
+        if st != OK or landed is not None or bfinal:
+            res.status = st
+            res.final = st == OK and landed is None and bool(bfinal)
+            res.end_bit = br.pos
+            return res, (("part", landed) if landed is not None else None)
+    link = None
+    while True:
+        pos = br.pos
+        while j < len(cand) and (cand[j] is None or cand[j] < pos):
+            j += 1
+        if j < len(cand) and cand[j] == pos:
+            link = ("chunk", j)
+            break
+        last = br.get(1)
+        typ = br.get(2)
+        if br.over:
+            res.status = ERR_INPUT
+            break
+        landed = None
+        if typ == 0:
+            br.pos = (br.pos + 7) & ~7
+            ln, nln = br.get(16), br.get(16)
+            if ln != (~nln & 0xFFFF):
+                res.status = ERR_STORED_LEN
+                break
+            b = br.pos // 8
+            if b + ln > len(data):
+                res.status = ERR_INPUT
+                break
+            out.extend(data[b:b + ln])
+            br.pos += 8 * ln
+        elif typ == 3:
+            res.status = ERR_BLOCK_TYPE
+            break
+        else:
+            if typ == 1:
+                ll, dd = fixed_codes()
+            else:
+                st, ll, dd = read_dynamic(br)
+                if st != OK:
+                    res.status = st
+                    break
+            st, landed, ti = codes_targets(br, ll, dd, out, res, spec, targets if in_first else [], ti)
+            if st != OK:
+                res.status = st
+                break
+        in_first = False
+        if landed is not None:
+            link = ("part", landed)
+            break
+        if br.over:
+            res.status = ERR_INPUT
+            break
+        if last:
+            res.final = True
+            break
+    res.end_bit = br.pos
+    return res, link
+
+
+def codes_targets(br: Bits, ll, dd, out: list, res: ChunkResult, spec: bool, targets, ti: int):
+    """codes() with per-token landing checks: (status, landed item index or
+    None, next target index)."""
+    while True:
+        while ti < len(targets) and targets[ti][0] < br.pos:
+            ti += 1
+        if ti < len(targets) and targets[ti][0] == br.pos:
+            return OK, targets[ti][1], ti
+        sym = decode_sym(br, ll)
+        if sym < 0 or br.over:
+            return (ERR_INPUT if br.over else ERR_SYMBOL), None, ti
+        if sym < 256:
+            out.append(sym)
+            continue
+        if sym == 256:
+            return OK, None, ti
+        k = sym - 257
+        if k >= 29:
+            return ERR_SYMBOL, None, ti
+        length = LEN_BASE[k] + br.get(LEN_EXTRA[k])
+        ds = decode_sym(br, dd)
+        if ds < 0 or ds >= 30:
+            return (ERR_INPUT if br.over else ERR_SYMBOL), None, ti
+        dist = DIST_BASE[ds] + br.get(DIST_EXTRA[ds])
+        if br.over:
+            return ERR_INPUT, None, ti
+        p = len(out)
+        if dist > p:
+            if not spec or dist > p + WINDOW:
+                return ERR_DIST, None, ti
+            res.reach = max(res.reach, dist - p)
+        for t in range(length):
+            s = p - dist + t
+            out.append(out[s] if s >= 0 else MARKER + WINDOW + s)
+
+
+def inflate_split_parts(data: bytes, cap: int, chunk_bytes: int, parts: int = 8, probe_tokens: int = 64):
+    """The scheme with `parts` items per chunk.  Returns (status, bytes,
+    stats) like inflate_split (status None: the serial decoder runs)."""
+    cand = find_candidates(data, chunk_bytes)
+    nbits = 8 * len(data)
+    starts = {}  # (k, j) -> (start, hdr)
+    tg = {}      # k -> [(b_m, m)]
+    for k, c in enumerate(cand):
+        if c is None:
+            continue
+        nxt = next((x for x in cand[k + 1:] if x is not None), nbits)
+        starts[(k, 0)] = (c, None)
+        bs = []
+        if k > 0 or c == 0:
+            last = c
+            for m in range(1, parts):
+                b = probe(data, c, c + m * (nxt - c) // parts, probe_tokens)
+                if b is not None and last < b < nxt:
+                    bs.append((b, m))
+                    starts[(k, m)] = (b, c)
+                    last = b
+        tg[k] = bs
+    results = {}
+    for (k, m), (st, hdr) in starts.items():
+        targets = [t for t in tg[k] if t[1] > m]
+        results[(k, m)] = part_decode(data, st, hdr, targets, cand, k, spec=(k, m) != (0, 0))
+    chain, item = [], (0, 0)
+    stats = {"chunks": len(cand), "items": len(starts), "fallback": None}
+    while True:
+        r, link = results[item]
+        chain.append(item)
+        if r.status != OK:
+            stats["fallback"] = f"item {item} status {r.status}"
+            return None, None, stats
+        if r.final:
+            break
+        if link is None:
+            stats["fallback"] = f"item {item} neither final nor linked"
+            return None, None, stats
+        item = (item[0], link[1]) if link[0] == "part" else (link[1], 0)
+    stats["chain"] = len(chain)
+    if (results[chain[-1]][0].end_bit + 7) // 8 > len(data):
+        stats["fallback"] = "input"
+        return None, None, stats
+    out = bytearray()
+    for it in chain:
+        r = results[it][0]
+        if r.reach > len(out):
+            stats["fallback"] = "distance before the stream start"
+            return None, None, stats
+        base = len(out)
+        for v in r.out:
+            out.append(v if v < MARKER else out[base - WINDOW + (v - MARKER)])
+    if len(out) > cap:
+        stats["fallback"] = "output"
+        return None, None, stats
+    return OK, bytes(out), stats

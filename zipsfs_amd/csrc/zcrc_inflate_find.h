@@ -156,6 +156,9 @@ __host__ __device__ inline bool full_ok(const uint32_t *w, uint32_t q, uint32_t 
       if (in_ll) mll = val > mll ? val : mll;
       if (rep > in_ll) md = val > md ? val : md;
       if (idx <= 256 && 256 < idx + rep) eob = true;
+      // over-subscribed already: reject now (garbage positions get here
+      // after a few dozen lengths instead of decoding all HLIT + HDIST)
+      if (kll > 32768u || kd > 32768u) return false;
     }
     idx += rep;
   }

@@ -363,14 +363,20 @@ __global__ __launch_bounds__(256) void inflate_body_kernel(ResolveArgs a) {
 // add pointer-jumping rounds.  The 32 Ki-history decoder (two per CU, no
 // reads of old output back from HBM) while its residents suffice, else the
 // 16 Ki ring (four per CU).  ZCRC_SPLIT_RING=16|32 forces one (measurement).
-InflateSplitShape inflate_split_shape(uint64_t src_len, uint64_t want, int num_cus) {
+InflateSplitShape inflate_split_shape(uint64_t src_len, uint64_t cap, uint64_t want, int num_cus) {
   static const int force = [] {
     const char *e = getenv("ZCRC_SPLIT_RING");
     return e ? atoi(e) : 0;
   }();
   const uint64_t cus = (uint64_t)(num_cus > 0 ? num_cus : 1);
   InflateSplitShape sh;
-  sh.wide = force ? force == 32 : (src_len + kInflateSplitChunk - 1) / kInflateSplitChunk <= kSpecPerCuWide * cus;
+  // text-like streams (ratio >= 2.5) reach back far more often: the whole
+  // history in LDS pays even at half the residents (64 MiB of text: 7.7
+  // against 9.4 ms; spectrum-like at 1.25: 13.2 against 10.2 ms,
+  // profiles/r03/s29/bench_ring*.jsonl)
+  sh.wide = force ? force == 32
+                  : ((src_len + kInflateSplitChunk - 1) / kInflateSplitChunk <= kSpecPerCuWide * cus ||
+                     cap >= src_len / 2 * 5);
   uint64_t c = want;
   if (!c) {
     const uint64_t resident = (sh.wide ? kSpecPerCuWide : kSpecPerCu) * cus;

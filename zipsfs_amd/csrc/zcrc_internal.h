@@ -165,7 +165,7 @@ struct InflateSplitShape {
   uint64_t chunk;  // compressed bytes per chunk
   bool wide;       // the 32 Ki-element-history decoder
 };
-InflateSplitShape inflate_split_shape(uint64_t src_len, uint64_t want, int num_cus);
+InflateSplitShape inflate_split_shape(uint64_t src_len, uint64_t cap, uint64_t want, int num_cus);
 constexpr uint32_t kSpecPerCu = 4;      // sp16::inflate_spec_kernel workgroups per CU (34.5 KB of LDS each)
 constexpr uint32_t kSpecPerCuWide = 2;  // sp32:: (67 KB each)
 uint64_t inflate_split_scratch_bytes(uint64_t src_len, uint64_t cap, uint64_t chunk);
