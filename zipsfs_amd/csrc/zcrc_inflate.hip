@@ -86,6 +86,7 @@ namespace sp16 {
 hipError_t launch_inflate_spec(const SpecArgs &args, bool wide, hipStream_t stream) {
   return wide ? sp32::launch_spec(args, stream) : sp16::launch_spec(args, stream);
 }
+hipError_t launch_inflate_probe(const SpecArgs &args, hipStream_t stream) { return sp16::launch_probe(args, stream); }
 
 // Longest-first dispatch.  Workgroups start in index order, so when a batch
 // has more streams than can be resident, a slow stream that happens to sit

@@ -70,6 +70,7 @@ __device__ __forceinline__ uint32_t e_extra(uint32_t e) { return (e >> 7) & 15u;
 __device__ __forceinline__ uint32_t e_val(uint32_t e) { return e >> 11; }
 
 __device__ __forceinline__ uint32_t uni(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); }
+__device__ __forceinline__ uint64_t uni64(uint64_t v) { return ((uint64_t)uni((uint32_t)(v >> 32)) << 32) | uni((uint32_t)v); }
 // The lane id through a volatile move: values derived from it (lane + 64 r,
 // their bit reversals) are then recomputed where they are used instead of
 // being hoisted to the kernel entry and kept live across the symbol loop
@@ -127,11 +128,17 @@ struct CodeMeta {
 // literal instead of ~30).
 constexpr uint32_t kDummy = kWin;
 struct Lds {
-  elem_t ring[kWin + 256];
+  elem_t ring[kWin + 256];  // first: the asm takes its LDS address as a constant
   uint16_t llsym[288], ddsym[32], clsym[20];
   CodeMeta llm, ddm;
   uint8_t lens[320];  // litlen lengths [0, nlen), distance lengths [nlen, nlen + ndist)
   uint8_t cllens[20];
+#if ZI_SPEC
+  // landing targets of a part (zcrc_inflate_split.hip): bit positions of the
+  // later parts of its chunk, ascending, and their item indices
+  uint64_t tpos[kMaxParts];
+  uint32_t titem[kMaxParts];
+#endif
 };
 
 // Build the canonical code for lens[0..n) (RFC 1951 3.2.2): the VGPR LUT
@@ -353,6 +360,9 @@ struct Out {
 #if ZI_SPEC
   uint32_t reach;  // furthest back-reference before the chunk's first element
   bool spec;       // the history is unknown (every chunk but the first)
+  uint64_t tpos;   // the next landing target (bit position), kSplitNone: none
+  uint32_t ti, tn; // its index in Lds::tpos, and the count
+  uint32_t landed; // the item landed on (codes() returned kSpecLanded)
 #endif
   __device__ void set_room() {
     const uint64_t c = cap - pos;
@@ -501,7 +511,8 @@ __device__ __noinline__ void copy_spec(Lds &s, const Out &o, uint32_t p0, uint32
 // v_readlane results.
 __device__ __forceinline__ uint32_t literal_run(Reader &r, uint32_t &p, uint32_t &room, const LLTab &ll,
                                                 const DTab &dd, uint32_t vsel, uint32_t vdum, uint32_t vdm,
-                                                uint32_t vlane, uint32_t ringl, uint32_t &mlen, uint32_t &mdist) {
+                                                uint32_t vlane, uint32_t ringl, uint32_t &mlen, uint32_t &mdist,
+                                                uint32_t rcap = 0xFFFFFFFFu) {
   uint32_t why, t0, t1, t2, t3, t4, t5;
   uint64_t bb = r.bb;
   uint64_t qr = r.q;
@@ -511,6 +522,7 @@ __device__ __forceinline__ uint32_t literal_run(Reader &r, uint32_t &p, uint32_t
   const uint32_t kend = P + 4u <= r.end ? (r.end - P) >> 2 : 0u;
   const uint32_t kblk = ((r.kA + 1u) * 1024u - P + 3u) >> 2;
   uint32_t rb = kend < kblk ? kend : kblk;
+  rb = uni(rb < rcap ? rb : rcap);  // ZI_SPEC landing targets: never refill past the next one
   asm volatile(
       "L_top_%=:\n\t"
       "s_cmp_le_u32 %[nb], 32\n\t"
@@ -682,6 +694,37 @@ __device__ int32_t codes(Lds &s, Reader &r, Out &o, const LLTab &ll, const DTab 
       st = ZCRC_INFLATE_ERR_INPUT;
       break;
     }
+    uint32_t rcap = 0xFFFFFFFFu;
+#if ZI_SPEC
+    // landing: at a token boundary equal to the next target the part stops
+    // (the later part's decode starts there); a target already passed was
+    // not a token boundary (its probe had not synchronised) and is skipped.
+    // Within 96 bits of a target the tokens are taken one at a time by the
+    // compiled path; before that the asm may refill only up to the target's
+    // byte, so it cannot run past it.  (`if`s, not loops: see settle().)
+    bool near = false;
+    if (o.tpos != kSplitNone) {
+      const uint64_t bit = ((uint64_t)(r.P - r.lead) << 3) - r.nb;
+      if (o.tpos < bit) {
+        o.ti++;
+        o.tpos = o.ti < o.tn ? ((uint64_t)uni((uint32_t)(s.tpos[o.ti] >> 32)) << 32) | uni((uint32_t)s.tpos[o.ti])
+                             : kSplitNone;
+      }
+      if (o.tpos == bit) {
+        o.landed = uni(s.titem[o.ti]);
+        st = kSpecLanded;
+        break;
+      }
+      if (o.tpos != kSplitNone && o.tpos > bit) {
+        near = o.tpos - bit < 96u;
+        const uint64_t tb = (uint64_t)r.lead + (o.tpos >> 3);  // the target's byte, aligned-base relative
+        rcap = tb > r.P ? (uint32_t)((tb - r.P) >> 2) : 0u;
+      } else {
+        rcap = 0;  // passed targets still ahead in the list: advance first
+      }
+    }
+    if (!near)
+#endif
 #ifndef ZI_NO_ASM
     {
       // (readfirstlane: the compiler cannot always prove this state
@@ -693,7 +736,7 @@ __device__ int32_t codes(Lds &s, Reader &r, Out &o, const LLTab &ll, const DTab 
       r.P = uni(r.P);
       r.q = uni(r.q);
       uint32_t room = uni(o.room), ml = 0, md = 0;
-      const uint32_t why = literal_run(r, p, room, ll, dd, vsel, vdum, vdm, lane, ring_lds, ml, md);
+      const uint32_t why = literal_run(r, p, room, ll, dd, vsel, vdum, vdm, lane, ring_lds, ml, md, uni(rcap));
       o.room = room;
       o.pos += p - p0;
       if (!why) continue;
@@ -971,85 +1014,236 @@ __global__ __launch_bounds__(64, ZI_WPE) void inflate_kernel(InflateArgs a) {
   }
 }
 #else
-// Speculative decode of chunk k of one stream (zcrc_inflate_split.hip,
-// tests/inflate_split_model.py spec_decode): from candidate bit a.cand[k]
-// (chunk 0: bit 0, history known) to the first block start equal to a later
-// candidate (link), the end of the final block, or an error.  Elements go
-// to the chunk's region, which extends over the following chunks that have
-// no candidate (no decode of theirs writes there).
-__global__ __launch_bounds__(64, ZI_WPE) void inflate_spec_kernel(SpecArgs a) {
-  __shared__ __attribute__((aligned(16))) Lds s;
-  const uint64_t k = blockIdx.x;
-  const uint64_t c = a.cand[k];
-  SpecRec *rec = a.rec + k;
-  if (c == kSplitNone) {
-    if (threadIdx.x == 0) *rec = SpecRec{0, 0, kSpecSkipped, -1, 0, 0};
-    return;
+// The next chunk after k with a candidate (kn = nchunks: none) and its
+// candidate (cn = 8 src_len then).
+__device__ __forceinline__ void next_candidate(const SpecArgs &a, uint64_t k, uint64_t &kn, uint64_t &cn) {
+  kn = k + 1;
+  while (kn < a.nchunks && a.cand[kn] == kSplitNone) kn++;
+  cn = kn < a.nchunks ? a.cand[kn] : 8 * a.src_len;
+}
+
+// Chunk k's usable parts: the probed starts that lie strictly after the
+// previous usable one (or the candidate c) and before the next candidate,
+// ascending -- every item of the chunk filters the same way.
+__device__ __forceinline__ uint32_t usable_parts(const SpecArgs &a, uint64_t k, uint64_t c, uint64_t cn,
+                                                 uint64_t *pos, uint32_t *idx) {
+  uint32_t n = 0;
+  uint64_t last = c;
+  for (uint32_t m = 1; m < a.parts; m++) {
+    const uint64_t b = a.part[k * a.parts + m];
+    if (b != kSplitNone && b > last && b < cn) {
+      pos[n] = b;
+      idx[n] = m;
+      n++;
+      last = b;
+    }
   }
-  uint64_t nxt = k + 1;
-  while (nxt < a.nchunks && a.cand[nxt] == kSplitNone) nxt++;
-  Out o;
-  o.dst = a.region + k * a.region_elems;
-  o.cap = (nxt - k) * a.region_elems;
-  o.pos = 0;
-  o.fl = 0;
-  o.al16 = (reinterpret_cast<uint64_t>(o.dst) & 15u) == 0;
-  o.reach = 0;
-  o.spec = k > 0;
-  o.set_room();
-  int32_t st = ZCRC_INFLATE_OK;
-  int32_t link = -1;
-  uint32_t last = 0;
-  Reader r;
+  return n;
+}
+
+// Reader positioned at bit `bit` of the stream
+__device__ __forceinline__ bool reader_at(Reader &r, const SpecArgs &a, uint64_t bit) {
+  r.seek(r.lead + (uint32_t)(bit >> 3));
+  if (!r.ensure()) return false;
+  r.drop((uint32_t)(bit & 7u));
+  return true;
+}
+
+__device__ __forceinline__ void reader_init(Reader &r, const SpecArgs &a) {
   const uint64_t base = reinterpret_cast<uint64_t>(a.src) & ~(uint64_t)15;
   r.lead = (uint32_t)(reinterpret_cast<uint64_t>(a.src) - base);
   r.end = r.lead + (uint32_t)a.src_len;
   r.limit = r.end + 16u;
   r.rsrc = __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void *>(base), (short)0, (int)((r.end + 15u) & ~15u),
                                              0x00020000);
-  r.seek(r.lead + (uint32_t)(c >> 3));
-  if (!r.ensure()) st = ZCRC_INFLATE_ERR_INPUT;
-  else r.drop((uint32_t)(c & 7u));
+}
+
+__device__ __forceinline__ uint64_t reader_bit(const Reader &r) { return ((uint64_t)(r.P - r.lead) << 3) - r.nb; }
+
+// Probe for part j >= 1 of chunk k (tests/inflate_split_model.py probe):
+// parse the dynamic header at the chunk's candidate, decode
+// a.probe_tokens tokens from the guess c + j (cn - c) / parts without
+// output, and record the position after them -- a token boundary once the
+// code has resynchronised, which it usually has after a few dozen tokens
+// (a later part's landing check is what trusts it).  kSplitNone when the
+// guess runs into an end of block or an invalid code first.
+__global__ __launch_bounds__(64, ZI_WPE) void inflate_probe_kernel(SpecArgs a) {
+  __shared__ __attribute__((aligned(16))) Lds s;
+  const uint64_t i = blockIdx.x, k = i / a.parts;
+  const uint32_t j = (uint32_t)(i % a.parts);
+  if (j == 0) return;
+  const uint64_t c = a.cand[k];
+  uint64_t out = kSplitNone;
+  if (c != kSplitNone) {
+    uint64_t kn, cn;
+    next_candidate(a, k, kn, cn);
+    const uint64_t guess = c + (uint64_t)j * ((cn - c) / a.parts);
+    Reader r;
+    reader_init(r, a);
+    LLTab ll;
+    DTab dd;
+    bool ok = reader_at(r, a, c) && ((r.bb >> 1) & 3u) == 2u;
+    if (ok) {
+      r.drop(3);
+      ok = dynamic_tables(s, r, ll, dd) == ZCRC_INFLATE_OK && guess > reader_bit(r) && reader_at(r, a, guess);
+    }
+    for (uint32_t t = 0; ok && t < a.probe_tokens; t++) {
+      if (!r.ensure()) {
+        ok = false;
+        break;
+      }
+      const uint32_t ix = (uint32_t)r.bb & ((1u << kLLRoot) - 1u);
+      uint32_t e = lane_get(ll[ix >> 6], ix);
+      if (e_kind(e) == K_LONG) e = uni(decode_slow(r.peek(15), &s.llm, s.llsym, kLLRoot, A_LITLEN));
+      const uint32_t kind = e_kind(e);
+      if (kind == K_LIT && e_len(e)) {
+        r.drop(e_len(e));
+        continue;
+      }
+      if (kind != K_BASE || e_len(e) == 0) {
+        ok = false;  // end of block, invalid or missing code
+        break;
+      }
+      r.drop(e_len(e) + e_extra(e));
+      if (!r.ensure()) {
+        ok = false;
+        break;
+      }
+      const uint32_t jx = (uint32_t)r.bb & ((1u << kDRoot) - 1u);
+      uint32_t d = lane_get(dd[jx >> 6], jx);
+      if (e_kind(d) == K_LONG) d = uni(decode_slow(r.peek(15), &s.ddm, s.ddsym, kDRoot, A_DIST));
+      if (e_kind(d) != K_BASE || e_len(d) == 0) {
+        ok = false;
+        break;
+      }
+      r.drop(e_len(d) + e_extra(d));
+    }
+    if (ok && r.consumed() <= a.src_len) out = reader_bit(r);
+  }
+  if (threadIdx.x == 0) a.part[i] = out;
+}
+
+// Speculative decode of item i = (chunk k, part j) of one stream
+// (zcrc_inflate_split.hip; tests/inflate_split_model.py part_decode): from
+// its start (part 0: the chunk's candidate, chunk 0: bit 0, history known;
+// part j: its probed token boundary, with the tables of the block whose
+// header is at the candidate) until it lands on a later part's start (per
+// token, while in that first block), reaches a block start equal to a later
+// candidate, ends the final block, or fails.  Elements go to the item's
+// region, which extends over the following items that have no work.
+__global__ __launch_bounds__(64, ZI_WPE) void inflate_spec_kernel(SpecArgs a) {
+  __shared__ __attribute__((aligned(16))) Lds s;
+  const uint64_t i = blockIdx.x, k = i / a.parts;
+  const uint32_t j = (uint32_t)(i % a.parts);
+  const uint64_t c = a.cand[k];
+  SpecRec *rec = a.rec + i;
+  uint64_t kn = 0, cn = 0, start = c, vpos[kMaxParts];
+  uint32_t vidx[kMaxParts], np = 0, me = 0;
+  bool work = c != kSplitNone;
+  if (work) {
+    next_candidate(a, k, kn, cn);
+    np = usable_parts(a, k, c, cn, vpos, vidx);
+    if (j > 0) {
+      work = false;
+      for (uint32_t t = 0; t < np; t++)
+        if (vidx[t] == j) work = true, start = vpos[t], me = t + 1;
+    }
+  }
+  if (!work) {
+    if (threadIdx.x == 0) *rec = SpecRec{0, 0, kSpecSkipped, -1, 0, 0};
+    return;
+  }
+  // (the compiler keeps the small arrays above in VGPRs: everything taken
+  // from them is made provably uniform before it reaches the decode state,
+  // whose asm wants SGPRs)
+  start = uni64(start);
+  np = uni(np);
+  me = uni(me);
+  // landing targets: the usable parts after this one; the region runs to the
+  // next item with work
+  const uint32_t tn = np - me;
+  if (threadIdx.x < tn) {
+    s.tpos[threadIdx.x] = vpos[me + threadIdx.x];
+    s.titem[threadIdx.x] = (uint32_t)(k * a.parts + vidx[me + threadIdx.x]);
+  }
+  __syncthreads();
+  const uint64_t next_work = uni64(tn ? k * a.parts + vidx[me] : kn * a.parts);
+  Out o;
+  o.dst = a.region + i * a.region_elems;
+  o.cap = (next_work - i) * a.region_elems;
+  o.pos = 0;
+  o.fl = 0;
+  o.al16 = (reinterpret_cast<uint64_t>(o.dst) & 15u) == 0;
+  o.reach = 0;
+  o.spec = i > 0;
+  o.tpos = uni64(tn ? vpos[me] : kSplitNone);
+  o.ti = 0;
+  o.tn = tn;
+  o.landed = 0;
+  o.set_room();
+  int32_t st = ZCRC_INFLATE_OK;
+  int32_t link = -1;
+  uint32_t last = 0;
+  Reader r;
+  reader_init(r, a);
   LLTab ll;
   DTab dd;
-  uint64_t j = k + 1;  // the next candidate at or past the decode position
-  while (st == ZCRC_INFLATE_OK) {
+  // mid: the first round of the loop reads the header at c -- of the block
+  // this part starts inside -- and continues that block from `start`, so
+  // that one call site of each decode step serves both (second inlined
+  // copies of the header decode or the symbol loop did not compile: illegal
+  // VGPR to SGPR copies)
+  bool mid = j > 0;
+  if (!reader_at(r, a, c)) st = ZCRC_INFLATE_ERR_INPUT;
+  uint64_t jc = k + 1;  // the next candidate at or past the decode position
+  bool first = true;    // part targets live in the chunk's first block only
+  while (st == ZCRC_INFLATE_OK && !last) {
     if (!r.ensure()) {
       st = ZCRC_INFLATE_ERR_INPUT;
       break;
     }
-    const uint64_t bit = ((uint64_t)(r.P - r.lead) << 3) - r.nb;
-    while (j < a.nchunks) {
-      const uint64_t cj = a.cand[j];
+    const uint64_t bit = reader_bit(r);
+    while (jc < a.nchunks) {
+      const uint64_t cj = a.cand[jc];
       if (cj != kSplitNone && cj >= bit) break;
-      j++;
+      jc++;
     }
-    if (j < a.nchunks && a.cand[j] == bit) {
-      link = (int32_t)j;
+    if (jc < a.nchunks && a.cand[jc] == bit) {
+      link = (int32_t)(jc * a.parts);
       break;
     }
     last = r.peek(1);
     const uint32_t type = (uint32_t)(r.bb >> 1) & 3u;
     r.drop(3);
-    if (type == 0) {
+    if (mid && type != 2) {
+      st = ZCRC_INFLATE_ERR_CODES;  // (a part's candidate is a dynamic header: the probe read it)
+    } else if (type == 0) {
       st = stored(s, r, o);
     } else if (type == 1) {
       fixed_tables(s, ll, dd);
       st = codes(s, r, o, ll, dd);
     } else if (type == 2) {
       st = dynamic_tables(s, r, ll, dd);
+      if (mid && st == ZCRC_INFLATE_OK && !reader_at(r, a, start)) st = ZCRC_INFLATE_ERR_INPUT;
       if (st == ZCRC_INFLATE_OK) st = codes(s, r, o, ll, dd);
     } else {
       st = ZCRC_INFLATE_ERR_BLOCK_TYPE;
     }
     st = (int32_t)uni((uint32_t)st);
-    if (last) break;
+    if (first) o.tpos = kSplitNone;
+    first = false;
+    mid = false;
+    if (st == kSpecLanded) {
+      link = (int32_t)o.landed;
+      st = ZCRC_INFLATE_OK;
+      break;
+    }
   }
   if (st == ZCRC_INFLATE_OK && link < 0 && r.consumed() > a.src_len) st = ZCRC_INFLATE_ERR_INPUT;
   if (st == ZCRC_INFLATE_OK) flush_to(s, o, o.pos);
   if (threadIdx.x == 0) {
     rec->out_len = o.pos;
-    rec->end_bit = ((uint64_t)(r.P - r.lead) << 3) - r.nb;
+    rec->end_bit = reader_bit(r);
     rec->status = st;
     rec->link = link;
     rec->reach = o.reach;
@@ -1067,7 +1261,11 @@ hipError_t launch(const InflateArgs &args, hipStream_t stream) {
 }
 #else
 hipError_t launch_spec(const SpecArgs &args, hipStream_t stream) {
-  hipLaunchKernelGGL(inflate_spec_kernel, dim3((unsigned)args.nchunks), dim3(64), 0, stream, args);
+  hipLaunchKernelGGL(inflate_spec_kernel, dim3((unsigned)(args.nchunks * args.parts)), dim3(64), 0, stream, args);
+  return hipGetLastError();
+}
+hipError_t launch_probe(const SpecArgs &args, hipStream_t stream) {
+  hipLaunchKernelGGL(inflate_probe_kernel, dim3((unsigned)(args.nchunks * args.parts)), dim3(64), 0, stream, args);
   return hipGetLastError();
 }
 #endif

@@ -385,14 +385,34 @@ InflateSplitShape inflate_split_shape(uint64_t src_len, uint64_t cap, uint64_t w
   }
   const uint64_t need = (src_len + kChainLds - 1) / kChainLds;  // at most kChainLds chunks
   sh.chunk = c < need ? need : c;
+  // parts: while the chunks leave resident decoders idle, cut each chunk's
+  // first block into parts (items), up to kMaxParts; items stay <= kChainLds
+  const uint64_t nch = src_len ? (src_len + sh.chunk - 1) / sh.chunk : 1;
+  const uint64_t resident = (sh.wide ? kSpecPerCuWide : kSpecPerCu) * cus;
+  uint64_t parts = nch < resident ? resident / nch : 1;
+  static const int force_parts = [] {
+    const char *e = getenv("ZCRC_SPLIT_PARTS");
+    return e ? atoi(e) : 0;
+  }();
+  if (force_parts > 0) parts = (uint64_t)force_parts;
+  if (parts > kMaxParts) parts = kMaxParts;
+  if (parts < 1) parts = 1;
+  while (parts > 1 && nch * parts > kChainLds) parts--;
+  sh.parts = (uint32_t)parts;
   return sh;
 }
 
-uint64_t inflate_split_scratch_bytes(uint64_t src_len, uint64_t cap, uint64_t chunk) {
-  const uint64_t nch = src_len ? (src_len + chunk - 1) / chunk : 1;
-  const uint64_t relems = ((2 * cap) / nch + kInflateSplitSlack + 7) & ~7ull;
-  return 256 + nch * (8 + sizeof(SpecRec) + 4 + 8) + 8 + 64 + nch * relems * 2 + 2 * 4ull * kInflateHist * nch +
-         64 * 12;
+// item regions: 3 x the average share (a part that absorbs a neighbour whose
+// start it did not land on needs twice its own) + kInflateSplitSlack
+static uint64_t region_elems(uint64_t cap, uint64_t nitems) {
+  return ((3 * cap) / nitems + kInflateSplitSlack + 7) & ~7ull;
+}
+
+uint64_t inflate_split_scratch_bytes(uint64_t src_len, uint64_t cap, InflateSplitShape shape) {
+  const uint64_t nch = src_len ? (src_len + shape.chunk - 1) / shape.chunk : 1;
+  const uint64_t nit = nch * shape.parts;
+  return 256 + nch * 8 + nit * (8 + sizeof(SpecRec) + 4 + 8) + 8 + 64 + nit * region_elems(cap, nit) * 2 +
+         2 * 4ull * kInflateHist * nit + 64 * 14;
 }
 
 // One stream: find, speculative decode, chain, resolve, serial fall-back.
@@ -401,7 +421,8 @@ hipError_t launch_inflate_split(const uint8_t *src, uint64_t src_len, uint8_t *d
                                 int num_cus, hipStream_t stream) {
   const uint64_t chunk = shape.chunk;
   const uint64_t nch = src_len ? (src_len + chunk - 1) / chunk : 1;
-  const uint64_t relems = ((2 * cap) / nch + kInflateSplitSlack + 7) & ~7ull;
+  const uint64_t nit = nch * shape.parts;  // items: (chunk, part)
+  const uint64_t relems = region_elems(cap, nit);
   uint8_t *p = static_cast<uint8_t *>(scratch);
   auto take = [&](uint64_t bytes) {
     uint8_t *r = p;
@@ -414,26 +435,29 @@ hipError_t launch_inflate_split(const uint8_t *src, uint64_t src_len, uint8_t *d
   uint8_t **fb_dst = reinterpret_cast<uint8_t **>(take(8));
   uint64_t *fb_cap = reinterpret_cast<uint64_t *>(take(8));
   uint64_t *cand = reinterpret_cast<uint64_t *>(take(8 * nch));
-  SpecRec *rec = reinterpret_cast<SpecRec *>(take(sizeof(SpecRec) * nch));
-  uint32_t *chain = reinterpret_cast<uint32_t *>(take(4 * (nch + 1)));
-  uint64_t *off = reinterpret_cast<uint64_t *>(take(8 * nch));
-  uint16_t *region = reinterpret_cast<uint16_t *>(take(2 * nch * relems));
-  uint32_t *win[2] = {reinterpret_cast<uint32_t *>(take(4ull * kInflateHist * nch)),
-                      reinterpret_cast<uint32_t *>(take(4ull * kInflateHist * nch))};
+  uint64_t *part = reinterpret_cast<uint64_t *>(take(8 * nit));
+  SpecRec *rec = reinterpret_cast<SpecRec *>(take(sizeof(SpecRec) * nit));
+  uint32_t *chain = reinterpret_cast<uint32_t *>(take(4 * (nit + 1)));
+  uint64_t *off = reinterpret_cast<uint64_t *>(take(8 * nit));
+  uint16_t *region = reinterpret_cast<uint16_t *>(take(2 * nit * relems));
+  uint32_t *win[2] = {reinterpret_cast<uint32_t *>(take(4ull * kInflateHist * nit)),
+                      reinterpret_cast<uint32_t *>(take(4ull * kInflateHist * nit))};
 
   FindArgs fa{src, src_len, chunk, nch, cand};
   hipLaunchKernelGGL(inflate_find_kernel, dim3((unsigned)nch), dim3(kFindThreads), 0, stream, fa);
-  SpecArgs sa{src, src_len, cand, rec, region, relems, nch};
-  hipError_t e = launch_inflate_spec(sa, shape.wide, stream);
+  SpecArgs sa{src, src_len, cand, rec, region, relems, nch, part, shape.parts, kInflateProbeTokens};
+  hipError_t e = hipSuccess;
+  if (shape.parts > 1) e = launch_inflate_probe(sa, stream);
+  if (e == hipSuccess) e = launch_inflate_spec(sa, shape.wide, stream);
   if (e != hipSuccess) return e;
-  ChainArgs ca{rec, nch, cap, chain, off, run_serial, out_len, status, fb_src, fb_src_len, fb_dst, fb_cap,
+  ChainArgs ca{rec, nit, cap, chain, off, run_serial, out_len, status, fb_src, fb_src_len, fb_dst, fb_cap,
                src, src_len, dst};
   hipLaunchKernelGGL(inflate_chain_kernel, dim3(1), dim3(1024), 0, stream, ca);
   // windows: build, ceil(log2 nch) pointer-jumping rounds, store the tails
   uint32_t rounds = 0;
-  while ((1ull << rounds) < nch) rounds++;
-  WinArgs wa{region, relems, rec, chain, off, nch, nullptr, win[0], dst};
-  const dim3 wgrid(kInflateHist / 1024, (unsigned)nch);
+  while ((1ull << rounds) < nit) rounds++;
+  WinArgs wa{region, relems, rec, chain, off, nit, nullptr, win[0], dst};
+  const dim3 wgrid(kInflateHist / 1024, (unsigned)nit);
   hipLaunchKernelGGL(inflate_win_build_kernel, wgrid, dim3(1024), 0, stream, wa);
   for (uint32_t r = 0; r < rounds; r++) {
     wa.win_in = win[r & 1];
@@ -441,8 +465,8 @@ hipError_t launch_inflate_split(const uint8_t *src, uint64_t src_len, uint8_t *d
     hipLaunchKernelGGL(inflate_win_jump_kernel, wgrid, dim3(1024), 0, stream, wa);
   }
   hipLaunchKernelGGL(inflate_win_store_kernel, wgrid, dim3(1024), 0, stream, wa);
-  ResolveArgs ra{region, relems, rec, chain, off, nch, dst};
-  const unsigned gy = (unsigned)(nch < 4096 ? nch : 4096);
+  ResolveArgs ra{region, relems, rec, chain, off, nit, dst};
+  const unsigned gy = (unsigned)(nit < 4096 ? nit : 4096);
   const unsigned gx = (unsigned)((4u * (unsigned)num_cus + gy - 1) / gy) + 1u;
   hipLaunchKernelGGL(inflate_body_kernel, dim3(gx, gy), dim3(256), 0, stream, ra);
   e = hipGetLastError();

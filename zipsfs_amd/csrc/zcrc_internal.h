@@ -131,7 +131,9 @@ struct InflateArgs {
 constexpr uint32_t kInflateMarker = 0x8000u;
 constexpr uint32_t kInflateHist = 32768u;
 constexpr uint64_t kSplitNone = ~0ull;  // no candidate block start in the chunk
-constexpr int32_t kSpecSkipped = -1;    // SpecRec::status of a chunk without a candidate
+constexpr int32_t kSpecSkipped = -1;    // SpecRec::status of an item without work
+constexpr int32_t kSpecLanded = 100;    // codes(): stopped on a later part's start (internal)
+constexpr uint32_t kMaxParts = 8;       // items per chunk (a chunk's first block cut into parts)
 struct SpecRec {
   uint64_t out_len;  // elements produced
   uint64_t end_bit;  // bit position where the decode stopped
@@ -144,10 +146,13 @@ struct SpecArgs {
   const uint8_t *src;
   uint64_t src_len;
   const uint64_t *cand;  // per chunk: candidate bit position, or kSplitNone
-  SpecRec *rec;
-  uint16_t *region;      // chunk k's elements start at region + k * region_elems
+  SpecRec *rec;          // per item (chunk k, part j) = item k * parts + j
+  uint16_t *region;      // item i's elements start at region + i * region_elems
   uint64_t region_elems;
   uint64_t nchunks;
+  uint64_t *part;        // per item: the probed start of part j >= 1 (kSplitNone: none)
+  uint32_t parts;        // items per chunk (<= kMaxParts)
+  uint32_t probe_tokens;
 };
 constexpr uint64_t kInflateMaxSrc = 0xF0000000ull;  // 32-bit buffer range and block arithmetic
 // order_scratch: >= 4 * n bytes of device memory for the dispatch order
@@ -156,6 +161,7 @@ hipError_t launch_inflate(const InflateArgs &args, int num_cus, hipStream_t stre
 // wide: the 32 Ki-element-history decoder (kSpecPerCuWide per CU), else the
 // 16 Ki-element ring (kSpecPerCu per CU)
 hipError_t launch_inflate_spec(const SpecArgs &args, bool wide, hipStream_t stream);
+hipError_t launch_inflate_probe(const SpecArgs &args, hipStream_t stream);
 constexpr uint64_t kInflateSplitChunk = 8192;   // compressed bytes per chunk (at least; at most 16,384 chunks)
 constexpr uint64_t kInflateSplitSlack = 16384;  // elements added to each chunk's region
 constexpr uint64_t kInflateSplitMinSrc = 65536; // smaller streams decode serially
@@ -164,11 +170,13 @@ constexpr uint64_t kInflateSplitMinSrc = 65536; // smaller streams decode serial
 struct InflateSplitShape {
   uint64_t chunk;  // compressed bytes per chunk
   bool wide;       // the 32 Ki-element-history decoder
+  uint32_t parts;  // items per chunk
 };
 InflateSplitShape inflate_split_shape(uint64_t src_len, uint64_t cap, uint64_t want, int num_cus);
 constexpr uint32_t kSpecPerCu = 4;      // sp16::inflate_spec_kernel workgroups per CU (34.5 KB of LDS each)
 constexpr uint32_t kSpecPerCuWide = 2;  // sp32:: (67 KB each)
-uint64_t inflate_split_scratch_bytes(uint64_t src_len, uint64_t cap, uint64_t chunk);
+uint64_t inflate_split_scratch_bytes(uint64_t src_len, uint64_t cap, InflateSplitShape shape);
+constexpr uint32_t kInflateProbeTokens = 64;  // tokens a part's probe decodes past its guess
 hipError_t launch_inflate_split(const uint8_t *src, uint64_t src_len, uint8_t *dst, uint64_t cap,
                                 uint64_t *out_len, int32_t *status, InflateSplitShape shape, void *scratch,
                                 int num_cus, hipStream_t stream);

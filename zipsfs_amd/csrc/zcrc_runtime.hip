@@ -1554,8 +1554,8 @@ int zcrc_inflate_device(const void *d_src, uint64_t src_len, void *d_dst, uint64
   }
   // streams below kInflateSplitMinSrc: one chunk (the same kernels, no split)
   InflateSplitShape shape = inflate_split_shape(src_len, cap, chunk_bytes, dc->num_cus);
-  if (src_len < kInflateSplitMinSrc) shape.chunk = src_len;
-  const size_t need = inflate_split_scratch_bytes(src_len, cap, shape.chunk);
+  if (src_len < kInflateSplitMinSrc) shape.chunk = src_len, shape.parts = 1;
+  const size_t need = inflate_split_scratch_bytes(src_len, cap, shape);
   void *scratch = nullptr;
   size_t have = 0;
   std::unique_lock<std::mutex> lk;
