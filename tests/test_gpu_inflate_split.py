@@ -149,3 +149,19 @@ def test_host_batch_routes_large_entries_through_split():
     res = z.inflate_batch(comps, [len(d) for d in datas])
     for (st, out, crc), d in zip(res, datas):
         assert st == 0 and out == d and crc == zlib.crc32(d)
+
+
+@pytest.mark.parametrize("parts,probe", [(1, 0), (8, 0), (8, 2), (3, 5)])
+def test_split_inflate_parts_and_unsynchronised_probes(monkeypatch, parts, probe):
+    """Parts per chunk forced (ZCRC_SPLIT_PARTS) and probes of a few tokens
+    (ZCRC_SPLIT_PROBE): part starts that are not token boundaries are
+    stepped over by the part before -- the bytes stay zlib's."""
+    monkeypatch.setenv("ZCRC_SPLIT_PARTS", str(parts))
+    if probe:
+        monkeypatch.setenv("ZCRC_SPLIT_PROBE", str(probe))
+    for kind, size in (("text", 900000), ("spectrum", 700000), ("runs", 500000)):
+        data = S.PAYLOADS[kind](size, 90 + parts + probe)
+        comp = S.deflate(data, 6)
+        for chunk in (0, 4096):
+            st, out = _run(comp, len(data), chunk)
+            assert st == 0 and out == data, (kind, chunk)

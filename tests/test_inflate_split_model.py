@@ -107,3 +107,25 @@ def test_model_truncated_stream_falls_back():
     comp = S.deflate(data, 6)[:-3]
     st, _, stats = M.inflate_split(comp, len(data), 1024)
     assert st is None and stats["fallback"]
+
+
+@pytest.mark.parametrize("kind,level,strategy", [("text", 6, "default"), ("spectrum", 6, "default"),
+                                                 ("runs", 6, "rle"), ("text", 6, "fixed"), ("far", 9, "default")])
+def test_model_parts_equal_zlib(kind, level, strategy):
+    """Second level: each chunk's first block cut into 8 parts that start at
+    probed token boundaries; parts land on each other per token."""
+    data = S.PAYLOADS[kind](160 << 10, 13)
+    comp = S.deflate(data, level, strategy)
+    st, out, stats = M.inflate_split_parts(comp, len(data), 4096, parts=8, probe_tokens=64)
+    assert stats["fallback"] is None, stats
+    assert st == M.OK and out == _zlib(comp)
+
+
+def test_model_parts_survive_unsynchronised_probes():
+    """With 2-token probes most part starts are not token boundaries: the
+    earlier part steps over them and decodes on -- slower, never wrong."""
+    data = S.text_payload(120 << 10, 21)
+    comp = S.deflate(data, 6)
+    st, out, stats = M.inflate_split_parts(comp, len(data), 4096, parts=8, probe_tokens=2)
+    assert st == M.OK and out == data, stats
+    assert stats["chain"] < stats["items"]

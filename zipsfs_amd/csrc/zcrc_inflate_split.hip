@@ -390,10 +390,8 @@ InflateSplitShape inflate_split_shape(uint64_t src_len, uint64_t cap, uint64_t w
   const uint64_t nch = src_len ? (src_len + sh.chunk - 1) / sh.chunk : 1;
   const uint64_t resident = (sh.wide ? kSpecPerCuWide : kSpecPerCu) * cus;
   uint64_t parts = nch < resident ? resident / nch : 1;
-  static const int force_parts = [] {
-    const char *e = getenv("ZCRC_SPLIT_PARTS");
-    return e ? atoi(e) : 0;
-  }();
+  const char *fp = getenv("ZCRC_SPLIT_PARTS");  // (read per call: tests set it)
+  const int force_parts = fp ? atoi(fp) : 0;
   if (force_parts > 0) parts = (uint64_t)force_parts;
   if (parts > kMaxParts) parts = kMaxParts;
   if (parts < 1) parts = 1;
@@ -445,7 +443,9 @@ hipError_t launch_inflate_split(const uint8_t *src, uint64_t src_len, uint8_t *d
 
   FindArgs fa{src, src_len, chunk, nch, cand};
   hipLaunchKernelGGL(inflate_find_kernel, dim3((unsigned)nch), dim3(kFindThreads), 0, stream, fa);
-  SpecArgs sa{src, src_len, cand, rec, region, relems, nch, part, shape.parts, kInflateProbeTokens};
+  const char *pt = getenv("ZCRC_SPLIT_PROBE");  // test knob: tokens per probe (a few: unsynchronised part starts)
+  SpecArgs sa{src, src_len, cand, rec, region, relems, nch, part, shape.parts,
+              pt && atoi(pt) > 0 ? (uint32_t)atoi(pt) : kInflateProbeTokens};
   hipError_t e = hipSuccess;
   if (shape.parts > 1) e = launch_inflate_probe(sa, stream);
   if (e == hipSuccess) e = launch_inflate_spec(sa, shape.wide, stream);
