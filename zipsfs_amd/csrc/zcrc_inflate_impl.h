@@ -1150,7 +1150,7 @@ __global__ __launch_bounds__(64, ZI_WPE) void inflate_spec_kernel(SpecArgs a) {
     }
   }
   if (!work) {
-    if (threadIdx.x == 0) *rec = SpecRec{0, 0, kSpecSkipped, -1, 0, 0};
+    if (threadIdx.x == 0) *rec = SpecRec{0, 0, 0, kSpecSkipped, -1, 0, 0};
     return;
   }
   // (the compiler keeps the small arrays above in VGPRs: everything taken
@@ -1167,10 +1167,19 @@ __global__ __launch_bounds__(64, ZI_WPE) void inflate_spec_kernel(SpecArgs a) {
     s.titem[threadIdx.x] = (uint32_t)(k * a.parts + vidx[me + threadIdx.x]);
   }
   __syncthreads();
-  const uint64_t next_work = uni64(tn ? k * a.parts + vidx[me] : kn * a.parts);
+  // Region: the chunk owns the elements of its items and of the items of the
+  // candidate-less chunks after it, [k parts, kn parts) x region_elems, split
+  // evenly among its usable parts -- a part that steps over a later part's
+  // start (unsynchronised probe) and absorbs its range has room for it.
+  // (Per-item regions overflowed there: most items have no work, so one
+  // item's share was well below a part's output, profiles/r03/s30.)
+  const uint64_t span = (kn - k) * a.parts * a.region_elems, nused = np + 1;
+  const uint64_t r0 = uni64(k * a.parts * a.region_elems + ((me * span / nused) & ~7ull));
+  const uint64_t r1 = uni64(me + 1 == nused ? k * a.parts * a.region_elems + span
+                                            : k * a.parts * a.region_elems + (((me + 1) * span / nused) & ~7ull));
   Out o;
-  o.dst = a.region + i * a.region_elems;
-  o.cap = (next_work - i) * a.region_elems;
+  o.dst = a.region + r0;
+  o.cap = r1 - r0;
   o.pos = 0;
   o.fl = 0;
   o.al16 = (reinterpret_cast<uint64_t>(o.dst) & 15u) == 0;
@@ -1242,6 +1251,7 @@ __global__ __launch_bounds__(64, ZI_WPE) void inflate_spec_kernel(SpecArgs a) {
   if (st == ZCRC_INFLATE_OK && link < 0 && r.consumed() > a.src_len) st = ZCRC_INFLATE_ERR_INPUT;
   if (st == ZCRC_INFLATE_OK) flush_to(s, o, o.pos);
   if (threadIdx.x == 0) {
+    rec->region = r0;
     rec->out_len = o.pos;
     rec->end_bit = reader_bit(r);
     rec->status = st;

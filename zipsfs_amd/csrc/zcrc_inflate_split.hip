@@ -30,7 +30,10 @@
 // and the GPU tests compare the bytes with zlib.decompress.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdio.h>
 #include <stdlib.h>
+
+#include <vector>
 
 #include "../../include/zcrc.h"
 #include "zcrc_inflate_find.h"
@@ -307,7 +310,7 @@ __global__ __launch_bounds__(1024) void inflate_win_build_kernel(WinArgs a) {
   const uint32_t i = blockIdx.x * 1024u + threadIdx.x;
   uint32_t v;
   if (i >= kInflateHist - n) {
-    const uint32_t e = a.region[k * a.region_elems + (len - kInflateHist + i)];
+    const uint32_t e = a.region[a.rec[k].region + (len - kInflateHist + i)];
     v = e < kInflateMarker ? (kWinByte | e) : (m ? ((m - 1) << 15) | (e - kInflateMarker) : kWinByte);
   } else {
     v = m ? ((m - 1) << 15) | (i + n) : kWinByte;  // W_0's front: before the stream, never referenced
@@ -344,7 +347,7 @@ __global__ __launch_bounds__(256) void inflate_body_kernel(ResolveArgs a) {
     const uint32_t k = a.chain[m];
     const uint64_t len = a.rec[k].out_len, off = a.off[k];
     const uint64_t body = len > kInflateHist ? len - kInflateHist : 0;
-    const uint16_t *el = a.region + k * a.region_elems;
+    const uint16_t *el = a.region + a.rec[k].region;
     for (uint64_t t = (uint64_t)blockIdx.x * kTile; t < body; t += (uint64_t)gridDim.x * kTile) {
 #pragma unroll
       for (uint32_t j = 0; j < 16; j++) {
@@ -400,8 +403,9 @@ InflateSplitShape inflate_split_shape(uint64_t src_len, uint64_t cap, uint64_t w
   return sh;
 }
 
-// item regions: 3 x the average share (a part that absorbs a neighbour whose
-// start it did not land on needs twice its own) + kInflateSplitSlack
+// item regions: 3 x the average share + kInflateSplitSlack each; a chunk
+// with a candidate owns its items' and the following candidate-less chunks'
+// regions and splits them among its parts (inflate_spec_kernel)
 static uint64_t region_elems(uint64_t cap, uint64_t nitems) {
   return ((3 * cap) / nitems + kInflateSplitSlack + 7) & ~7ull;
 }
@@ -481,7 +485,32 @@ hipError_t launch_inflate_split(const uint8_t *src, uint64_t src_len, uint8_t *d
   ia.status = status;
   ia.n = 1;
   ia.run_if = run_serial;
-  return launch_inflate(ia, num_cus, stream, nullptr);
+  e = launch_inflate(ia, num_cus, stream, nullptr);
+  if (e == hipSuccess && getenv("ZCRC_SPLIT_TRACE")) {  // diagnostics: why a chain did (not) form
+    std::vector<uint64_t> hc(nch), hp(nit);
+    std::vector<SpecRec> hr(nit);
+    std::vector<uint32_t> hch(nit + 1), hrs(1);
+    e = hipStreamSynchronize(stream);
+    if (e == hipSuccess) e = hipMemcpy(hc.data(), cand, 8 * nch, hipMemcpyDeviceToHost);
+    if (e == hipSuccess) e = hipMemcpy(hp.data(), part, 8 * nit, hipMemcpyDeviceToHost);
+    if (e == hipSuccess) e = hipMemcpy(hr.data(), rec, sizeof(SpecRec) * nit, hipMemcpyDeviceToHost);
+    if (e == hipSuccess) e = hipMemcpy(hch.data(), chain, 4 * (nit + 1), hipMemcpyDeviceToHost);
+    if (e == hipSuccess) e = hipMemcpy(hrs.data(), run_serial, 4, hipMemcpyDeviceToHost);
+    if (e != hipSuccess) return e;
+    fprintf(stderr, "[split] src %llu cap %llu chunk %llu chunks %llu parts %u items %llu wide %d region %llu elems; "
+            "chain %u serial %u\n", (unsigned long long)src_len, (unsigned long long)cap, (unsigned long long)chunk,
+            (unsigned long long)nch, shape.parts, (unsigned long long)nit, (int)shape.wide,
+            (unsigned long long)relems, hch[nit], hrs[0]);
+    for (uint64_t i = 0; i < nit; i++) {
+      const SpecRec &r = hr[i];
+      if (r.status == kSpecSkipped) continue;
+      fprintf(stderr, "[split]   item %llu (chunk %llu part %llu) cand %lld part %lld: status %d link %d out %llu "
+              "reach %u final %u end_bit %llu\n", (unsigned long long)i, (unsigned long long)(i / shape.parts),
+              (unsigned long long)(i % shape.parts), (long long)hc[i / shape.parts], (long long)hp[i], r.status,
+              r.link, (unsigned long long)r.out_len, r.reach, r.final_, (unsigned long long)r.end_bit);
+    }
+  }
+  return e;
 }
 
 }  // namespace zcrc

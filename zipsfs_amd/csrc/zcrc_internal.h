@@ -135,6 +135,7 @@ constexpr int32_t kSpecSkipped = -1;    // SpecRec::status of an item without wo
 constexpr int32_t kSpecLanded = 100;    // codes(): stopped on a later part's start (internal)
 constexpr uint32_t kMaxParts = 8;       // items per chunk (a chunk's first block cut into parts)
 struct SpecRec {
+  uint64_t region;   // element offset of the item's output in the region array
   uint64_t out_len;  // elements produced
   uint64_t end_bit;  // bit position where the decode stopped
   int32_t status;    // ZCRC_INFLATE_*, or kSpecSkipped
@@ -147,8 +148,8 @@ struct SpecArgs {
   uint64_t src_len;
   const uint64_t *cand;  // per chunk: candidate bit position, or kSplitNone
   SpecRec *rec;          // per item (chunk k, part j) = item k * parts + j
-  uint16_t *region;      // item i's elements start at region + i * region_elems
-  uint64_t region_elems;
+  uint16_t *region;      // item outputs (SpecRec::region); chunk k with a candidate owns
+  uint64_t region_elems; // [k parts, k' parts) x region_elems up to the next such chunk k', split among its parts
   uint64_t nchunks;
   uint64_t *part;        // per item: the probed start of part j >= 1 (kSplitNone: none)
   uint32_t parts;        // items per chunk (<= kMaxParts)
