@@ -57,7 +57,7 @@ __host__ __device__ inline void window96(uint32_t w0, uint32_t w1, uint32_t w2, 
 // order 16 17 18 0 8 7 9 6 10 5 11 4 12 3 13 2 14 1 15, RFC 1951 3.2.7).
 // `avail`: staged bits from q.  sorted:
 // this thread's 19-byte scratch for the canonical symbol order.
-__host__ __device__ inline bool full_ok(const uint32_t *w, uint32_t q, uint32_t avail, uint8_t *sorted) {
+__host__ __device__ __forceinline__ bool full_ok(const uint32_t *w, uint32_t q, uint32_t avail, uint8_t *sorted) {
   const uint64_t v = bits64(w, q);
   const uint32_t nlen = (uint32_t)((v >> 3) & 31u) + 257u, ndist = (uint32_t)((v >> 8) & 31u) + 1u;
   const uint32_t hclen = (uint32_t)((v >> 13) & 15u) + 4u;
