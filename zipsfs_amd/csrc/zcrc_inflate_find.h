@@ -103,9 +103,18 @@ __host__ __device__ __forceinline__ bool full_ok(const uint32_t *w, uint32_t q, 
   const uint32_t total = nlen + ndist, end = q + avail;
   uint32_t idx = 0, prev = 0, kll = 0, kd = 0, mll = 0, md = 0;
   bool eob = false;
+  // a register bit buffer: bb holds the bits from p on (nb of them, >= 32
+  // at every symbol), refilled one aligned word at a time, so a symbol
+  // costs no dependent LDS read (bits64 per symbol did: 3 reads on the chain)
+  uint32_t wi = (p >> 5) + 1, nb = 32 - (p & 31u);
+  uint64_t bb = w[p >> 5] >> (p & 31u);
   while (idx < total) {
     if (p + 32 > end) return false;  // the header would run past the staged bytes
-    const uint32_t b = (uint32_t)bits64(w, p);
+    if (nb < 32) {
+      bb |= (uint64_t)w[wi++] << nb;
+      nb += 32;
+    }
+    const uint32_t b = (uint32_t)bb;
     // canonical decode, bit by bit (codes of at most 7 bits)
     uint32_t code = 0, first = 0, index = 0, sym = 32, used = 0;
 #pragma unroll
@@ -124,29 +133,32 @@ __host__ __device__ __forceinline__ bool full_ok(const uint32_t *w, uint32_t q, 
       }
     }
     if (sym == 32) return false;
-    p += used;
     const uint32_t x = b >> used;
-    uint32_t val, rep;
+    uint32_t val, rep, extra;
     if (sym < 16) {
       val = sym;
       rep = 1;
       prev = sym;
+      extra = 0;
     } else if (sym == 16) {
       if (idx == 0) return false;
       val = prev;
       rep = 3 + (x & 3u);
-      p += 2;
+      extra = 2;
     } else if (sym == 17) {
       val = 0;
       rep = 3 + (x & 7u);
-      p += 3;
+      extra = 3;
       prev = 0;
     } else {
       val = 0;
       rep = 11 + (x & 127u);
-      p += 7;
+      extra = 7;
       prev = 0;
     }
+    p += used + extra;  // <= 14 bits of the >= 32 buffered
+    bb >>= used + extra;
+    nb -= used + extra;
     if (idx + rep > total) return false;
     if (val) {
       // split the run at the literal/length | distance boundary
