@@ -54,6 +54,7 @@ struct FindArgs {
   uint64_t chunk;  // compressed bytes per chunk
   uint64_t nchunks;
   uint64_t *cand;
+  uint32_t timing;  // measurement builds only (ZCRC_SPLIT_FIND_TIMING): 1 = no full checks, 2 = no quick filter either
 };
 
 // One workgroup per chunk k >= 1: the first bit position in [8 k chunk,
@@ -120,7 +121,7 @@ __global__ __launch_bounds__(kFindThreads) void inflate_find_kernel(FindArgs a) 
     for (uint32_t sub = 0; sub * 32u * kFindSub < npos; sub++) {
       const uint32_t p = sub & 1u;
       const uint32_t i = sub * kFindSub + tid;  // this thread's word: positions 32 i .. 32 i + 31
-      if (32u * i < npos) {
+      if (32u * i < npos && a.timing < 2) {
         const uint32_t w0 = w[i], w1 = w[i + 1], w2 = w[i + 2], w3 = w[i + 3];
         uint32_t mask = 0;
 #pragma unroll
@@ -143,7 +144,7 @@ __global__ __launch_bounds__(kFindThreads) void inflate_find_kernel(FindArgs a) 
       __syncthreads();  // every thread has also read the other parity's counters of the last sub-window
       if (tid == 0) nsurv[p ^ 1u] = 0, best[p ^ 1u] = 0xFFFFFFFFu;
       const uint32_t ns = nsurv[p] < kFindSurv ? nsurv[p] : kFindSurv;  // more: the rest go unchecked (parallelism lost, never correctness)
-      for (uint32_t j = tid; j < ns; j += kFindThreads) {
+      for (uint32_t j = tid; j < ns && !a.timing; j += kFindThreads) {
         const uint32_t q = surv[j];
         if (find::full_ok(w, q, 8u * nbytes - q, sorted[j])) atomicMin(&best[p], q);
       }
@@ -463,7 +464,8 @@ hipError_t launch_inflate_split(const uint8_t *src, uint64_t src_len, uint8_t *d
   uint32_t *win[2] = {reinterpret_cast<uint32_t *>(take(4ull * kInflateHist * nit)),
                       reinterpret_cast<uint32_t *>(take(4ull * kInflateHist * nit))};
 
-  FindArgs fa{src, src_len, chunk, nch, cand};
+  const char *ft = getenv("ZCRC_SPLIT_FIND_TIMING");  // measurement only: candidates are then none
+  FindArgs fa{src, src_len, chunk, nch, cand, ft ? (uint32_t)atoi(ft) : 0u};
   hipLaunchKernelGGL(inflate_find_kernel, dim3((unsigned)nch), dim3(kFindThreads), 0, stream, fa);
   const char *pt = getenv("ZCRC_SPLIT_PROBE");  // test knob: tokens per probe (a few: unsynchronised part starts)
   SpecArgs sa{src, src_len, cand, rec, region, relems, nch, part, shape.parts,
