@@ -99,6 +99,19 @@ __host__ __device__ __forceinline__ bool full_ok(const uint32_t *w, uint32_t q, 
       }
     }
   }
+  // canonical code of each length: first code (MSB-first numbering) and
+  // the index of its first symbol in `sorted`
+  uint32_t first[8], base[8];
+  {
+    uint32_t code = 0, index = 0;
+#pragma unroll
+    for (uint32_t L = 1; L < 8; L++) {
+      first[L] = code;
+      base[L] = index;
+      index += cnt[L];
+      code = (code + cnt[L]) << 1;
+    }
+  }
   uint32_t p = q + 17 + 3 * hclen;  // next bit
   const uint32_t total = nlen + ndist, end = q + avail;
   uint32_t idx = 0, prev = 0, kll = 0, kd = 0, mll = 0, md = 0;
@@ -115,23 +128,20 @@ __host__ __device__ __forceinline__ bool full_ok(const uint32_t *w, uint32_t q, 
       nb += 32;
     }
     const uint32_t b = (uint32_t)bb;
-    // canonical decode, bit by bit (codes of at most 7 bits)
-    uint32_t code = 0, first = 0, index = 0, sym = 32, used = 0;
+    // branch-free canonical decode: the code's first L bits, MSB first, are
+    // rev7 >> (7 - L); the symbol's length is the smallest L whose codes
+    // [first, first + cnt) contain them (a prefix code: exactly one, or none
+    // for an incomplete code)
+    const uint32_t rev7 = __builtin_bitreverse32(b) >> 25;
+    uint32_t used = 0, at = 0;
 #pragma unroll
-    for (uint32_t L = 1; L < 8; L++) {
-      if (sym == 32) {
-        code |= (b >> (L - 1)) & 1u;
-        const uint32_t c = cnt[L];
-        if (code - first < c) {
-          sym = sorted[index + code - first];
-          used = L;
-        } else {
-          index += c;
-          first = (first + c) << 1;
-          code <<= 1;
-        }
-      }
+    for (uint32_t L = 7; L >= 1; L--) {
+      const uint32_t d = (rev7 >> (7 - L)) - first[L];
+      const bool hit = d < cnt[L];
+      used = hit ? L : used;
+      at = hit ? base[L] + d : at;
     }
+    const uint32_t sym = used ? sorted[at] : 32u;
     if (sym == 32) return false;
     const uint32_t x = b >> used;
     uint32_t val, rep, extra;
