@@ -133,7 +133,7 @@ constexpr uint32_t kInflateHist = 32768u;
 constexpr uint64_t kSplitNone = ~0ull;  // no candidate block start in the chunk
 constexpr int32_t kSpecSkipped = -1;    // SpecRec::status of an item without work
 constexpr int32_t kSpecLanded = 100;    // codes(): stopped on a later part's start (internal)
-constexpr uint32_t kMaxParts = 8;       // items per chunk (a chunk's first block cut into parts)
+constexpr uint32_t kMaxParts = 16;      // items per chunk (a chunk's first block cut into parts)
 struct SpecRec {
   uint64_t region;   // element offset of the item's output in the region array
   uint64_t out_len;  // elements produced
