@@ -165,3 +165,25 @@ def test_split_inflate_parts_and_unsynchronised_probes(monkeypatch, parts, probe
         for chunk in (0, 4096):
             st, out = _run(comp, len(data), chunk)
             assert st == 0 and out == data, (kind, chunk)
+
+
+def test_finder_finds_every_block_start(monkeypatch, capfd):
+    """Every dynamic block start of a zlib stream is found (a missed one only
+    costs parallelism, so the parity tests would not notice): with one part
+    per chunk and chunks smaller than a block, the chain has one item per
+    block (ZCRC_SPLIT_TRACE prints it)."""
+    import inflate_split_model as M
+    from test_inflate_split_model import _block_starts
+    monkeypatch.setenv("ZCRC_SPLIT_PARTS", "1")
+    monkeypatch.setenv("ZCRC_SPLIT_TRACE", "1")
+    for kind in ("text", "spectrum"):
+        data = S.PAYLOADS[kind](1 << 20, 5)
+        comp = S.deflate(data, 6)
+        blocks = _block_starts(comp)
+        assert all(t == 2 for _, t in blocks)
+        st, out = _run(comp, len(data), 4096)
+        assert st == 0 and out == data
+        err = capfd.readouterr().err
+        line = [l for l in err.splitlines() if l.startswith("[split] src")][-1]
+        chain = int(line.split("chain ")[1].split()[0])
+        assert chain == len(blocks), (kind, chain, len(blocks))
