@@ -48,6 +48,105 @@ constexpr uint32_t kFindLook = 1024;     // + look-ahead: a dynamic header is at
 constexpr uint32_t kFindWords = (kFindWin + kFindLook) / 4 + 4;
 constexpr uint32_t kFindSurv = 1024;     // survivors of the quick filter checked per window
 
+__device__ __forceinline__ uint32_t wuni(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); }
+__device__ __forceinline__ uint64_t wuni64(uint64_t v) { return ((uint64_t)wuni((uint32_t)(v >> 32)) << 32) | wuni((uint32_t)v); }
+
+// Position of code-length symbol s in the header's order (the inverse of
+// 16 17 18 0 8 7 9 6 10 5 11 4 12 3 13 2 14 1 15), 5 bits per symbol
+constexpr uint64_t kClenPosLo = 0x520c429d2b6be23ull;  // symbols 0..11
+constexpr uint64_t kClenPosHi = 0x820941ccull;         // symbols 12..18
+
+// find::full_ok for one position per WAVE (q wave-uniform): the same
+// checks, with the code-length code built by ballots (lane s holds symbol
+// s) into a 128-entry lookup table held in two VGPRs, and the length decode
+// run on scalar registers -- a table lookup (v_readlane) per symbol instead
+// of a per-lane canonical decode.  The lane-per-position form spent ~0.5 us
+// per symbol of its longest lane (profiles/r03/s34).  lut: this wave's
+// 128 bytes of LDS.
+__device__ bool full_ok_wave(const uint32_t *w, uint32_t q, uint32_t avail, uint8_t *lut) {
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint64_t v = wuni64(find::bits64(w, q));
+  const uint32_t nlen = (uint32_t)((v >> 3) & 31u) + 257u, ndist = (uint32_t)((v >> 8) & 31u) + 1u;
+  const uint32_t hclen = (uint32_t)((v >> 13) & 15u) + 4u;
+  const uint64_t cl = wuni64(find::bits64(w, q + 17));
+  const uint32_t pos = lane < 12 ? (uint32_t)(kClenPosLo >> (5 * lane)) & 31u
+                                 : (lane < 19 ? (uint32_t)(kClenPosHi >> (5 * (lane - 12))) & 31u : 31u);
+  const uint32_t l = pos < hclen ? (uint32_t)(cl >> (3 * pos)) & 7u : 0u;  // lane s: length of symbol s
+  // canonical codes (the quick filter made the code complete: 128 entries)
+  const uint64_t lt = (1ull << lane) - 1ull;
+  uint32_t code = 0, mycode = 0;
+#pragma unroll
+  for (uint32_t L = 1; L < 8; L++) {
+    const uint64_t m = __ballot(l == L);
+    if (l == L) mycode = code + (uint32_t)__builtin_popcountll(m & lt);
+    code = (code + (uint32_t)__builtin_popcountll(m)) << 1;
+  }
+  if (l) {  // entries in stream bit order: the reversed code, then any bits
+    const uint32_t r = __builtin_bitreverse32(mycode) >> (32 - l);
+    for (uint32_t t = 0; t < (1u << (7 - l)); t++) lut[r | (t << l)] = (uint8_t)(lane | (l << 5));
+  }
+  __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): the wave's LUT writes are done
+  __builtin_amdgcn_wave_barrier();
+  const uint32_t lut_lo = lut[lane], lut_hi = lut[lane + 64];
+  uint32_t p = q + 17 + 3 * hclen;
+  const uint32_t total = nlen + ndist, end = q + avail;
+  uint32_t idx = 0, prev = 0, kll = 0, kd = 0, mll = 0, md = 0;
+  bool eob = false;
+  uint32_t wi = (p >> 5) + 1, nb = 32 - (p & 31u);
+  uint64_t bb = wuni(w[p >> 5]) >> (p & 31u);
+  while (idx < total) {
+    if (p + 32 > end) return false;  // the header would run past the staged bytes
+    if (nb < 32) {
+      bb |= (uint64_t)wuni(w[wi++]) << nb;
+      nb += 32;
+    }
+    const uint32_t x = (uint32_t)bb & 127u;
+    const uint32_t e = (uint32_t)__builtin_amdgcn_readlane((int)(x < 64 ? lut_lo : lut_hi), (int)(x & 63u));
+    const uint32_t sym = e & 31u, used = e >> 5;
+    const uint32_t xb = (uint32_t)(bb >> used);
+    uint32_t val, rep, extra;
+    if (sym < 16) {
+      val = sym;
+      rep = 1;
+      prev = sym;
+      extra = 0;
+    } else if (sym == 16) {
+      if (idx == 0) return false;
+      val = prev;
+      rep = 3 + (xb & 3u);
+      extra = 2;
+    } else if (sym == 17) {
+      val = 0;
+      rep = 3 + (xb & 7u);
+      extra = 3;
+      prev = 0;
+    } else {
+      val = 0;
+      rep = 11 + (xb & 127u);
+      extra = 7;
+      prev = 0;
+    }
+    p += used + extra;
+    bb >>= used + extra;
+    nb -= used + extra;
+    if (idx + rep > total) return false;
+    if (val) {
+      const uint32_t in_ll = idx < nlen ? (nlen - idx < rep ? nlen - idx : rep) : 0u;
+      kll += in_ll << (15 - val);
+      kd += (rep - in_ll) << (15 - val);
+      if (in_ll) mll = val > mll ? val : mll;
+      if (rep > in_ll) md = val > md ? val : md;
+      if (idx <= 256 && 256 < idx + rep) eob = true;
+      if (kll > 32768u || kd > 32768u) return false;
+    }
+    idx += rep;
+  }
+  if (!eob) return false;
+  if (kll > 32768u || (kll < 32768u && mll != 1u)) return false;
+  if (kd > 32768u || (kd < 32768u && md > 1u)) return false;
+  return true;
+}
+
 struct FindArgs {
   const uint8_t *src;
   uint64_t src_len;
@@ -70,7 +169,7 @@ constexpr uint32_t kFindSub = kFindThreads;  // words per sub-window (32 positio
 __global__ __launch_bounds__(kFindThreads) void inflate_find_kernel(FindArgs a) {
   __shared__ uint32_t w[kFindWords];
   __shared__ uint32_t surv[kFindSurv];
-  __shared__ uint8_t sorted[kFindSurv][20];
+  __shared__ uint8_t lutw[kFindThreads / 64][128];  // each wave's code-length LUT (full_ok_wave)
   // per sub-window parity: its survivor count and best position (double-
   // buffered: a count is reset one sub-window after it was last read)
   __shared__ uint32_t nsurv[2], best[2];
@@ -144,9 +243,13 @@ __global__ __launch_bounds__(kFindThreads) void inflate_find_kernel(FindArgs a) 
       __syncthreads();  // every thread has also read the other parity's counters of the last sub-window
       if (tid == 0) nsurv[p ^ 1u] = 0, best[p ^ 1u] = 0xFFFFFFFFu;
       const uint32_t ns = nsurv[p] < kFindSurv ? nsurv[p] : kFindSurv;  // more: the rest go unchecked (parallelism lost, never correctness)
-      for (uint32_t j = tid; j < ns && !a.timing; j += kFindThreads) {
-        const uint32_t q = surv[j];
-        if (find::full_ok(w, q, 8u * nbytes - q, sorted[j])) atomicMin(&best[p], q);
+      // one survivor per wave at a time (the CPU test checks find::full_ok,
+      // which full_ok_wave restates; the GPU test checks the chain finds
+      // every block start)
+      const uint32_t wv = tid >> 6;
+      for (uint32_t j = wv; j < ns && !a.timing; j += kFindThreads / 64) {
+        const uint32_t q = wuni(surv[j]);
+        if (full_ok_wave(w, q, 8u * nbytes - q, lutw[wv]) && (tid & 63u) == 0) atomicMin(&best[p], q);
       }
       __syncthreads();
       const uint32_t bq = best[p];  // workgroup-uniform
