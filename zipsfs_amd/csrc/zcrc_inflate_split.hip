@@ -510,14 +510,17 @@ InflateSplitShape inflate_split_shape(uint64_t src_len, uint64_t cap, uint64_t w
   }
   const uint64_t need = (src_len + kChainLds - 1) / kChainLds;  // at most kChainLds chunks
   sh.chunk = c < need ? need : c;
-  // parts: while the chunks leave resident decoders idle, cut each chunk's
-  // first block into parts (items), up to kMaxParts; items stay <= kChainLds.
-  // Typically half the chunks or fewer find a block start (zlib's blocks
-  // span 2-4 chunks of 8 KiB), so the items with work are about half the
-  // items: 2 x resident / chunks parts fill the decoders.
+  // parts: for small streams (at most a quarter as many chunks as resident
+  // decoders), cut each chunk's first block into parts (items), up to
+  // kMaxParts; items stay <= kChainLds.  Typically half the chunks or fewer
+  // find a block start (zlib's blocks span 2-4 chunks of 8 KiB), so 2 x
+  // resident / chunks parts fill the decoders.  Above that the probes'
+  // header parses and the pointer-jumping rounds over twice the items cost
+  // more than the shorter decodes save (16 MiB spectrum 5.6 against 3.8 ms,
+  // 64 MiB text 9.3 against 6.4 ms: profiles/r03/s38 against s35).
   const uint64_t nch = src_len ? (src_len + sh.chunk - 1) / sh.chunk : 1;
   const uint64_t resident = (sh.wide ? kSpecPerCuWide : kSpecPerCu) * cus;
-  uint64_t parts = nch < 2 * resident ? 2 * resident / nch : 1;
+  uint64_t parts = 4 * nch <= resident ? 2 * resident / nch : 1;
   const char *fp = getenv("ZCRC_SPLIT_PARTS");  // (read per call: tests set it)
   const int force_parts = fp ? atoi(fp) : 0;
   if (force_parts > 0) parts = (uint64_t)force_parts;
