@@ -142,13 +142,17 @@ int zcrc_inflate_batch_device(const void *const *d_src, const uint64_t *d_src_le
  * deflated entry at a time (zip_fread() in preloadram_now,
  * src/ZIPsFS_preloadfileram.c:286-306), which the batch call above would
  * decode on a single wave.  The compressed bytes are cut into chunks of
- * chunk_bytes (0: 16 KiB, grown so that there are at most 16,384); each chunk
+ * chunk_bytes (0: 8 KiB, grown to fill the resident decoders and so that
+ * there are at most 16,384); each chunk
  * decodes from the first valid block header in it with an unknown history,
  * the chunks reachable from the stream's start are stitched together, and
  * when that fails (corrupt data, a chunk's output far above the average
  * ratio) the stream is decoded serially, with zlib's status.  Same results
  * as zcrc_inflate_batch_device for one stream (*d_out_len, *d_status).
- * Scratch: about 4 x cap bytes of HBM, kept per HIP stream.  Asynchronous. */
+ * Scratch: about 6 x cap bytes of HBM plus ~288 KiB per decode item (two
+ * 128 KiB history windows and slack; items = chunks x parts, at most 16,384),
+ * kept per HIP stream.  Not graph-capturable (ZCRC_ERR_ARG under capture).
+ * Asynchronous. */
 int zcrc_inflate_device(const void *d_src, uint64_t src_len, void *d_dst, uint64_t cap, uint64_t *d_out_len,
                         int32_t *d_status, uint64_t chunk_bytes, void *stream);
 /* Same for host memory, plus the CRC-32 of every output: the preload of a
@@ -194,8 +198,8 @@ void zcrc32_stream_close(zcrc32_stream *s);
 int zcrc32_stream_stats(const zcrc32_stream *s, uint64_t *registered_pieces, uint64_t *staged_pieces,
                         uint64_t *pageable_pieces);
 
-/* Device initialisation plus up to `staging_slots` pinned staging slots,
- * created now and exercised by two staged calls (~20 ms once; the HIP
+/* Device initialisation plus up to `staging_slots` pinned staging slots per
+ * logical device of the set (zcrc_device_set), created now and exercised by two staged calls (~20 ms once; the HIP
  * runtime's first few SDMA copies of a process can block their caller for
  * milliseconds) -- call it at startup (ZIPsFS: before the preload threads),
  * outside any lock.  The drop-in never creates a slot itself (it runs under
@@ -287,6 +291,23 @@ const char *zcrc_kernel_name_for(size_t n);
 /* The small-buffer kernel the general-form device entry points launch. */
 const char *zcrc_small_kernel_name(void);
 int zcrc_device_info(int *num_cus, int *arch_major, int *arch_minor);
+/* The device set the host-memory entry points spread over (zcrc32,
+ * zcrc32_checked, zcrc32_batch, zcrc32_stream_open*, zcrc_inflate_batch,
+ * zcrc_zip_verify_host): env ZCRC_DEVICES (read once; comma-separated HIP
+ * device indices, repeats allowed), default every visible gfx950.  A host
+ * call of T bytes runs on min(devices, T / ZCRC_SHARD_MIN_BYTES) of them
+ * (default 8 MiB per device; at least 1, the least loaded): buffers are cut
+ * into byte-balanced shards, one per device, and a buffer cut at a shard
+ * boundary is reassembled with the GF(2) combine.  A stream lives on the
+ * least loaded device when opened.  Device-pointer entry points use the
+ * caller's current device.  Writes up to `capacity` indices; *n = set size. */
+int zcrc_device_set(int *devices, size_t capacity, size_t *n);
+/* The shard plan of a host batch (no device needed): with lens[0..n) cut
+ * into `shards` byte-balanced shards, buffer i starts in shard first[i] and
+ * has pieces[i] pieces (its later pieces open the following shards);
+ * shard_bytes[g] = bytes of shard g.  Any output may be NULL. */
+int zcrc_shard_plan(const size_t *lens, size_t n, size_t shards, uint32_t *first, uint32_t *pieces,
+                    uint64_t *shard_bytes);
 /* When enabled, each device launch of the CRC kernels is timed by
  * timestamps of its own dispatch packet; zcrc_profile_read returns the
  * summed milliseconds and launch count of the batch kernel since the last

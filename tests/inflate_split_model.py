@@ -297,6 +297,8 @@ def codes(br: Bits, ll, dd, out: list, res: ChunkResult, spec: bool) -> int:
         if br.over:
             return ERR_INPUT
         p = len(out)
+        if MATCH_HOOK is not None:
+            MATCH_HOOK(p, length, dist, spec)
         if dist > p:
             if not spec or dist > p + WINDOW:
                 return ERR_DIST
@@ -304,6 +306,9 @@ def codes(br: Bits, ll, dd, out: list, res: ChunkResult, spec: bool) -> int:
         for t in range(length):
             s = p - dist + t
             out.append(out[s] if s >= 0 else MARKER + WINDOW + s)
+
+
+MATCH_HOOK = None  # tests: called with (position, length, distance, spec) per match of codes()
 
 
 def inflate_split(data: bytes, cap: int, chunk_bytes: int, region=None):

@@ -47,6 +47,20 @@ def far_repeat_payload(n: int, seed: int) -> bytes:
     return (blk * (n // len(blk) + 2))[:n]
 
 
+def near_ring_payload(n: int, seed: int, period: int = 16484, fresh: int = 8000) -> bytes:
+    """Periods of `fresh` random bytes followed by a copy of the bytes one
+    period back: the copies deflate to length-258 matches at distance
+    `period`, just past a 16 Ki ring (the sp16 decoder's copy_spec
+    aliased ring slots for kWin < dist < kWin + len)."""
+    rng = np.random.default_rng(seed)
+    out = bytearray(rng.integers(0, 256, period, dtype=np.uint8).tobytes())
+    while len(out) < n:
+        base = len(out)
+        out += rng.integers(0, 256, fresh, dtype=np.uint8).tobytes()
+        out += out[base + fresh - period: base]  # the bytes one period back
+    return bytes(out[:n])
+
+
 def runs_payload(n: int, seed: int) -> bytes:
     rnd = random.Random(seed)
     out = bytearray()
@@ -74,6 +88,18 @@ def deflate_chunked(data: bytes, chunk: int, level: int = 6) -> bytes:
     for k in range(0, len(data), chunk):
         out.append(c.compress(data[k:k + chunk]))
         out.append(c.flush(zlib.Z_FULL_FLUSH if (k // chunk) % 2 else zlib.Z_SYNC_FLUSH))
+    out.append(c.flush())
+    return b"".join(out)
+
+
+def deflate_sync(data: bytes, every: int, level: int = 6) -> bytes:
+    """A Z_SYNC_FLUSH every `every` input bytes: block starts at chosen output
+    positions, the history kept across them."""
+    c = zlib.compressobj(level, zlib.DEFLATED, -15)
+    out = []
+    for k in range(0, len(data), every):
+        out.append(c.compress(data[k:k + every]))
+        out.append(c.flush(zlib.Z_SYNC_FLUSH))
     out.append(c.flush())
     return b"".join(out)
 

@@ -167,6 +167,24 @@ def test_split_inflate_parts_and_unsynchronised_probes(monkeypatch, parts, probe
             assert st == 0 and out == data, (kind, chunk)
 
 
+@pytest.mark.parametrize("parts", [1, 8])
+def test_sp16_matches_just_past_the_ring(monkeypatch, parts):
+    """with the 16 Ki ring forced, back-references at
+    distances in (16 Ki, 16 Ki + len) that reach before a chunk's start
+    (copy_spec) must not read ring slots an earlier 64-lane step of the same
+    copy overwrote.  Block starts at several offsets put such copies at every
+    position relative to the chunk start (tests/test_inflate_split_model.py
+    checks the stream holds them)."""
+    monkeypatch.setenv("ZCRC_SPLIT_RING", "16")
+    monkeypatch.setenv("ZCRC_SPLIT_PARTS", str(parts))
+    data = S.near_ring_payload(1 << 20, 3)
+    for every in (24000, 33000, 40000):
+        comp = S.deflate_sync(data, every)
+        for chunk in (0, 4096, 512):
+            st, out = _run(comp, len(data), chunk)
+            assert st == 0 and out == data, (every, chunk)
+
+
 def test_finder_finds_every_block_start(monkeypatch, capfd):
     """Every dynamic block start of a zlib stream is found (a missed one only
     costs parallelism, so the parity tests would not notice): with one part

@@ -129,3 +129,31 @@ def test_model_parts_survive_unsynchronised_probes():
     st, out, stats = M.inflate_split_parts(comp, len(data), 4096, parts=8, probe_tokens=2)
     assert st == M.OK and out == data, stats
     assert stats["chain"] < stats["items"]
+
+
+def test_near_ring_stream_holds_aliasing_copies(monkeypatch):
+    """The stream of tests/test_gpu_inflate_split.py::test_sp16_matches_just_past_the_ring
+    really holds speculative copies that reach before the chunk start at
+    16 Ki < dist < 16 Ki + len, where a 64-lane step would read a ring slot an
+    earlier step of the same copy wrote."""
+    hits = []
+
+    def hook(p, length, dist, spec):
+        if not spec or dist <= p or not 16384 < dist < 16384 + length:
+            return
+        for i in range(max(dist - p, 0), length):  # source p - dist + i >= 0: a ring element
+            w = i - (dist - 16384)                   # the element whose slot it shares
+            if 0 <= w and w // 64 < i // 64:
+                hits.append((p, length, dist))
+                return
+
+    monkeypatch.setattr(M, "MATCH_HOOK", hook)
+    data = S.near_ring_payload(320 << 10, 3)
+    for every in (24000, 40000):
+        comp = S.deflate_sync(data, every)
+        assert _zlib(comp) == data
+        cand = M.find_candidates(comp, 4096)
+        for k, c in enumerate(cand):
+            if c is not None:
+                M.spec_decode(comp, c, cand, k, True)
+    assert hits

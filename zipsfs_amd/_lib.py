@@ -56,6 +56,8 @@ _SIGNATURES = {
     "zcrc_kernel_name_for": (ctypes.c_char_p, [ctypes.c_size_t]),
     "zcrc_small_kernel_name": (ctypes.c_char_p, []),
     "zcrc_device_info": (_c_int, [ctypes.POINTER(_c_int)] * 3),
+    "zcrc_device_set": (_c_int, [_c_p, _c_sz, ctypes.POINTER(_c_sz)]),
+    "zcrc_shard_plan": (_c_int, [_c_p, _c_sz, _c_sz, _c_p, _c_p, _c_p]),
     "zcrc_profile_enable": (None, [_c_int]),
     "zcrc_profile_read": (_c_int, [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(_c_int)]),
     "zcrc_profile_read_kind": (_c_int, [_c_int, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(_c_int)]),

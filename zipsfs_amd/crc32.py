@@ -28,6 +28,7 @@ __all__ = [
     "crc32_batch_strided", "crc32_tensors", "crc32_combine", "fhandle_check_crc32",
     "verify_entries", "fill_synthetic", "profile", "device_info", "version",
     "inflate_batch_device", "inflate_to_device", "inflate_batch", "inflate_device", "INFLATE_STATUS",
+    "device_set", "shard_plan",
 ]
 
 
@@ -475,3 +476,28 @@ def kernel_source_hash() -> str:
     for f in ("zcrc_batch_kernel.h", "zcrc_small_kernel.h", "zcrc_internal.h", "zcrc_gf2.h", "zcrc_kernels.hip"):
         h.update(open(os.path.join(d, f), "rb").read())
     return h.hexdigest()[:16]
+
+
+def device_set() -> list:
+    """HIP device indices the host-memory entry points spread over
+    (zcrc_device_set; env ZCRC_DEVICES, default every visible gfx950)."""
+    n = ctypes.c_size_t(0)
+    lib().zcrc_device_set(None, 0, ctypes.byref(n))
+    buf = (ctypes.c_int * max(n.value, 1))()
+    check(lib().zcrc_device_set(buf, n.value, ctypes.byref(n)), "zcrc_device_set")
+    return [int(buf[k]) for k in range(n.value)]
+
+
+def shard_plan(lens: Sequence[int], shards: int) -> dict:
+    """zcrc_shard_plan: how a host batch of these lengths is cut into
+    byte-balanced shards (first shard and piece count per buffer, bytes per
+    shard).  Host-only arithmetic."""
+    n = len(lens)
+    ln = np.ascontiguousarray(np.asarray(lens, dtype=np.uint64))
+    first = np.zeros(max(n, 1), dtype=np.uint32)
+    pieces = np.zeros(max(n, 1), dtype=np.uint32)
+    sb = np.zeros(max(int(shards), 1), dtype=np.uint64)
+    check(lib().zcrc_shard_plan(ln.ctypes.data if n else None, n, int(shards), first.ctypes.data, pieces.ctypes.data,
+                                sb.ctypes.data), "zcrc_shard_plan")
+    return {"first": first[:n], "pieces": pieces[:n], "shard_bytes": sb}
+

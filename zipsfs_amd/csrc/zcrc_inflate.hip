@@ -35,6 +35,7 @@
 
 #include "../../include/zcrc.h"
 #include "zcrc_internal.h"
+#include "zcrc_inflate_internal.h"
 
 #ifdef ZCRC_INFLATE_TRACE
 #define ITRACE(...) do { if (threadIdx.x == 0 && blockIdx.x < 4) printf(__VA_ARGS__); } while (0)

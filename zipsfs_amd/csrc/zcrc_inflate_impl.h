@@ -472,8 +472,12 @@ __device__ __forceinline__ void copy_match(Lds &s, const Out &o, uint32_t p0, ui
 // source precedes the copy, so the 64-lane steps are independent.
 __device__ __noinline__ void copy_spec(Lds &s, const Out &o, uint32_t p0, uint32_t len, uint32_t dist) {
   const uint32_t lane = lane_id();
-  // flushed elements [0, p0 - kWin) are read back from dst (sc1)
-  const uint32_t nfar = p0 > kWin ? p0 - kWin : 0u;
+  // Sources below p0 + len - kWin are read back from dst (sc1): they are
+  // flushed (pos - fl < kFlushLag + 1024 + 258 < kWin - 258), and their ring
+  // slots are the ones this copy's earlier 64-lane steps overwrite (a source
+  // p0 + i' - kWin shares slot p0 + i' with element i' when kWin < dist <
+  // kWin + len).  Sources at or above it sit in slots no step writes.
+  const uint32_t nfar = p0 + len > kWin ? p0 + len - kWin : 0u;
   const __amdgpu_buffer_rsrc_t far = __builtin_amdgcn_make_buffer_rsrc(o.dst, (short)0, (int)(nfar << kEsh), 0x00020000);
   for (uint32_t i0 = 0; i0 < len; i0 += 64) {
     const uint32_t i = i0 + lane;

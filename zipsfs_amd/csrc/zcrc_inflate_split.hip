@@ -38,6 +38,7 @@
 #include "../../include/zcrc.h"
 #include "zcrc_inflate_find.h"
 #include "zcrc_internal.h"
+#include "zcrc_inflate_internal.h"
 
 namespace zcrc {
 namespace {
@@ -489,10 +490,8 @@ __global__ __launch_bounds__(256) void inflate_body_kernel(ResolveArgs a) {
 // reads of old output back from HBM) while its residents suffice, else the
 // 16 Ki ring (four per CU).  ZCRC_SPLIT_RING=16|32 forces one (measurement).
 InflateSplitShape inflate_split_shape(uint64_t src_len, uint64_t cap, uint64_t want, int num_cus) {
-  static const int force = [] {
-    const char *e = getenv("ZCRC_SPLIT_RING");
-    return e ? atoi(e) : 0;
-  }();
+  const char *fr = getenv("ZCRC_SPLIT_RING");  // (read per call: tests set it)
+  const int force = fr ? atoi(fr) : 0;
   const uint64_t cus = (uint64_t)(num_cus > 0 ? num_cus : 1);
   InflateSplitShape sh;
   // text-like streams (ratio >= 2.5) reach back far more often: the whole

@@ -18,7 +18,10 @@
 #include <atomic>
 #include <chrono>
 #include <condition_variable>
+#include <deque>
+#include <functional>
 #include <map>
+#include <memory>
 #include <mutex>
 #include <new>
 #include <string>
@@ -29,6 +32,8 @@
 #include "../../include/zcrc.h"
 #include "zcrc_gf2.h"
 #include "zcrc_internal.h"
+#include "zcrc_inflate_internal.h"
+#include "zcrc_runtime.h"
 #include "zcrc_tables.h"
 
 namespace zcrc {
@@ -111,6 +116,102 @@ int device_ctx(DeviceCtx **out) {
   *out = &c;
   return ZCRC_OK;
 }
+
+// ------------------------------------------------------------- device set
+// The GPUs the host-memory entry points spread over (ZIPsFS is one process
+// whose preload threads -- up to ROOTS=32, src/ZIPsFS_async.c:468-497,
+// src/ZIPsFS_configuration.h:110 -- all call cg_crc32 from
+// src/ZIPsFS_preloadfileram.c:243).  ZCRC_DEVICES (read once) lists device
+// indices, repeats allowed ("0,0": two logical devices on one GPU, each
+// with its own worker and staging leases -- the multi-device path on a
+// one-GPU box); unset or "all": every visible gfx950.  Device-pointer entry
+// points run on the caller's current device, where their data lives.
+struct DeviceSet {
+  std::vector<int> phys;                    // logical -> HIP device index
+  std::unique_ptr<std::atomic<int>[]> load;  // per logical device: host calls in flight + open streams
+  std::string err;                          // why the set is empty
+};
+
+const DeviceSet &device_set() {
+  static DeviceSet ds;
+  static std::once_flag once;
+  std::call_once(once, [] {
+    int count = 0;
+    if (hipGetDeviceCount(&count) != hipSuccess || count <= 0) {
+      (void)hipGetLastError();
+      ds.err = "no HIP device visible";
+      return;
+    }
+    const char *env = getenv("ZCRC_DEVICES");
+    if (env && *env && strcmp(env, "all") != 0) {
+      for (const char *p = env; *p;) {
+        char *end = nullptr;
+        const long d = strtol(p, &end, 10);
+        if (end == p || d < 0 || d >= count || (*end && *end != ',')) {
+          ds.phys.clear();
+          ds.err = std::string("ZCRC_DEVICES=\"") + env + "\": expected comma-separated device indices below " +
+                   std::to_string(count);
+          return;
+        }
+        ds.phys.push_back((int)d);
+        p = *end ? end + 1 : end;
+      }
+    } else {
+      for (int d = 0; d < count; d++) {
+        hipDeviceProp_t prop;
+        if (hipGetDeviceProperties(&prop, d) == hipSuccess && strncmp(prop.gcnArchName, "gfx950", 6) == 0)
+          ds.phys.push_back(d);
+      }
+      if (ds.phys.empty()) ds.err = "no gfx950 device visible";
+    }
+    ds.load.reset(new std::atomic<int>[ds.phys.size() ? ds.phys.size() : 1]);
+    for (size_t k = 0; k < ds.phys.size(); k++) ds.load[k].store(0);
+  });
+  return ds;
+}
+
+// The logical device with the least work in flight (host calls + open
+// streams), ties broken round-robin so that serial callers -- ZIPsFS's
+// drop-in calls run one at a time under mutex_fhandle -- still rotate.
+size_t pick_logical() {
+  const DeviceSet &ds = device_set();
+  const size_t g = ds.phys.size();
+  if (g <= 1) return 0;
+  static std::atomic<uint32_t> rr{0};
+  const size_t start = rr.fetch_add(1, std::memory_order_relaxed) % g;
+  size_t best = start;
+  int best_load = ds.load[start].load(std::memory_order_relaxed);
+  for (size_t k = 1; k < g; k++) {
+    const size_t j = (start + k) % g;
+    const int l = ds.load[j].load(std::memory_order_relaxed);
+    if (l < best_load) best = j, best_load = l;
+  }
+  return best;
+}
+
+struct LoadMark {
+  size_t lg;
+  explicit LoadMark(size_t l) : lg(l) { device_set().load[lg].fetch_add(1, std::memory_order_relaxed); }
+  ~LoadMark() { device_set().load[lg].fetch_sub(1, std::memory_order_relaxed); }
+};
+
+// Makes `dev` the calling thread's current device for a scope and restores
+// the caller's afterwards (a caller such as PyTorch keeps its own).
+struct DeviceGuard {
+  int prev = -1;
+  int enter(int dev) {
+    int cur = 0;
+    ZCRC_HIP_TRY(hipGetDevice(&cur));
+    if (cur != dev) {
+      ZCRC_HIP_TRY(hipSetDevice(dev));
+      prev = cur;
+    }
+    return ZCRC_OK;
+  }
+  ~DeviceGuard() {
+    if (prev >= 0) (void)hipSetDevice(prev);
+  }
+};
 
 // ------------------------------------------------------------- profiling
 
@@ -372,6 +473,28 @@ int batch_device_ws(const void *const *d_ptrs, const uint64_t *d_lens, const uin
 // ZCRC_FUSED=1 takes it for every n <= kFusedMaxN, ZCRC_FUSED=0 never (the
 // in-kernel scan alone made config 2's CRC launch 7.7 us longer than the plan
 // launch it replaced: profiles/r02/fused_vs_two_launch_c2.jsonl).
+// Which form the last zcrc32_batch_device call on a (device, stream) took:
+// the one-launch form has no prefix and never sets the fault word, so
+// zcrc32_batch_device_faults must not report a stale word a two-launch call
+// left in the stream's batch scratch.
+std::mutex g_last_form_mu;
+std::map<std::pair<int, hipStream_t>, bool> g_last_fused;
+
+void note_last_form(hipStream_t st, bool fused) {
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  std::lock_guard<std::mutex> lk(g_last_form_mu);
+  g_last_fused[{dev, st}] = fused;
+}
+
+bool last_form_fused(hipStream_t st) {
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  std::lock_guard<std::mutex> lk(g_last_form_mu);
+  const auto it = g_last_fused.find({dev, st});
+  return it != g_last_fused.end() && it->second;
+}
+
 bool fused_enabled(size_t n, int num_cus) {
   const char *e = getenv("ZCRC_FUSED");  // read per call: tests switch it
   if (e && e[0] == '0') return false;
@@ -1071,6 +1194,213 @@ int batch_host(const void *const *ptrs, const size_t *lens, const uint32_t *seed
   return ZCRC_OK;
 }
 
+// ------------------------------------------------------------- multi-device host batches
+// A host batch (zcrc32_batch, zcrc32_checked, the drop-in) is cut into G
+// byte-balanced shards, one per logical device: shard g covers bytes
+// [T g / G, T (g+1) / G) of the buffers' concatenation (T = total bytes).  A
+// buffer that crosses a shard boundary is cut there; its later pieces are
+// checksummed from seed 0 and folded in on the host with the GF(2) combine,
+// crc(A || B) = combine(crc(A), crc(B), |B|).  Byte ranges rather than
+// "buffer i to device i mod G": ZIP entries are Zipf-sized (config 4: 2,339
+// buffers of >= 1 MiB carry 76% of the bytes), and ZIPsFS hands the drop-in
+// ONE entry per call under mutex_fhandle -- only cutting the entry spreads
+// it over the devices' PCIe links.  Every device gets at least
+// shard_min_bytes() (ZCRC_SHARD_MIN_BYTES, default 8 MiB, read per call so
+// tests can force small shards): below that a device's fixed cost per call
+// (~20-40 us of lease, launch and event) outweighs its share.
+constexpr size_t kShardMinBytes = 8ull << 20;
+
+size_t shard_min_bytes() {
+  const char *e = getenv("ZCRC_SHARD_MIN_BYTES");
+  if (e && *e) {
+    const unsigned long long v = strtoull(e, nullptr, 0);
+    return v ? (size_t)v : 1;
+  }
+  return kShardMinBytes;
+}
+
+size_t shard_count(uint64_t total, size_t devices, size_t min_bytes) {
+  const uint64_t by_bytes = total / (min_bytes ? min_bytes : 1);
+  return (size_t)std::max<uint64_t>(1, std::min<uint64_t>(devices, by_bytes));
+}
+
+struct ShardPlan {
+  struct Piece {
+    size_t buf, off, len;
+  };
+  std::vector<std::vector<Piece>> shard;  // shard g's pieces, in buffer order
+  // buffer i: first piece = shard[first[i]][item[i]]; its `extra[i]` later
+  // pieces are item 0 of shards first[i] + 1 ... first[i] + extra[i]
+  std::vector<uint32_t> first, item, extra;
+};
+
+void plan_shards(const size_t *lens, size_t n, size_t g_count, ShardPlan *p) {
+  uint64_t total = 0;
+  for (size_t i = 0; i < n; i++) total += lens[i];
+  p->shard.assign(g_count, {});
+  p->first.resize(n);
+  p->item.resize(n);
+  p->extra.assign(n, 0);
+  auto end_of = [&](size_t g) -> uint64_t {
+    return g + 1 >= g_count ? total : (uint64_t)((unsigned __int128)total * (g + 1) / g_count);
+  };
+  size_t g = 0;
+  uint64_t pos = 0;
+  for (size_t i = 0; i < n; i++) {
+    while (g + 1 < g_count && pos >= end_of(g)) g++;  // a buffer starting on a boundary opens the next shard
+    p->first[i] = (uint32_t)g;
+    p->item[i] = (uint32_t)p->shard[g].size();
+    size_t off = 0;
+    for (;;) {
+      size_t take = lens[i] - off;
+      if (g + 1 < g_count) take = (size_t)std::min<uint64_t>(take, end_of(g) - pos);
+      p->shard[g].push_back({i, off, take});
+      off += take;
+      pos += take;
+      if (off == lens[i]) break;
+      g++;  // the rest continues as item 0 of the next shard
+      p->extra[i]++;
+    }
+  }
+}
+
+// One persistent worker thread per shard index >= 1 (shard 0 runs on the
+// calling thread).  Jobs of concurrent callers queue per worker; a job never
+// waits on another worker.
+class ShardWorkers {
+ public:
+  static ShardWorkers &get() {
+    static ShardWorkers *w = new ShardWorkers();  // never destroyed: threads outlive static destructors
+    return *w;
+  }
+  void run(size_t m, const std::function<void(size_t)> &fn) {
+    if (m == 0) return;
+    struct Latch {
+      std::mutex mu;
+      std::condition_variable cv;
+      size_t left = 0;
+    } latch;
+    latch.left = m - 1;
+    for (size_t k = 1; k < m; k++) {
+      Worker &w = worker(k);
+      {
+        std::lock_guard<std::mutex> lk(w.mu);
+        w.q.push_back([&fn, &latch, k] {
+          fn(k);
+          std::lock_guard<std::mutex> l2(latch.mu);
+          if (--latch.left == 0) latch.cv.notify_one();
+        });
+      }
+      w.cv.notify_one();
+    }
+    fn(0);
+    std::unique_lock<std::mutex> lk(latch.mu);
+    latch.cv.wait(lk, [&] { return latch.left == 0; });
+  }
+
+ private:
+  struct Worker {
+    std::mutex mu;
+    std::condition_variable cv;
+    std::deque<std::function<void()>> q;
+  };
+  Worker &worker(size_t k) {
+    std::lock_guard<std::mutex> lk(mu_);
+    while (workers_.size() <= k) {
+      workers_.emplace_back(new Worker());
+      Worker *w = workers_.back().get();
+      std::thread([w] {
+        for (;;) {
+          std::function<void()> job;
+          {
+            std::unique_lock<std::mutex> l(w->mu);
+            w->cv.wait(l, [&] { return !w->q.empty(); });
+            job = std::move(w->q.front());
+            w->q.pop_front();
+          }
+          job();
+        }
+      }).detach();
+    }
+    return *workers_[k];
+  }
+  std::mutex mu_;
+  std::vector<std::unique_ptr<Worker>> workers_;
+};
+
+int run_sharded_impl(size_t shards, const std::function<int(size_t)> &job) {
+  const DeviceSet &ds = device_set();
+  if (ds.phys.empty()) return fail(ZCRC_ERR_HIP, ds.err);
+  if (shards == 0) return ZCRC_OK;
+  const size_t first = pick_logical();
+  std::vector<int> rcs(shards, ZCRC_OK);
+  std::vector<std::string> errs(shards);
+  ShardWorkers::get().run(shards, [&](size_t g) {
+    const size_t lg = (first + g) % ds.phys.size();
+    LoadMark lm(lg);
+    DeviceGuard dg;
+    int rc = dg.enter(ds.phys[lg]);
+    if (!rc) rc = job(g);
+    rcs[g] = rc;
+    if (rc) errs[g] = t_last_error;
+  });
+  int pos = 0;
+  for (size_t g = 0; g < shards; g++) {
+    if (rcs[g] < 0) return fail(rcs[g], errs[g]);
+    if (rcs[g] > 0 && !pos) pos = rcs[g];
+  }
+  return pos;
+}
+
+// batch_host over the device set: one device (the least loaded) below two
+// shards' worth of bytes, else byte-balanced shards on consecutive logical
+// devices.  kBusy when any shard found no staging slot (wait == false).
+int batch_host_multi(const void *const *ptrs, const size_t *lens, const uint32_t *seeds, uint32_t *out, size_t n,
+                     bool wait) {
+  if (n == 0) return ZCRC_OK;
+  if (!ptrs || !lens || !out) return fail(ZCRC_ERR_ARG, "null argument");
+  const DeviceSet &ds = device_set();
+  if (ds.phys.empty()) return fail(ZCRC_ERR_HIP, ds.err);
+  uint64_t total = 0;
+  for (size_t i = 0; i < n; i++) {
+    if (lens[i] && !ptrs[i]) return fail(ZCRC_ERR_ARG, "null buffer pointer");
+    total += lens[i];
+  }
+  const size_t g_count = shard_count(total, ds.phys.size(), shard_min_bytes());
+  if (g_count == 1)
+    return run_sharded_impl(1, [&](size_t) { return batch_host(ptrs, lens, seeds, out, n, wait); });
+  ShardPlan plan;
+  plan_shards(lens, n, g_count, &plan);
+  struct Part {
+    std::vector<const void *> p;
+    std::vector<size_t> l;
+    std::vector<uint32_t> s, r;
+  };
+  std::vector<Part> parts(g_count);
+  for (size_t g = 0; g < g_count; g++) {
+    Part &P = parts[g];
+    for (const ShardPlan::Piece &pc : plan.shard[g]) {
+      P.p.push_back(static_cast<const uint8_t *>(ptrs[pc.buf]) + pc.off);
+      P.l.push_back(pc.len);
+      P.s.push_back(pc.off == 0 && seeds ? seeds[pc.buf] : 0u);
+    }
+    P.r.assign(P.p.size(), 0u);
+  }
+  const int rc = run_sharded_impl(g_count, [&](size_t g) {
+    Part &P = parts[g];
+    return batch_host(P.p.data(), P.l.data(), P.s.data(), P.r.data(), P.p.size(), wait);
+  });
+  if (rc) return rc;  // kBusy when a shard found no staging slot
+  const XPowTable &xp = host_xpow();
+  for (size_t i = 0; i < n; i++) {
+    const size_t g0 = plan.first[i];
+    uint32_t c = parts[g0].r[plan.item[i]];
+    for (uint32_t e = 1; e <= plan.extra[i]; e++) c = gf2_crc_combine(xp, c, parts[g0 + e].r[0], parts[g0 + e].l[0]);
+    out[i] = c;
+  }
+  return ZCRC_OK;
+}
+
 // ------------------------------------------------------------- streaming
 
 // Stream pieces from a registered segment or a pinned staging region are
@@ -1101,6 +1431,13 @@ static_assert(kStreamRegions == 4, "zcrc32_stream::staged holds one slot's 4 reg
 
 int set_error(int code, const char *msg) { return fail(code, msg); }
 
+size_t host_shards(uint64_t bytes) {
+  const DeviceSet &ds = device_set();
+  return shard_count(bytes, ds.phys.empty() ? 1 : ds.phys.size(), shard_min_bytes());
+}
+
+int run_sharded(size_t shards, const std::function<int(size_t)> &job) { return run_sharded_impl(shards, job); }
+
 }  // namespace zcrc
 
 // A stream object owns a HIP stream, events, a 2-word device CRC cell and a
@@ -1111,6 +1448,7 @@ int set_error(int code, const char *msg) { return fail(code, msg); }
 // returned by final() and close(), so an open but idle stream holds none.
 struct zcrc32_stream {
   int dev = -1;
+  size_t logical = 0;             // its device in the device set (load accounting), while open
   hipStream_t stream = nullptr;
   zcrc::StageSlot *slot = nullptr;
   bool slot_tried = false;        // the pool had no free slot for this entry: pageable copies
@@ -1327,7 +1665,7 @@ int zcrc32_checked(const void *data, size_t n_bytes, uint32_t crc, uint32_t *out
   const void *ptrs[1] = {data};
   const size_t lens[1] = {n_bytes};
   const uint32_t seeds[1] = {crc};
-  return batch_host(ptrs, lens, seeds, out_crc, 1);
+  return batch_host_multi(ptrs, lens, seeds, out_crc, 1, true);
 }
 
 uint32_t zcrc32(const void *data, size_t n_bytes, uint32_t crc) {
@@ -1342,7 +1680,7 @@ uint32_t zcrc32(const void *data, size_t n_bytes, uint32_t crc) {
   const uint32_t seeds[1] = {crc};
   // no waiting for staging under the caller's mutex_fhandle: with every slot
   // of the pool busy, the host CRC answers (counted as a host call)
-  const int rc = batch_host(ptrs, lens, seeds, &r, 1, false);
+  const int rc = batch_host_multi(ptrs, lens, seeds, &r, 1, false);
   if (rc == ZCRC_OK) {
     g_dropin_gpu.fetch_add(1, std::memory_order_relaxed);
     return r;
@@ -1373,7 +1711,7 @@ void zcrc32_dropin_stats(uint64_t *gpu_calls, uint64_t *host_calls, uint64_t *fa
 int zcrc32_batch(const void *const *ptrs, const size_t *lens, const uint32_t *seeds_or_null, uint32_t *out,
                  size_t n, unsigned flags) {
   (void)flags;
-  return batch_host(ptrs, lens, seeds_or_null, out, n);
+  return batch_host_multi(ptrs, lens, seeds_or_null, out, n, true);
 }
 
 size_t zcrc32_batch_device_scratch_bytes(size_t n) {
@@ -1414,8 +1752,10 @@ int zcrc32_batch_device(const void *const *d_ptrs, const uint64_t *d_lens, const
   if (fused_enabled(n, dc->num_cus)) {
     const int rc = stream_scratch(st, kScratchFused, fused_scratch_bytes(), &scratch, &have, &lk);
     if (rc) return rc;
+    note_last_form(st, true);
     return batch_device_fused(d_ptrs, d_lens, d_seeds_or_null, d_out, n, scratch, st);
   }
+  note_last_form(st, false);
   const int rc = stream_scratch(st, kScratchBatch, bytes, &scratch, &have, &lk);
   if (rc) return rc;
   return batch_device_ws(d_ptrs, d_lens, d_seeds_or_null, d_out, n, scratch, have, st);
@@ -1425,14 +1765,14 @@ int zcrc32_batch_device_faults(const void *d_scratch_or_null, void *stream, uint
   if (!faults) return fail(ZCRC_ERR_ARG, "null faults");
   hipStream_t st = static_cast<hipStream_t>(stream);
   const void *sc = d_scratch_or_null;
-  std::unique_lock<std::mutex> lk;
-  if (!sc) {
+  if (!sc && !last_form_fused(st)) {  // (after a one-launch call: no prefix, nothing to report)
     void *p = nullptr;
     size_t have = 0;
+    std::unique_lock<std::mutex> lk;
     const int rc = stream_scratch(st, kScratchBatch, 0, &p, &have, &lk);
     if (rc) return rc;
     sc = p;
-  }
+  }  // the cache lock is released here: the synchronize below must not stall other streams' calls
   ZCRC_HIP_TRY(hipStreamSynchronize(st));
   *faults = 0;
   if (sc) ZCRC_HIP_TRY(hipMemcpy(faults, static_cast<const uint8_t *>(sc) + kFaultByte, 4, hipMemcpyDeviceToHost));
@@ -1547,6 +1887,13 @@ int zcrc_inflate_device(const void *d_src, uint64_t src_len, void *d_dst, uint64
   int rc = device_ctx(&dc);
   if (rc) return rc;
   hipStream_t st = static_cast<hipStream_t>(stream);
+  // the split decode keeps per-stream scratch and sizes its launches on the
+  // host: under graph capture the cached scratch would be frozen into the
+  // graph (replays and later calls sharing it), so refuse
+  hipStreamCaptureStatus capst = hipStreamCaptureStatusNone;
+  ZCRC_HIP_TRY(hipStreamIsCapturing(st, &capst));
+  if (capst != hipStreamCaptureStatusNone)
+    return fail(ZCRC_ERR_ARG, "zcrc_inflate_device cannot be captured into a graph (use zcrc_inflate_batch_device)");
   if (src_len == 0) {  // nothing to read (d_src may be null): input exhausted, as the batch kernel reports
     ZCRC_HIP_TRY(hipMemsetAsync(d_out_len, 0, sizeof(uint64_t), st));
     ZCRC_HIP_TRY(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(d_status), ZCRC_INFLATE_ERR_INPUT, 1, st));
@@ -1601,7 +1948,7 @@ thread_local InflateStage t_inflate;
 constexpr double kSplitCallUs = 6000.0;        // one zcrc_inflate_device call on a text-like entry
 constexpr double kWaveCompressedBps = 8.0e6;   // compressed bytes per second one wave decodes
 constexpr size_t kSplitMaxPerGroup = 64;
-constexpr uint64_t kSplitMaxCap = 1ull << 32;  // split scratch is ~4 x cap of HBM
+constexpr uint64_t kSplitMaxCap = 1ull << 32;  // split scratch is ~6 x cap of HBM + ~288 KiB per item
 constexpr size_t kInflateGroupBytes = 1ull << 30;  // in + out bytes staged per group
 
 // streams [a, b): pack, one H2D, inflate, CRC, one D2H, unpack
@@ -1702,6 +2049,26 @@ int inflate_host_group(const void *const *src, const size_t *src_len, void *cons
   return ZCRC_OK;
 }
 
+// streams [a0, b0) on the current device, in groups of <= kInflateGroupBytes
+int inflate_batch_range(const void *const *src, const size_t *src_len, void *const *dst, const size_t *cap,
+                        size_t *out_len, int32_t *status, uint32_t *crc_or_null, size_t a0, size_t b0) {
+  DeviceCtx *dc = nullptr;
+  int rc = device_ctx(&dc);
+  if (rc) return rc;
+  Lease lease;  // for its HIP stream; the inflate staging is its own
+  rc = lease.take(true, false);
+  if (rc) return rc;
+  StageSlot &slot = *lease.slot[0];
+  for (size_t a = a0; a < b0;) {
+    size_t b = a, bytes = 0;
+    while (b < b0 && (b == a || bytes + src_len[b] + cap[b] <= kInflateGroupBytes)) bytes += src_len[b] + cap[b], b++;
+    rc = inflate_host_group(src, src_len, dst, cap, out_len, status, crc_or_null, a, b, slot.stream);
+    if (rc) return rc;
+    a = b;
+  }
+  return ZCRC_OK;
+}
+
 }  // namespace
 }  // namespace zcrc
 
@@ -1714,31 +2081,43 @@ int zcrc_inflate_batch(const void *const *src, const size_t *src_len, void *cons
     if ((src_len[i] && !src[i]) || (cap[i] && !dst[i])) return fail(ZCRC_ERR_ARG, "null buffer pointer");
     if (src_len[i] >= kInflateMaxSrc) return fail(ZCRC_ERR_TOO_BIG, "compressed stream of 3.75 GiB or more");
   }
-  DeviceCtx *dc = nullptr;
-  int rc = device_ctx(&dc);
-  if (rc) return rc;
-  Lease lease;  // for its HIP stream; the inflate staging is its own
-  rc = lease.take(true, false);
-  if (rc) return rc;
-  StageSlot &slot = *lease.slot[0];
-  for (size_t a = 0; a < n;) {
-    size_t b = a, bytes = 0;
-    while (b < n && (b == a || bytes + src_len[b] + cap[b] <= kInflateGroupBytes)) bytes += src_len[b] + cap[b], b++;
-    rc = inflate_host_group(src, src_len, dst, cap, out_len, status, crc_or_null, a, b, slot.stream);
-    if (rc) return rc;
-    a = b;
+  // over the device set: contiguous runs of streams balanced by compressed
+  // bytes (decode time follows them), one run per device
+  const DeviceSet &ds = device_set();
+  if (ds.phys.empty()) return fail(ZCRC_ERR_HIP, ds.err);
+  uint64_t total = 0;
+  for (size_t i = 0; i < n; i++) total += src_len[i];
+  const size_t g_count = std::min(n, shard_count(total, ds.phys.size(), shard_min_bytes()));
+  std::vector<size_t> cut(g_count + 1, n);
+  cut[0] = 0;
+  uint64_t acc = 0;
+  for (size_t g = 1, i = 0; g < g_count; g++) {
+    const uint64_t want = (uint64_t)((unsigned __int128)total * g / g_count);
+    while (i < n && acc < want) acc += src_len[i++];
+    cut[g] = i;
   }
-  return ZCRC_OK;
+  return run_sharded_impl(g_count, [&](size_t g) {
+    return cut[g] < cut[g + 1] ? inflate_batch_range(src, src_len, dst, cap, out_len, status, crc_or_null, cut[g],
+                                                     cut[g + 1])
+                               : ZCRC_OK;
+  });
 }
 
+// A stream lives on one device of the set: the least loaded one when it is
+// opened (each entry's pieces chain on that device's HIP stream).  Its calls
+// switch to that device and back.
 zcrc32_stream *zcrc32_stream_open(uint32_t seed) {
-  DeviceCtx *dc = nullptr;
-  if (device_ctx(&dc) != ZCRC_OK) return nullptr;
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess) {
-    fail(ZCRC_ERR_HIP, "hipGetDevice failed");
+  const DeviceSet &ds = device_set();
+  if (ds.phys.empty()) {
+    fail(ZCRC_ERR_HIP, ds.err);
     return nullptr;
   }
+  const size_t lg = pick_logical();
+  const int dev = ds.phys[lg];
+  DeviceGuard dg;
+  if (dg.enter(dev) != ZCRC_OK) return nullptr;
+  DeviceCtx *dc = nullptr;
+  if (device_ctx(&dc) != ZCRC_OK) return nullptr;
   zcrc32_stream *s = nullptr;
   {
     std::lock_guard<std::mutex> lk(g_streams_mu);
@@ -1768,6 +2147,8 @@ zcrc32_stream *zcrc32_stream_open(uint32_t seed) {
     t_last_error = err;
     return nullptr;
   }
+  s->logical = lg;
+  ds.load[lg].fetch_add(1, std::memory_order_relaxed);
   return s;
 }
 
@@ -1778,9 +2159,12 @@ zcrc32_stream *zcrc32_stream_open_registered(uint32_t seed, const void *segment,
   }
   zcrc32_stream *s = zcrc32_stream_open(seed);
   if (!s || !segment_bytes) return s;
+  DeviceGuard dg;
+  if (dg.enter(s->dev) != ZCRC_OK) return s;  // works unregistered
   // page-locks the segment (and maps it for the DMA engines) until close();
   // memory someone else registered is used as it is and left registered
-  const hipError_t e = hipHostRegister(const_cast<void *>(segment), segment_bytes, hipHostRegisterMapped);
+  const hipError_t e = hipHostRegister(const_cast<void *>(segment), segment_bytes,
+                                       hipHostRegisterMapped | hipHostRegisterPortable);
   if (e == hipSuccess || e == hipErrorHostMemoryAlreadyRegistered) {
     s->reg_base = static_cast<const uint8_t *>(segment);
     s->reg_size = segment_bytes;
@@ -1797,12 +2181,10 @@ zcrc32_stream *zcrc32_stream_open_registered(uint32_t seed, const void *segment,
 int zcrc32_stream_update(zcrc32_stream *s, const void *data, size_t n_bytes) {
   if (!s) return fail(ZCRC_ERR_ARG, "null stream");
   if (s->err) return fail(s->err, "stream failed earlier: " + s->err_msg);
-  int dev = -1;
+  DeviceGuard dg;
   int rc;
   if (n_bytes && !data) rc = fail(ZCRC_ERR_ARG, "null data");
-  else if (hipGetDevice(&dev) != hipSuccess) rc = fail(ZCRC_ERR_HIP, "hipGetDevice failed");
-  else if (dev != s->dev) rc = fail(ZCRC_ERR_ARG, "stream used on another device");
-  else rc = stream_update(s, static_cast<const uint8_t *>(data), n_bytes);
+  else if ((rc = dg.enter(s->dev)) == ZCRC_OK) rc = stream_update(s, static_cast<const uint8_t *>(data), n_bytes);
   if (rc) {  // sticky: final() must never return the CRC of part of the entry
     s->err = rc;
     s->err_msg = t_last_error;
@@ -1812,6 +2194,8 @@ int zcrc32_stream_update(zcrc32_stream *s, const void *data, size_t n_bytes) {
 
 int zcrc32_stream_final(zcrc32_stream *s, uint32_t *crc) {
   if (!s || !crc) return fail(ZCRC_ERR_ARG, "null argument");
+  DeviceGuard dg;
+  if (const int rc = dg.enter(s->dev)) return rc;
   if (s->err) {
     (void)hipStreamSynchronize(s->stream);
     stream_release_slots(s);
@@ -1827,6 +2211,9 @@ int zcrc32_stream_final(zcrc32_stream *s, uint32_t *crc) {
 
 void zcrc32_stream_close(zcrc32_stream *s) {
   if (!s) return;
+  device_set().load[s->logical].fetch_sub(1, std::memory_order_relaxed);
+  DeviceGuard dg;
+  (void)dg.enter(s->dev);
   if (hipStreamSynchronize(s->stream) != hipSuccess) {  // a broken stream is not reused
     stream_destroy(s);
     return;
@@ -1850,13 +2237,12 @@ int zcrc32_stream_stats(const zcrc32_stream *s, uint64_t *dma_pieces, uint64_t *
   return ZCRC_OK;
 }
 
-int zcrc32_prewarm(size_t staging_slots) {
+namespace zcrc {
+namespace {
+int prewarm_device(int dev, size_t staging_slots) {
   DeviceCtx *dc = nullptr;
   int rc = device_ctx(&dc);
   if (rc) return rc;
-  (void)CopyPool::get();  // its threads start now, not in the first staged call
-  int dev = 0;
-  ZCRC_HIP_TRY(hipGetDevice(&dev));
   size_t have = 0;
   rc = SlotPool::get().prewarm(dev, staging_slots, &have);
   if (rc || !have) return rc;
@@ -1872,6 +2258,26 @@ int zcrc32_prewarm(size_t staging_slots) {
   for (int r = 0; r < 2 && !rc; r++) rc = batch_host(ptrs, lens, nullptr, &crc, 1, true);
   return rc;
 }
+}  // namespace
+}  // namespace zcrc
+
+int zcrc32_prewarm(size_t staging_slots) {
+  const DeviceSet &ds = device_set();
+  if (ds.phys.empty()) return fail(ZCRC_ERR_HIP, ds.err);
+  (void)CopyPool::get();  // its threads start now, not in the first staged call
+  std::vector<int> done;
+  for (const int dev : ds.phys) {  // every GPU of the set once, with slots for each time it is listed
+    if (std::find(done.begin(), done.end(), dev) != done.end()) continue;
+    done.push_back(dev);
+    const size_t times = (size_t)std::count(ds.phys.begin(), ds.phys.end(), dev);
+    DeviceGuard dg;
+    int rc = dg.enter(dev);
+    if (!rc) rc = prewarm_device(dev, staging_slots * times);
+    if (rc) return rc;
+  }
+  return ZCRC_OK;
+}
+
 
 int zcrc_staging_info(uint64_t *pinned_bytes, uint64_t *slots_in_use, uint64_t *slots_peak, uint64_t *slots_budget) {
   SlotPool::get().info(pinned_bytes, slots_in_use, slots_peak, slots_budget);
@@ -1889,6 +2295,33 @@ int zcrc_device_info(int *num_cus, int *arch_major, int *arch_minor) {
   if (num_cus) *num_cus = dc->num_cus;
   if (arch_major) *arch_major = dc->arch_major;
   if (arch_minor) *arch_minor = dc->arch_minor;
+  return ZCRC_OK;
+}
+
+int zcrc_device_set(int *devices, size_t capacity, size_t *n) {
+  if (!n) return fail(ZCRC_ERR_ARG, "null n");
+  const DeviceSet &ds = device_set();
+  *n = ds.phys.size();
+  if (ds.phys.empty()) return fail(ZCRC_ERR_HIP, ds.err);
+  for (size_t k = 0; k < ds.phys.size() && k < capacity && devices; k++) devices[k] = ds.phys[k];
+  return ZCRC_OK;
+}
+
+int zcrc_shard_plan(const size_t *lens, size_t n, size_t shards, uint32_t *first, uint32_t *pieces,
+                    uint64_t *shard_bytes) {
+  if ((n && !lens) || shards == 0) return fail(ZCRC_ERR_ARG, "null lens or zero shards");
+  ShardPlan p;
+  plan_shards(lens, n, shards, &p);
+  for (size_t i = 0; i < n; i++) {
+    if (first) first[i] = p.first[i];
+    if (pieces) pieces[i] = 1 + p.extra[i];
+  }
+  if (shard_bytes)
+    for (size_t g = 0; g < shards; g++) {
+      uint64_t b = 0;
+      for (const ShardPlan::Piece &pc : p.shard[g]) b += pc.len;
+      shard_bytes[g] = b;
+    }
   return ZCRC_OK;
 }
 

@@ -22,10 +22,13 @@
 #include <stdint.h>
 #include <string.h>
 
+#include <algorithm>
 #include <vector>
 
 #include "../../include/zcrc.h"
 #include "zcrc_internal.h"
+#include "zcrc_inflate_internal.h"
+#include "zcrc_runtime.h"
 
 namespace {
 
@@ -407,19 +410,79 @@ extern "C" int zcrc_zip_verify_device(const void *d_archive, size_t archive_len,
   return ZCRC_OK;
 }
 
-extern "C" int zcrc_zip_verify_host(const void *archive, size_t archive_len, zcrc_zip_entry *entries, size_t n) {
-  if (!archive || (n && !entries)) return zfail("null argument");
-  // stage the image once and verify it where the GPU reads it
+namespace {
+
+// One device's share of zcrc_zip_verify_host: the sub-image [lo, hi) holding
+// the data of entries idx[a, b) is staged into HBM once and verified there
+// (offsets rebased to the sub-image).
+int verify_host_run(const uint8_t *archive, zcrc_zip_entry *entries, const std::vector<size_t> &idx, size_t a,
+                    size_t b) {
+  if (a == b) return ZCRC_OK;
+  uint64_t lo = UINT64_MAX, hi = 0;
+  for (size_t k = a; k < b; k++) {
+    const zcrc_zip_entry &E = entries[idx[k]];
+    lo = std::min<uint64_t>(lo, E.data_offset);
+    hi = std::max<uint64_t>(hi, E.data_offset + E.comp_size);
+  }
+  std::vector<zcrc_zip_entry> local(b - a);
+  for (size_t k = a; k < b; k++) {
+    local[k - a] = entries[idx[k]];
+    local[k - a].data_offset -= lo;
+  }
   hipStream_t st = nullptr;
   if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess) return zfail("stream create failed");
+  const uint64_t len = hi - lo;
   void *d = nullptr;
   int rc = ZCRC_OK;
-  if (hipMallocAsync(&d, archive_len ? archive_len : 1, st) != hipSuccess) rc = zfail("archive allocation failed");
-  if (!rc && archive_len && hipMemcpyAsync(d, archive, archive_len, hipMemcpyHostToDevice, st) != hipSuccess)
+  if (hipMallocAsync(&d, len ? len : 1, st) != hipSuccess) rc = zfail("archive allocation failed");
+  if (!rc && len && hipMemcpyAsync(d, archive + lo, len, hipMemcpyHostToDevice, st) != hipSuccess)
     rc = zfail("archive upload failed");
-  if (!rc) rc = zcrc_zip_verify_device(d, archive_len, entries, n, st);
+  if (!rc) rc = zcrc_zip_verify_device(d, len, local.data(), local.size(), st);
   if (d) (void)hipFreeAsync(d, st);
   (void)hipStreamSynchronize(st);
   (void)hipStreamDestroy(st);
-  return rc;
+  if (rc) return rc;
+  for (size_t k = a; k < b; k++) {
+    zcrc_zip_entry &E = entries[idx[k]];
+    E.status = local[k - a].status;
+    E.crc_computed = local[k - a].crc_computed;
+    E.inflate_status = local[k - a].inflate_status;
+  }
+  return ZCRC_OK;
+}
+
+}  // namespace
+
+// Over the device set (zcrc_runtime.h): the entries, in archive order, are cut
+// into runs of about equal data bytes, one per device, and each device
+// stages only its run's part of the image -- a ZIP's entry data is laid out
+// in order, so the parts barely overlap and the image crosses PCIe about once
+// in all.
+extern "C" int zcrc_zip_verify_host(const void *archive, size_t archive_len, zcrc_zip_entry *entries, size_t n) {
+  if (!archive || (n && !entries)) return zfail("null argument");
+  std::vector<size_t> idx;
+  uint64_t total = 0;
+  for (size_t i = 0; i < n; i++) {
+    zcrc_zip_entry &E = entries[i];
+    if (E.status == ZCRC_ZIP_BAD) continue;
+    if (E.data_offset > archive_len || E.comp_size > archive_len - E.data_offset) {
+      E.status = ZCRC_ZIP_UNVERIFIED;  // as zcrc_zip_verify_device leaves it
+      continue;
+    }
+    idx.push_back(i);
+    total += E.comp_size;
+  }
+  std::stable_sort(idx.begin(), idx.end(),
+                   [&](size_t x, size_t y) { return entries[x].data_offset < entries[y].data_offset; });
+  const size_t shards = std::max<size_t>(1, std::min(idx.size(), zcrc::host_shards(total)));
+  std::vector<size_t> cut(shards + 1, idx.size());
+  cut[0] = 0;
+  uint64_t acc = 0;
+  for (size_t g = 1, k = 0; g < shards; g++) {
+    const uint64_t want = (uint64_t)((unsigned __int128)total * g / shards);
+    while (k < idx.size() && acc < want) acc += entries[idx[k++]].comp_size;
+    cut[g] = k;
+  }
+  const uint8_t *a = static_cast<const uint8_t *>(archive);
+  return zcrc::run_sharded(shards, [&](size_t g) { return verify_host_run(a, entries, idx, cut[g], cut[g + 1]); });
 }
