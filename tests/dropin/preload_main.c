@@ -25,6 +25,19 @@
  *           registration, close_us the unregistration): the chunks are DMA'd
  *           from it, update() copies nothing
  *   none    the loop with no CRC at all (its loop_ms is the baseline)
+ *
+ * Deflated entries (ZCRC_PRELOAD_DEFLATED=<uncompressed size> in the
+ * environment; the entry file then holds the entry's raw DEFLATE data, as
+ * libzip reads it after the local header).  ZIPsFS inflates with
+ * zip_fread() (src/ZIPsFS.c:2016-2019: libzip over zlib) in the same 16 MiB
+ * pieces and checks the CRC after the loop; the compressed bytes are read
+ * into memory first in every mode (libzip's own reads).  Modes:
+ *   zlib_ref     zlib raw inflate in 16 MiB output pieces, then the
+ *                reference's cg_crc32 (-O0) under the lock (what ZIPsFS does)
+ *   zlib_dropin  the same loop, then the drop-in cg_crc32 under the lock
+ *   gpu_inflate  one zcrc_inflate_batch call: inflate + CRC on the GPU, the
+ *                bytes copied into the segment; under the lock only the
+ *                compare of the CRC it returned
  * Usage: preload_main <entry file> <expected crc hex> <reps> mode...
  * Output: one JSON line per mode with the median over reps.
  */
@@ -39,6 +52,7 @@
 #include <sys/stat.h>
 #include <time.h>
 #include <unistd.h>
+#include <zlib.h>
 
 #define PRELOADRAM_READ_BYTES_NUM (16L << 20)
 #define THRESHOLD_MALLOC_MMAP (128L << 10)
@@ -69,6 +83,76 @@ typedef struct {
   uint32_t crc;
   double loop_ms, hold_us, open_us, close_us;
 } result_t;
+
+/* a deflated entry (ZCRC_PRELOAD_DEFLATED): mode 5 zlib_ref, 6 zlib_dropin,
+ * 7 gpu_inflate.  st_size = the uncompressed size (central directory). */
+static int preload_deflated_once(const char *path, off_t st_size, int mode, ref_fn ref, result_t *r) {
+  const int fd = open(path, O_RDONLY);
+  if (fd < 0) return -1;
+  struct stat st;
+  if (fstat(fd, &st)) return -1;
+  const size_t clen = (size_t)st.st_size;
+  const int use_mmap = st_size > THRESHOLD_MALLOC_MMAP;
+  char *dst = use_mmap ? mmap(NULL, st_size ? st_size : 1, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0)
+                       : malloc(st_size ? st_size : 1);
+  if (!dst || dst == MAP_FAILED) return -1;
+  r->open_us = r->close_us = 0;
+  const double t0 = now_us();
+  unsigned char *comp = malloc(clen ? clen : 1);
+  if (!comp) return -1;
+  for (size_t got = 0; got < clen;) {  /* the compressed bytes, as libzip reads them */
+    const ssize_t n = read(fd, comp + got, clen - got);
+    if (n <= 0) return -1;
+    got += (size_t)n;
+  }
+  off_t already = 0;
+  uint32_t gpu_crc = 0;
+  if (mode == 5 || mode == 6) {
+    z_stream zs;
+    memset(&zs, 0, sizeof zs);
+    if (inflateInit2(&zs, -15) != Z_OK) return -1;
+    zs.next_in = comp;
+    zs.avail_in = (uInt)clen;
+    int zr = Z_OK;
+    while (st_size > already && zr != Z_STREAM_END) {  /* zip_fread(zf, dst + already, n_max) (:288) */
+      const off_t n_max = st_size - already < PRELOADRAM_READ_BYTES_NUM ? st_size - already : PRELOADRAM_READ_BYTES_NUM;
+      zs.next_out = (unsigned char *)dst + already;
+      zs.avail_out = (uInt)n_max;
+      while (zs.avail_out && zr == Z_OK) zr = inflate(&zs, Z_NO_FLUSH);
+      if (zr != Z_OK && zr != Z_STREAM_END) return -1;
+      pthread_mutex_lock(&mutex_fhandle);
+      already += n_max - (off_t)zs.avail_out;
+      pthread_mutex_unlock(&mutex_fhandle);
+    }
+    inflateEnd(&zs);
+  } else {
+    const void *src[1] = {comp};
+    const size_t src_len[1] = {clen}, cap[1] = {(size_t)st_size};
+    void *dsts[1] = {dst};
+    size_t out_len[1] = {0};
+    int32_t status[1] = {-1};
+    if (zcrc_inflate_batch(src, src_len, dsts, cap, out_len, status, &gpu_crc, 1, 0) || status[0] != 0) return -1;
+    pthread_mutex_lock(&mutex_fhandle);
+    already = (off_t)out_len[0];
+    pthread_mutex_unlock(&mutex_fhandle);
+  }
+  r->loop_ms = (now_us() - t0) * 1e-3;
+  free(comp);
+  if (already != st_size) return -1;
+  pthread_mutex_lock(&mutex_fhandle); /* LOCK(mutex_fhandle, ok_crc=fhandle_check_crc32(d)) (:313) */
+  const double h = now_us();
+  uint32_t crc = 0;
+  if (mode == 5) crc = ref(dst, st_size, 0);
+  if (mode == 6) crc = cg_crc32(dst, st_size, 0, &mutex_crc);
+  if (mode == 7) crc = gpu_crc;
+  r->hold_us = now_us() - h;
+  pthread_mutex_unlock(&mutex_fhandle);
+  r->crc = crc;
+  if (!use_mmap) free(dst);
+  else munmap(dst, st_size ? st_size : 1);
+  close(fd);
+  return 0;
+}
 
 /* one preload of the entry; mode: 0 dropin, 1 stream, 2 ref, 3 stream_reg, 4 none */
 static int preload_once(const char *path, int mode, ref_fn ref, result_t *r) {
@@ -142,23 +226,28 @@ int main(int argc, char **argv) {
    * init and staging slots, which the drop-in never creates under
    * mutex_fhandle; without a GPU it fails and the drop-in answers on the host */
   (void)zcrc32_prewarm(2);
+  const char *defl = getenv("ZCRC_PRELOAD_DEFLATED");
+  const off_t usize = defl ? (off_t)strtoll(defl, NULL, 10) : -1;
   int bad = 0;
   for (int a = 4; a < argc; a++) {
     const char *m = argv[a];
-    const int mode = !strcmp(m, "dropin")       ? 0
-                     : !strcmp(m, "stream")     ? 1
-                     : !strcmp(m, "ref")        ? 2
-                     : !strcmp(m, "stream_reg") ? 3
-                     : !strcmp(m, "none")       ? 4
-                                                : -1;
-    if (mode < 0) return 2;
+    const int mode = !strcmp(m, "dropin")        ? 0
+                     : !strcmp(m, "stream")      ? 1
+                     : !strcmp(m, "ref")         ? 2
+                     : !strcmp(m, "stream_reg")  ? 3
+                     : !strcmp(m, "none")        ? 4
+                     : !strcmp(m, "zlib_ref")    ? 5
+                     : !strcmp(m, "zlib_dropin") ? 6
+                     : !strcmp(m, "gpu_inflate") ? 7
+                                                 : -1;
+    if (mode < 0 || (mode >= 5) != (usize >= 0)) return 2;  /* deflated modes need ZCRC_PRELOAD_DEFLATED */
     ref_fn ref = NULL;
-    if (mode == 2) {
+    if (mode == 2 || mode == 5) {
       const char *lib = getenv("ZCRC_REF_LIB");
       void *h = lib ? dlopen(lib, RTLD_NOW | RTLD_LOCAL) : NULL;
       ref = h ? (ref_fn)dlsym(h, "ref_cg_crc32") : NULL;
       if (!ref) {
-        printf("{\"mode\": \"ref\", \"skipped\": \"ZCRC_REF_LIB not loadable\"}\n");
+        printf("{\"mode\": \"%s\", \"skipped\": \"ZCRC_REF_LIB not loadable\"}\n", m);
         continue;
       }
     }
@@ -166,9 +255,8 @@ int main(int argc, char **argv) {
     uint32_t crc = 0;
     int ok = 1;
     for (int k = 0; k < reps; k++) {
-      result_t r;
-      r.crc = expected;
-      if (preload_once(path, mode, ref, &r)) {
+      result_t r = {expected, 0, 0, 0, 0};
+      if (mode >= 5 ? preload_deflated_once(path, usize, mode, ref, &r) : preload_once(path, mode, ref, &r)) {
         fprintf(stderr, "%s: preload failed (%s)\n", argv[a], zcrc_last_error());
         return 1;
       }

@@ -86,7 +86,7 @@ def build_preload_harness(tmp_path) -> str:
     cmd = ["gcc", "-O1", "-Wall", "-Werror", "-I", os.path.join(ROOT, "zipsfs_amd"), "-I",
            os.path.join(ROOT, "include"), os.path.join(HERE, "dropin", "preload_main.c"), "-o", exe,
            "-L", os.path.join(ROOT, "zipsfs_amd"), "-lzcrc", "-Wl,-rpath," + os.path.join(ROOT, "zipsfs_amd"),
-           "-pthread", "-ldl"]
+           "-pthread", "-ldl", "-lz"]
     subprocess.run(cmd, check=True)
     return exe
 

@@ -394,11 +394,13 @@ def crc_small_group(mem: np.ndarray, pstart: int, length: int, seed: int, G: int
 K_SMALL_MAX = 8192
 K_SIZE_CLASSES = K_SMALL_MAX // 256 + 1
 K_SMALL_COST = 14  # zcrc_internal.h kSmallCostDefault (quarters of a batch-kernel byte)
+K_BIG_MIN = 1 << 20  # zcrc_internal.h kBigMin
 
 
 def split_plan(lens, grid: int = 256, force: bool = False, small_cost: int = K_SMALL_COST):
     """zcrc_kernels.hip plan_split_scatter's decisions and lists: (split,
-    large list in order with its prefix, small list tile by tile (8192
+    large list -- on a split, buffers below kBigMin first, then the others,
+    each in index order -- with its prefix, small list tile by tile (8192
     buffers), by size class within a tile and in index order within a class,
     small workgroups, small lanes)."""
     lens = [int(x) for x in lens]
@@ -417,6 +419,8 @@ def split_plan(lens, grid: int = 256, force: bool = False, small_cost: int = K_S
         return dict(split=False, large=list(range(len(lens))), small=[], wgs=wgs, lanes=16)
     by_class = sorted(small, key=lambda i: (i // 8192, (lens[i] + 255) >> 8, i))
     lanes = 8 if as_ <= 2048 * len(small) else 16
+    # round 4: the batch kernel's buffers medium first, then big (>= kBigMin), each in index order
+    large = [i for i in large if lens[i] < K_BIG_MIN] + [i for i in large if lens[i] >= K_BIG_MIN]
     return dict(split=True, large=large, small=by_class, wgs=wgs, lanes=lanes)
 
 
@@ -463,6 +467,32 @@ def braid_lds_built() -> np.ndarray:
                 c = t + 1024 * k
                 lds[4 * c:4 * c + 4] = e[src]
     return lds
+
+
+def comb_lds_built() -> np.ndarray:
+    """The round-4 per-buffer mode's combine area (zcrc_batch_kernel.h,
+    comb_gen): thread (w, l) writes chunk 64 w + l of tables 0..3 and chunk
+    1024 + 64 w + l of tables 4..7; chunk t holds table c = t >> 8, row j =
+    (t >> 6) & 3, entries v = 4 (t & 63) + e, e < 4, each the xor of the
+    products q_c[8 j + b] = x^(-8 * 4 * 2^c) * (1 << (8 j + b)) over v's set bits
+    (bits 2..7 from the lane, shared by its four entries)."""
+    area = np.zeros(8192, dtype=np.uint32)
+    for c in range(8):
+        q = [gf2_mul(xinvpow8(4 << c), 1 << p) for p in range(32)]
+        for w in range(16):
+            if (w >> 2) != (c & 3):
+                continue
+            j = w & 3
+            for l in range(64):
+                t = (1024 if c >= 4 else 0) + 64 * w + l
+                assert t >> 8 == c and (t >> 6) & 3 == j
+                base = 0
+                for i in range(6):
+                    if (l >> i) & 1:
+                        base ^= q[8 * j + 2 + i]
+                words = [base, base ^ q[8 * j], base ^ q[8 * j + 1], base ^ q[8 * j] ^ q[8 * j + 1]]
+                area[4 * t:4 * t + 4] = words
+    return area
 
 
 def per_buffer_plan(lens, num_cus: int = 256):

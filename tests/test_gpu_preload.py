@@ -46,3 +46,33 @@ def test_preload_loop_modes(tmp_path, size):
     if out:
         with open(out, "a") as f:
             f.write(json.dumps(line) + "\n")
+
+
+@pytest.mark.parametrize("kind,size", [("text", 1 << 20), ("spectrum", 1 << 20), ("text", 16 << 20),
+                                       ("spectrum", 16 << 20)])
+def test_preload_deflated_entry_modes(tmp_path, kind, size):
+    """A deflated entry through the same loop: zlib raw
+    inflate in 16 MiB pieces + the reference cg_crc32 (-O0) -- what ZIPsFS
+    does through zip_fread -- against the drop-in after the same loop and one
+    zcrc_inflate_batch call (inflate + CRC on the GPU).  Every mode must give
+    the entry's CRC; timings go to $ZCRC_PRELOAD_TABLE."""
+    import zlib
+    import inflate_streams as S
+    exe = du.build_preload_harness(tmp_path)
+    data = S.PAYLOADS[kind](size, 17)
+    path = tmp_path / "entry.deflate"
+    path.write_bytes(S.deflate(data, 6))
+    exp = zlib.crc32(data)
+    modes = ["zlib_dropin", "gpu_inflate"] + (["zlib_ref"] if os.path.exists(du.REF_O0) else [])
+    rc, rows, stats, err = du.run_preload(exe, path, exp, 3, modes, {"ZCRC_PRELOAD_DEFLATED": str(len(data))})
+    assert rc == 0, err
+    for m, r in rows.items():
+        if "skipped" not in r:
+            assert r["ok"] and int(r["crc"], 16) == exp, (m, r)
+    assert {"zlib_dropin", "gpu_inflate"} <= set(rows)
+    line = {"size": size, "kind": kind, "deflated": True, "rows": rows}
+    print(json.dumps(line))
+    out = os.environ.get("ZCRC_PRELOAD_TABLE")
+    if out:
+        with open(out, "a") as f:
+            f.write(json.dumps(line) + "\n")

@@ -291,8 +291,8 @@ def _split_lists(scratch, n):
     T = -(-n // 8192)
     prefix = 256
     tiles = prefix + 8 * (n + 1)
-    tile_pre = tiles + 24 * T
-    ptrs = tile_pre + 24 * (T + 1)
+    tile_pre = tiles + 40 * T  # kTileWords = 5
+    ptrs = tile_pre + 40 * (T + 1)
     seeds = ptrs + 8 * n
     oidx = seeds + 4 * n
     sdesc = (oidx + 4 * n + 15) // 16 * 16
@@ -302,7 +302,7 @@ def _split_lists(scratch, n):
 
 
 @pytest.mark.parametrize("n,shape", [(20_000, "mixed"), (50_000, "all_small"), (4_200_000, "mixed"),
-                                     (4_300_000, "all_small")])
+                                     (4_300_000, "all_small"), (20_000, "mixed_big"), (60_000, "mixed_big")])
 def test_split_plan_lists_equal_the_model(n, shape):
     """The plan's decision, the compacted batch (order and byte prefix) and the
     small list (tile by tile, by size class, index order within a class) equal
@@ -313,8 +313,13 @@ def test_split_plan_lists_equal_the_model(n, shape):
     top = SMALL_MAX + 1 if n < 1_000_000 else 600  # keep the 4M-buffer batches near 1 GiB
     if shape == "all_small":
         lens = rng.integers(0, min(top, 700), n)
-    else:  # ZIP-entry-like: most small, some large
+    elif shape == "mixed":  # ZIP-entry-like: most small, some large
         lens = np.where(rng.random(n) < 0.995, rng.integers(0, top, n), rng.integers(SMALL_MAX + 1, 40_000, n))
+    else:  # mixed_big: medium and big (>= 1 MiB, kBigMin) batch-kernel buffers interleaved (round-4 order)
+        u = rng.random(n)
+        lens = np.where(u < 0.99, rng.integers(0, top, n),
+                        np.where(u < 0.995, rng.integers(SMALL_MAX + 1, 1 << 20, n), rng.integers(1 << 20, 3 << 20, n)))
+        lens[:3] = [1 << 20, (1 << 20) - 1, SMALL_MAX + 1]  # the class edges
     lens = lens.astype(np.int64)
     offs = np.zeros(n, dtype=np.int64)
     offs[1:] = np.cumsum(lens + 3)[:-1]

@@ -175,7 +175,8 @@ def test_small_group_model_matches_oracle(G):
 
 
 def test_split_plan_model_lists():
-    """The split plan's lists: the large buffers keep their order, the small
+    """The split plan's lists: the batch kernel's buffers below 1 MiB first,
+    then the others, each class in index order (round 4); the small
     list holds every buffer <= 8 KiB once, ordered by 256-B block count within
     each 8192-buffer tile (index order within a class); the split rule and the
     workgroup share follow zcrc_kernels.hip."""
@@ -186,7 +187,10 @@ def test_split_plan_model_lists():
     p = km.split_plan(lens)
     assert p["split"] and 1 <= p["wgs"] <= 255
     assert sorted(p["large"] + p["small"]) == list(range(len(lens)))
-    assert p["large"] == sorted(p["large"]) and all(lens[i] > 8192 for i in p["large"])
+    assert all(lens[i] > 8192 for i in p["large"])
+    med = [i for i in p["large"] if lens[i] < (1 << 20)]
+    assert med == sorted(med) and p["large"] == med + sorted(set(p["large"]) - set(med))
+    assert 0 < len(med) < len(p["large"])
     key = [(i // 8192, (int(lens[i]) + 255) >> 8, i) for i in p["small"]]
     assert key == sorted(key)
     # all large: nothing to split; all small: every workgroup takes the small list
@@ -223,8 +227,17 @@ def test_per_buffer_braid_build_equals_loaded_fill():
     assert np.array_equal(km.braid_lds_built(), km.braid_lds_loaded())
 
 
+def test_per_buffer_comb_build_equals_table_blob():
+    """Round 4: the per-buffer mode also builds the 8 combine tables in
+    registers (comb_gen); the 8,192-word combine area must equal
+    TableBlob::comb as the other forms load it."""
+    T = km.tables()
+    comb = np.concatenate([t.reshape(-1) for t in T.comb])
+    assert np.array_equal(km.comb_lds_built(), comb)
+
+
 def test_per_buffer_flags_sit_on_zero_combine_words():
-    """The per-buffer mode stores wave s's decision flag in the combine-area
+    """The round-3 per-buffer form (kPB = 3, kept for A/B in tools/) stores wave s's decision flag in the combine-area
     word 256 s: the first word of the chunk lane 0 of wave s writes (chunk
     64 s = table s >> 2, sub-table j = s & 3, v = 0), which is MCT(c)[j][0] =
     0 in every table -- so an all-clear decision leaves the tables exact."""

@@ -14,7 +14,10 @@
 //                starts at a hashed block of its buffer and wraps; -np:
 //                no slot priorities
 //   crc          the product kernel (prefix precomputed: the plan's output)
-//   crc-fused    the one-launch kernel (scans the lengths itself)
+//   crc-fused    the one-launch kernel (per-buffer mode, round-4 form: tables
+//                built in registers, the batch decided after the work)
+//   crc-fused-r3 the same kernel with the round-3 per-buffer form (tables and
+//                lengths in front of its one barrier), for A/B
 // and one stamped launch of each CRC form (s_memrealtime, 100 MHz) printed
 // as a timeline: kernel entry, range search done, LDS fill + barrier done,
 // wave end -- percentiles over all waves, relative to the first entry.  The
@@ -180,8 +183,9 @@ int main(int argc, char **argv) {
   };
   std::vector<hipEvent_t> ev(2 * kBatches);
   for (auto &e : ev) CHECK(hipEventCreate(&e));
-  enum { kProbeWave, kProbeGrid, kCrc, kCrcFused, kProbePb, kProbePbRot, kProbePbNoPrio, kNumV };
-  const char *names[kNumV] = {"probe-wave", "probe-grid", "crc", "crc-fused", "probe-pb", "probe-pb-rot", "probe-pb-np"};
+  enum { kProbeWave, kProbeGrid, kCrc, kCrcFused, kCrcFusedR3, kProbePb, kProbePbRot, kProbePbNoPrio, kNumV };
+  const char *names[kNumV] = {"probe-wave", "probe-grid", "crc", "crc-fused", "crc-fused-r3", "probe-pb", "probe-pb-rot",
+                              "probe-pb-np"};
   auto launch = [&](int v, int b, hipEvent_t e0, hipEvent_t e1) {
     const uint8_t *base = data + b * kBatchBytes;
     switch (v) {
@@ -208,6 +212,10 @@ int main(int argc, char **argv) {
         hipExtLaunchKernelGGL((crc32_batch_kernel<false, kDepth, 0, true, false, 1, kLoadNt, true>), dim3(cus),
                               dim3(kThreads), 0, 0, e0, e1, 0, crc_args(b, true));
         break;
+      case kCrcFusedR3:
+        hipExtLaunchKernelGGL((crc32_batch_kernel<false, kDepth, 0, true, false, 1, kLoadNt, true, kWindowed, 3>),
+                              dim3(cus), dim3(kThreads), 0, 0, e0, e1, 0, crc_args(b, true));
+        break;
     }
     CHECK(hipGetLastError());
   };
@@ -230,7 +238,10 @@ int main(int argc, char **argv) {
   CHECK(hipMemcpy(o1.data(), out, 4 * kN, hipMemcpyDeviceToHost));
   launch(kCrcFused, 0, nullptr, nullptr);
   CHECK(hipMemcpy(o2.data(), out, 4 * kN, hipMemcpyDeviceToHost));
-  const bool eq = o1 == o2;
+  std::vector<uint32_t> o3(kN);
+  launch(kCrcFusedR3, 0, nullptr, nullptr);
+  CHECK(hipMemcpy(o3.data(), out, 4 * kN, hipMemcpyDeviceToHost));
+  const bool eq = o1 == o2 && o1 == o3;
   printf("c2_probe: %d CUs, 16 x 256 MiB batches rotated, %d reps; crc forms %s\n", cus, reps,
          eq ? "equal" : "DIFFER");
   for (int v = 0; v < kNumV; v++) {
@@ -239,11 +250,14 @@ int main(int argc, char **argv) {
            kBatchBytes / (avg * 1e-3) / 1e9);
   }
   // stamped timelines (one cold batch each)
-  auto timeline = [&](const char *name, bool fused, int b) {
+  auto timeline = [&](const char *name, bool fused, int b, int pb = 4) {
     BatchArgs a = crc_args(b, fused);
     a.stamps = stamps;
     CHECK(hipMemset(stamps, 0, 64 * (uint64_t)cus * kWaves));
-    if (fused)
+    if (fused && pb == 3)
+      hipExtLaunchKernelGGL((crc32_batch_kernel<false, kDepth, 0, true, true, 1, kLoadNt, true, kWindowed, 3>),
+                            dim3(cus), dim3(kThreads), 0, 0, ev[0], ev[1], 0, a);
+    else if (fused)
       hipExtLaunchKernelGGL((crc32_batch_kernel<false, kDepth, 0, true, true, 1, kLoadNt, true>), dim3(cus),
                             dim3(kThreads), 0, 0, ev[0], ev[1], 0, a);
     else
@@ -274,8 +288,9 @@ int main(int argc, char **argv) {
       printf("  %-7s %6.2f %6.2f %6.2f\n", k, pct(v, 0), pct(v, .5), pct(v, 1));
     };
     row("entry", entry);
-    if (fused) {  // per-buffer mode (round 3): tables built and batch decided at its one barrier
-      if (!lens.empty()) row("lengths", lens);
+    if (fused) {  // per-buffer mode: round 3 -- lengths in, tables built and batch decided at its one barrier;
+                  // round 4 -- tables written (the barrier waits for them alone)
+      if (!lens.empty()) row(pb == 3 ? "lengths" : "tables", lens);
       row("begin", begin);
       row("end", end);
     } else {
@@ -289,5 +304,6 @@ int main(int argc, char **argv) {
   };
   timeline("crc", false, 3);
   timeline("crc-fused", true, 5);
+  timeline("crc-fused-r3", true, 7, 3);
   return 0;
 }

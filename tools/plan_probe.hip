@@ -74,6 +74,7 @@ int main(int argc, char **argv) {
   p.ctr = reinterpret_cast<uint32_t *>(scratch);
   p.grid = (uint32_t)cus;
   p.small_cost = kSmallCostDefault;
+  p.big_min = kBigMin;
   for (int r = 0; r < 5; r++) CK(launch_plan_split(p, 0));
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0));

@@ -101,6 +101,47 @@ __device__ __forceinline__ uint32_t braid_gen_lane(uint32_t lane, uint32_t w) {
          braid_gen_bit<6>(j1, j2, v) ^ braid_gen_bit<7>(j1, j2, v);
 }
 
+// The combine tables (TableBlob::comb: MCT(x^-32 .. x^-4096)) built in
+// registers the same way, for the per-buffer mode (round 4): nothing in
+// front of its first barrier then waits on memory.  Chunk t of the combine
+// area holds table c = t >> 8 (c = 0..7: x^(-8 * 4 * 2^c)), row j = (t >> 6)
+// & 3, entries v = 4 (t & 63) + 0..3; for thread t's two chunks (t and t +
+// 1024) c and j are wave-uniform, so every product is an immediate and a
+// lane's four entries share the xor over v's bits 2..7 (its lane bits).
+template <int kBytes, int p>
+struct MctInvQ {
+  static constexpr uint32_t value = MctBasisInv<kBytes>{}.q[p];
+};
+template <int kBytes, int P>
+__device__ __forceinline__ uint32_t qsel(uint32_t lane, int bit) {
+  return ((lane >> bit) & 1u) ? MctInvQ<kBytes, P>::value : 0u;
+}
+template <int kBytes, int J>
+__device__ __forceinline__ uint4 comb_chunk_gen(uint32_t lane) {
+  const uint32_t base = qsel<kBytes, 8 * J + 2>(lane, 0) ^ qsel<kBytes, 8 * J + 3>(lane, 1) ^
+                        qsel<kBytes, 8 * J + 4>(lane, 2) ^ qsel<kBytes, 8 * J + 5>(lane, 3) ^
+                        qsel<kBytes, 8 * J + 6>(lane, 4) ^ qsel<kBytes, 8 * J + 7>(lane, 5);
+  const uint32_t q0 = MctInvQ<kBytes, 8 * J>::value, q1 = MctInvQ<kBytes, 8 * J + 1>::value;
+  return make_uint4(base, base ^ q0, base ^ q1, base ^ q0 ^ q1);
+}
+// chunks w * 64 + lane (tables 0..3) and 1024 + w * 64 + lane (tables 4..7)
+// of wave w (wave-uniform)
+__device__ __forceinline__ void comb_gen(uint32_t w, uint32_t lane, uint4 &c0, uint4 &c1) {
+  switch (w) {
+#define ZCRC_COMB_W(W)                                                   \
+  case W:                                                                \
+    c0 = comb_chunk_gen<(4 << ((W) >> 2)), (W) & 3>(lane);               \
+    c1 = comb_chunk_gen<(64 << ((W) >> 2)), (W) & 3>(lane);              \
+    break;
+    ZCRC_COMB_W(0) ZCRC_COMB_W(1) ZCRC_COMB_W(2) ZCRC_COMB_W(3) ZCRC_COMB_W(4) ZCRC_COMB_W(5) ZCRC_COMB_W(6)
+    ZCRC_COMB_W(7) ZCRC_COMB_W(8) ZCRC_COMB_W(9) ZCRC_COMB_W(10) ZCRC_COMB_W(11) ZCRC_COMB_W(12)
+    ZCRC_COMB_W(13) ZCRC_COMB_W(14) ZCRC_COMB_W(15)
+#undef ZCRC_COMB_W
+    default:
+      c0 = c1 = make_uint4(0, 0, 0, 0);
+  }
+}
+
 // Lane i gets lane i + d's value, d < 16, inside its 16-lane row (DPP
 // row_shl; lanes past the row end get 0).  The folds below only read it in
 // lanes whose source is in the same row, where it equals __shfl_down(x, d) --
@@ -490,7 +531,8 @@ template <bool kStrided, uint32_t kD, int kAblate, bool kRotate, int kPrio = 0, 
 __device__ __forceinline__ uint64_t process_range(const BatchArgs &args, const BatchView<kStrided> &bv,
                                                   const uint32_t *s_lds, const TableBlob *tab, uint64_t S0,
                                                   uint64_t S1, bool last_wave, uint32_t salt, uint32_t lane,
-                                                  bool band, uint64_t first0, uint64_t lb1, uint64_t *t_tail = nullptr) {
+                                                  bool band, uint64_t first0, uint64_t lb1, uint64_t *t_tail = nullptr,
+                                                  bool skip_small = false) {
   // Buffers [i_first, i_end) overlap this wave's range [S0, S1).
   // first0: the first buffer overlapping it, lb1 = lower_bound(S1) (BatchView::range)
   const uint64_t i_first = uni64(first0);
@@ -520,7 +562,12 @@ __device__ __forceinline__ uint64_t process_range(const BatchArgs &args, const B
       if (i >= i_end) i -= npieces;
       i = uni64(i);
       b0 = uni64(bv.prefix(i)), b1 = uni64(bv.prefix(i + 1));
+      if (skip_small) blen = uni64(args.lens[i]);
     }
+    // skip_small (the per-buffer mode's fall-back): buffers of at most
+    // kPerBufMax bytes were checksummed by their own wave already and count
+    // as empty in this prefix
+    if (kFused && skip_small && blen <= kPerBufMax) continue;
     const uint64_t n = b1 - b0;
     const uint64_t rel_lo = (S0 > b0 ? S0 - b0 : 0);
     const uint64_t rel_hi = (b1 < S1 || last_wave) ? n : S1 - b0;
@@ -760,8 +807,11 @@ template <bool kStrided, int G, int kD>
 __device__ __forceinline__ void small_body(const SmallArgs &a, uint32_t *s_lds, uint64_t n, uint32_t blk,
                                            uint32_t nblk);
 
+// kPB: the per-buffer mode's form (fused only): 4 = round 4 (tables built in
+// registers, the decision after the work), 3 = round 3 (tables and lengths
+// in front of the one barrier; kept for same-process A/B in tools/)
 template <bool kStrided, uint32_t kD = kDepth, int kAblate = 0, bool kRotate = true, bool kStamp = false,
-          int kPrio = 1, int kAux = kLoadNt, bool kFused = false, bool kWin = kWindowed>
+          int kPrio = 1, int kAux = kLoadNt, bool kFused = false, bool kWin = kWindowed, int kPB = 4>
 __global__ __launch_bounds__(kThreads) void crc32_batch_kernel(BatchArgs args) {
   __shared__ __attribute__((aligned(16))) uint32_t s_lds[kLdsBytes / 4];
   uint32_t grid = gridDim.x;  // the batch's workgroups
@@ -827,6 +877,7 @@ __global__ __launch_bounds__(kThreads) void crc32_batch_kernel(BatchArgs args) {
   // piece walk and the unit searches.  Every workgroup writes the same
   // values; each reads only after its own writes and a barrier.
   uint64_t *const lds_pre = reinterpret_cast<uint64_t *>(s_lds);
+  bool perbuf_done = false;  // the per-buffer pass ran: the scan and the walk take the long buffers only
   if (kFused) {
     static_assert(kFusedMaxN == 8u * kThreads, "fused scan: 8 lengths per thread");
     static_assert((kFusedMaxN + 1 + 16) * 8 <= kLdsBytes, "fused scan fits in LDS");
@@ -851,7 +902,91 @@ __global__ __launch_bounds__(kThreads) void crc32_batch_kernel(BatchArgs args) {
     // guarded length loads waited for one at a time: the table fill
     // completed 7.7 us after entry, now 3.5 us; tools/c2_probe,
     // profiles/r03/s11, s16.)
-    if (args.n <= (uint64_t)grid * kWaves) {
+    if (kPB >= 4 && args.n <= (uint64_t)grid * kWaves) {
+      // Round 4: nothing in front of the payload waits on memory but the
+      // wave's own descriptor.  The braid and combine tables are built in
+      // registers (braid_gen_lane, comb_gen) and the one barrier in front
+      // of the piece waits for ALU work alone; the decision -- is any buffer
+      // of the batch longer than kPerBufMax? -- is taken after the work:
+      // every wave checksums its own buffer when it is short enough, its
+      // lengths arrive while its first payload loads are in flight, and the
+      // workgroup compares notes behind two barriers at the end.  When some
+      // buffer is longer, the in-kernel scan below runs over the long ones
+      // only (the short ones count as empty and are skipped).  Every
+      // workgroup reads the same lengths, so all take the same decision.
+      const uint32_t lane = tid & 63u, slot = uni32(tid >> 6);
+      const uint64_t b = (uint64_t)slot * grid + blockIdx.x;
+      const bool wg_busy = blockIdx.x < args.n;  // workgroup-uniform
+      uint64_t blen = 0, bp = 0;
+      uint32_t bseed = 0;
+      if (b < args.n) {
+        blen = uni64(args.lens[b]);
+        bp = uni64(reinterpret_cast<uint64_t>(args.ptrs[b]));
+        bseed = args.seeds ? uni32(args.seeds[b]) : 0u;
+      }
+      uint64_t L[8];  // the decision's lengths (thread t: buffers t + 1024 j), clamped, unguarded
+#pragma unroll
+      for (uint32_t j = 0; j < 8; j++) {
+        const uint64_t idx = tid + 1024u * j;
+        L[j] = args.lens[idx < args.n ? idx : args.n - 1];
+      }
+      if (wg_busy) {
+        const uint32_t e = braid_gen_lane(lane, slot);
+        uint4 *dst = reinterpret_cast<uint4 *>(s_lds);
+#pragma unroll
+        for (uint32_t k = 0; k < 8; k++) {
+          const uint32_t src = (lane >> 4) + 4u * (k & 3u) + 16u * (2u * (k >> 2) + ((lane >> 3) & 1u));
+          const uint32_t val = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(src * 4u), (int)e);
+          dst[tid + 1024u * k] = make_uint4(val, val, val, val);
+        }
+        uint4 cm0, cm1;
+        comb_gen(slot, lane, cm0, cm1);
+        uint4 *cdst = reinterpret_cast<uint4 *>(s_lds + kLdsCombDword);
+        cdst[tid] = cm0;
+        cdst[tid + 1024u] = cm1;
+      }
+      const uint64_t t_lens = kStamp ? __builtin_amdgcn_s_memrealtime() : 0;  // diagnostic: tables written
+      __syncthreads();  // the tables are in LDS
+      const uint64_t t_fill = kStamp ? __builtin_amdgcn_s_memrealtime() : 0;
+      const bool own = b < args.n && blen <= kPerBufMax;  // wave-uniform
+      const uint8_t *bptr = reinterpret_cast<const uint8_t *>(bp);
+      uint4 pre[2 * kD];
+      piece_preload<kD, kAux>(bptr, 0, blen, lane, own && blen >= 4, pre);
+      bool big = false;
+#pragma unroll
+      for (uint32_t j = 0; j < 8; j++) big |= (tid + 1024u * j < args.n) & (L[j] > kPerBufMax);
+      const uint32_t any_big = __ballot(big) ? 1u : 0u;
+      if (own) {
+        // younger wave slots issue first (the round-3 per-buffer form below)
+        if (slot >= 12) __builtin_amdgcn_s_setprio(3);
+        else if (slot >= 8) __builtin_amdgcn_s_setprio(2);
+        else if (slot >= 4) __builtin_amdgcn_s_setprio(1);
+        uint32_t r;
+        if (blen < 4) {
+          r = ~bseed;
+          for (uint32_t p = 0; p < (uint32_t)blen; p++) r = (r >> 8) ^ tab->stdtab[(r ^ bptr[p]) & 0xFFu];
+        } else {
+          r = piece_raw<kD, kAblate, kAux, false, true>(s_lds, bptr, 0, blen, bseed, lane, nullptr, pre);
+        }
+        if (lane == 0) args.out[b] = ~r;
+        if (kStamp && lane == 0) {  // diagnostic build (tools/c2_probe): this wave's timeline
+          const uint64_t w = (uint64_t)blockIdx.x * kWaves + slot;
+          args.stamps[8 * w + 0] = t_fill;
+          args.stamps[8 * w + 1] = __builtin_amdgcn_s_memrealtime();
+          args.stamps[8 * w + 4] = t_entry;
+          args.stamps[8 * w + 5] = t_fill;
+          args.stamps[8 * w + 6] = t_lens;
+        }
+      }
+      __syncthreads();  // every wave is done with the tables: the LDS is free
+      if (lane == 0) s_lds[slot] = any_big;
+      __syncthreads();
+      const uint32_t fw = lane < (uint32_t)kWaves ? s_lds[lane] : 0u;
+      if (!__ballot(fw != 0)) return;  // workgroup-uniform, and the same in every workgroup
+      __syncthreads();  // every wave has read the flags before the scan overwrites LDS
+      perbuf_done = true;
+      load_tables();
+    } else if (args.n <= (uint64_t)grid * kWaves) {
       const uint32_t lane = tid & 63u, slot = uni32(tid >> 6);
       const uint64_t b = (uint64_t)slot * grid + blockIdx.x;
       const bool wg_busy = blockIdx.x < args.n;  // workgroup-uniform
@@ -945,6 +1080,7 @@ __global__ __launch_bounds__(kThreads) void crc32_batch_kernel(BatchArgs args) {
     for (uint32_t k = 0; k < 8; k++) {
       const uint64_t idx = 8u * tid + k;
       v[k] = idx < args.n ? args.lens[idx] : 0;
+      if (perbuf_done && v[k] <= kPerBufMax) v[k] = 0;
       sum += v[k];
     }
     uint64_t tot;
@@ -1047,7 +1183,7 @@ __global__ __launch_bounds__(kThreads) void crc32_batch_kernel(BatchArgs args) {
     }
     if (S0 < S1 || last)
       npieces += process_range<kStrided, kD, kAblate, kRotate, kPrio, kAux, kStamp, kFused, kWin>(
-          args, bv, s_lds, tab, S0, S1, last, salt, lane, band, f0, lb1, &t_tail);
+          args, bv, s_lds, tab, S0, S1, last, salt, lane, band, f0, lb1, &t_tail, perbuf_done);
     if (!units) break;
     if (first_claim) {
       nx = (uint32_t)w;  // units >= W whenever the dynamic part is on

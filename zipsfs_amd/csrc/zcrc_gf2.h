@@ -106,6 +106,20 @@ struct MctBasis {
   }
 };
 
+// The same for c = x^(-8 nbytes) (the combine tables, TableBlob::comb).
+ZCRC_HD constexpr uint32_t gf2_times_xinv_c(uint32_t r) {
+  return (r & 0x80000000u) ? (((r ^ kPolyReflected) << 1) | 1u) : (r << 1);
+}
+template <int nbytes>
+struct MctBasisInv {
+  uint32_t q[32];
+  constexpr MctBasisInv() : q{} {
+    uint32_t c = kOne;
+    for (int i = 0; i < 8 * nbytes; i++) c = gf2_times_xinv_c(c);
+    for (int p = 0; p < 32; p++) q[p] = gf2_mul(c, 1u << p);
+  }
+};
+
 // Standard reflected byte table T[v] = raw CRC of the single byte v.
 inline void build_std_table(uint32_t *table /* 256 */) {
   for (uint32_t v = 0; v < 256; v++) {

@@ -117,7 +117,8 @@ hipError_t launch_plan(const uint64_t *d_lens, uint64_t n, uint64_t *d_prefix, u
 // Split plan (device batches of more than kFusedMaxN buffers).  When buffers
 // of at most kSmallMax bytes are worth at least two of the batch kernel's
 // workgroups (zcrc_kernels.hip), they are listed for the small-buffer kernel (sdesc, count counts[1]) and the
-// others compacted, in order, into a batch for the batch kernel (ptrs_c,
+// others compacted -- those below kBigMin first, then the others, each in index
+// order -- into a batch for the batch kernel (ptrs_c,
 // seeds_c, prefix_c, original index oidx, count counts[0]); counts[2] = 1.
 // Otherwise prefix_c is the plain prefix of all n buffers, counts = {n, 0,
 // 0}.  out[] of the batch kernel's buffers is zeroed.  force: split whenever
@@ -129,7 +130,7 @@ struct SplitPlan {
   const uint64_t *lens;
   const uint32_t *seeds;  // nullable
   uint64_t n;
-  uint64_t *tile_sum;     // kTileWords per tile: large bytes, small bytes, packed counts
+  uint64_t *tile_sum;     // kTileWords per tile: medium, big, small bytes, medium | big << 32 counts, small count
   uint64_t *tile_pre;     // kTileWords x (tiles + 1): exclusive tile prefixes + totals (above kPlanDirectTiles)
   uint64_t *prefix_c;     // n + 1
   const uint8_t **ptrs_c;
@@ -141,11 +142,13 @@ struct SplitPlan {
   uint32_t small_cost;    // CU time of a small-list byte, in quarters of a batch-kernel byte
   uint32_t force;
   uint32_t *ctr;          // the batch kernel's work counter (zeroed)
+  uint64_t big_min;       // on a split, buffers of at least this go after the others (kBigMin)
   uint64_t *stamps;       // diagnostics (tools/plan_probe): 8 s_memrealtime stamps per scatter workgroup, or null
 };
 hipError_t launch_plan_split(const SplitPlan &p, hipStream_t stream);
 constexpr uint32_t kSizeClasses = kSmallMax / 256 + 1;  // small list order: 256-B block count
-constexpr uint32_t kTileWords = 3;
+constexpr uint32_t kTileWords = 5;
+constexpr uint64_t kBigMin = 1ull << 20;  // split plan: buffers of at least this go last in the batch kernel's order
 constexpr uint64_t kPlanDirectTiles = 512;  // up to this many tiles each scatter workgroup sums the tile words itself
 constexpr uint32_t kSmallCostDefault = 14;  // 3.5 batch-kernel bytes (zcrc_kernels.hip, plan_split_scatter)
 

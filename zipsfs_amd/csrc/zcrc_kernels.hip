@@ -118,25 +118,32 @@ __global__ __launch_bounds__(1024) void plan_one_tile(const uint64_t *lens, uint
 // ------------------------------------------------------------ split plan
 // Two passes like plan_tile_sums/plan_tile_scan, both with plan_one_tile's
 // coalesced layout: wave w of a tile owns its buffers [512w, 512w + 512), lane
-// l takes 512w + 64k + l for k < 8.  Per tile: bytes of the buffers above
-// kSmallMax, bytes of those at or below it, both counts packed (low half:
-// above, high half: at or below).  The scatter decides for the whole launch
-// (every workgroup reads the same tile sums, so all decide alike): split when
-// the small list is worth at least two of the batch kernel's workgroups (or
-// p.force and there is any small buffer); otherwise it writes the plain prefix
-// of all buffers, as plan_tile_scan does, and an empty small list.  The large
-// buffers keep their order; each tile's small buffers are listed by size
-// class (256-B blocks), in index order within a class, so that the buffers a
-// wave of the small body takes together run equal block counts.  The ranking
-// is a counting sort by ballots -- six ballots give each lane the mask of
-// lanes with its class -- with per (class, wave, k) counts scanned in LDS: no
+// l takes 512w + 64k + l for k < 8.  Buffers fall into three classes: small
+// (<= kSmallMax), big (>= kBigMin) and medium (between).  Per tile
+// (kTileWords): medium bytes, big bytes, small bytes, the medium and big
+// counts packed (low / high half) and the small count.  The scatter decides
+// for the whole launch (every workgroup reads the same tile sums, so all
+// decide alike): split when the small list is worth at least two of the batch
+// kernel's workgroups (or p.force and there is any small buffer); otherwise
+// it writes the plain prefix of all buffers, as plan_tile_scan does, and an
+// empty small list.  On a split the batch kernel's buffers are compacted
+// medium first, then big, each class in index order (round 4): the batch
+// kernel hands out the last bytes of its batch dynamically, in 128 KiB units,
+// and with the big buffers last those units are sequential runs of one
+// buffer; a unit full of medium buffers is a chain of latency-bound pieces,
+// and the waves that drew such units last were config 4's ~60 us tail
+// (DESIGN.md section 4).  Each tile's small buffers are listed by size class
+// (256-B blocks), in index order within a class, so that the buffers a wave
+// of the small body takes together run equal block counts.  The ranking is a
+// counting sort by ballots -- six ballots give each lane the mask of lanes
+// with its class -- with per (class, wave, k) counts scanned in LDS: no
 // atomics (the LDS class atomics of the round-2 plan serialised on uniform
 // batches: 25.5 us per config-4 plan, ~60 us of a 1M x 1 KiB call).
 
 __device__ __forceinline__ uint32_t size_class(uint64_t len) { return (uint32_t)((len + 255) >> 8); }  // 256-B blocks
 
 __global__ __launch_bounds__(1024) void plan_split_count(SplitPlan p) {
-  __shared__ uint64_t s_w[16][3];
+  __shared__ uint64_t s_w[16][kTileWords];
   const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
   const uint64_t base = (uint64_t)blockIdx.x * kPlanTile + 512u * wv + lane;
   uint64_t lv[kPlanPerThread];
@@ -145,21 +152,24 @@ __global__ __launch_bounds__(1024) void plan_split_count(SplitPlan p) {
     const uint64_t idx = base + 64u * k;
     lv[k] = idx < p.n ? p.lens[idx] : ~0ull;  // ~0: absent
   }
-  uint64_t bl = 0, bs = 0, cnt = 0;
+  uint64_t bm = 0, bb = 0, bs = 0, cmb = 0, cs = 0;
 #pragma unroll
   for (uint32_t k = 0; k < kPlanPerThread; k++) {
     const uint64_t L = lv[k];
     if (L == ~0ull) continue;
-    if (L > kSmallMax) bl += L, cnt += 1;
-    else bs += L, cnt += 1ull << 32;
+    if (L <= kSmallMax) bs += L, cs += 1;
+    else if (L >= p.big_min) bb += L, cmb += 1ull << 32;
+    else bm += L, cmb += 1;
   }
   // wave totals: DPP scans, lane 63 (butterflies of __shfl_xor were LDS round trips)
-  bl = rdlane64(wave_incl_scan(bl), 63);
+  bm = rdlane64(wave_incl_scan(bm), 63);
+  bb = rdlane64(wave_incl_scan(bb), 63);
   bs = rdlane64(wave_incl_scan(bs), 63);
-  cnt = rdlane64(wave_incl_scan(cnt), 63);
-  if (lane == 0) s_w[wv][0] = bl, s_w[wv][1] = bs, s_w[wv][2] = cnt;
+  cmb = rdlane64(wave_incl_scan(cmb), 63);
+  cs = rdlane64(wave_incl_scan(cs), 63);
+  if (lane == 0) s_w[wv][0] = bm, s_w[wv][1] = bb, s_w[wv][2] = bs, s_w[wv][3] = cmb, s_w[wv][4] = cs;
   __syncthreads();
-  if (threadIdx.x < 3) {
+  if (threadIdx.x < kTileWords) {
     uint64_t v = 0;
     for (uint32_t w = 0; w < 16; w++) v += s_w[w][threadIdx.x];
     p.tile_sum[(uint64_t)kTileWords * blockIdx.x + threadIdx.x] = v;
@@ -167,13 +177,13 @@ __global__ __launch_bounds__(1024) void plan_split_count(SplitPlan p) {
 }
 
 // Above kPlanDirectTiles tiles: one workgroup turns the tile sums into
-// exclusive prefixes (tile_pre[3t + q]) and totals (tile_pre[3 tiles + q]),
-// so that each scatter workgroup reads 6 words instead of every earlier
+// exclusive prefixes (tile_pre[kTileWords t + q]) and totals (tile_pre[kTileWords tiles + q]),
+// so that each scatter workgroup reads 2 kTileWords words instead of every earlier
 // tile's (that read grew with the square of the tile count).
 __global__ __launch_bounds__(1024) void plan_split_tiles(SplitPlan p, uint32_t tiles) {
   __shared__ uint64_t s_tmp[16];
   const uint32_t per = (tiles + 1023u) / 1024u, t0 = threadIdx.x * per;
-  for (uint32_t q = 0; q < 3; q++) {
+  for (uint32_t q = 0; q < kTileWords; q++) {
     uint64_t acc = 0;
     for (uint32_t t = t0; t < t0 + per && t < tiles; t++) acc += p.tile_sum[(uint64_t)kTileWords * t + q];
     uint64_t tot;
@@ -189,9 +199,9 @@ __global__ __launch_bounds__(1024) void plan_split_tiles(SplitPlan p, uint32_t t
 
 __global__ __launch_bounds__(1024) void plan_split_scatter(SplitPlan p) {
   constexpr uint32_t kGroups = 16 * kPlanPerThread;  // (wave, k) groups of 64 buffers per tile
-  __shared__ uint64_t s_tw[3][2];                    // large bytes, small bytes, counts: earlier tiles, all
-  __shared__ uint64_t s_wb[16];                      // wave byte totals
-  __shared__ uint32_t s_wc[16];                      // wave large counts
+  __shared__ uint64_t s_tw[kTileWords][2];           // tile words: earlier tiles, all tiles
+  __shared__ uint64_t s_wb[16][2];                   // wave byte totals: medium, big
+  __shared__ uint32_t s_wc[16][2];                   // wave counts: medium, big
   __shared__ uint64_t s_tmp[16];
   __shared__ uint32_t s_mode;
   __shared__ uint32_t s_cls[kSizeClasses * kGroups];  // small count per (class, group) -> exclusive position
@@ -215,9 +225,10 @@ __global__ __launch_bounds__(1024) void plan_split_scatter(SplitPlan p) {
   }
   // earlier tiles' and all tiles' sums
   if (p.tile_pre) {
-    if (tid < 3) s_tw[tid][0] = p.tile_pre[(uint64_t)kTileWords * blockIdx.x + tid];
-    else if (tid < 6) s_tw[tid - 3][1] = p.tile_pre[(uint64_t)kTileWords * gridDim.x + tid - 3];
-  } else if (wv < 3) {
+    if (tid < kTileWords) s_tw[tid][0] = p.tile_pre[(uint64_t)kTileWords * blockIdx.x + tid];
+    else if (tid < 2 * kTileWords)
+      s_tw[tid - kTileWords][1] = p.tile_pre[(uint64_t)kTileWords * gridDim.x + tid - kTileWords];
+  } else if (wv < kTileWords) {
     uint64_t prev = 0, all = 0;
     for (uint32_t t = lane; t < gridDim.x; t += 64) {
       const uint64_t x = p.tile_sum[(uint64_t)kTileWords * t + wv];
@@ -231,8 +242,9 @@ __global__ __launch_bounds__(1024) void plan_split_scatter(SplitPlan p) {
   for (uint32_t i = tid; i < kSizeClasses * kGroups; i += 1024) s_cls[i] = 0u;
   __syncthreads();
   if (p.stamps) st[1] = __builtin_amdgcn_s_memrealtime();
-  const uint64_t al = s_tw[0][1], as = s_tw[1][1], ac = s_tw[2][1];  // all tiles
-  const uint64_t n_large = ac & 0xFFFFFFFFull, n_small = ac >> 32;
+  const uint64_t am = s_tw[0][1], ab = s_tw[1][1], as = s_tw[2][1];  // all tiles: bytes
+  const uint64_t n_med = s_tw[3][1] & 0xFFFFFFFFull, n_big = s_tw[3][1] >> 32, n_small = s_tw[4][1];
+  const uint64_t al = am + ab, n_large = n_med + n_big;
   if (tid == 0) {
     // workgroups for the small list: its share of the CU time, a small-list
     // byte weighted small_cost/4 against a batch-kernel byte (config 4 forced
@@ -260,21 +272,29 @@ __global__ __launch_bounds__(1024) void plan_split_scatter(SplitPlan p) {
   __syncthreads();
   if (p.stamps) st[2] = __builtin_amdgcn_s_memrealtime();
   const bool split = s_mode != 0;
-  // byte prefix of this tile's batch-kernel buffers (all of them without a
-  // split) along (k, lane) = index order, wave carries; their count from ballots
-  uint64_t ex[kPlanPerThread], bcarry = 0;
-  uint32_t cx[kPlanPerThread], ccarry = 0, rank[kPlanPerThread], cls[kPlanPerThread];
+  // byte prefixes of this tile's batch-kernel buffers, per class (without a
+  // split: all of them as one class), along (k, lane) = index order, wave
+  // carries; their counts from ballots
+  uint64_t exm[kPlanPerThread], exb[kPlanPerThread], cmry = 0, cbry = 0;
+  uint32_t cxm[kPlanPerThread], cxb[kPlanPerThread], ccm = 0, ccb = 0, rank[kPlanPerThread], cls[kPlanPerThread];
+  bool isbig[kPlanPerThread];
 #pragma unroll
   for (uint32_t k = 0; k < kPlanPerThread; k++) {
     const bool in = base + 64u * k < p.n;
     const bool large = in && (!split || v[k] > kSmallMax);
-    const uint64_t x = large ? v[k] : 0;
-    const uint64_t inc = wave_incl_scan(x);
-    ex[k] = bcarry + inc - x;
-    bcarry += rdlane64(inc, 63);
-    const uint64_t m = __ballot(large);
-    cx[k] = ccarry + (uint32_t)__popcll(m & lt);
-    ccarry += (uint32_t)__popcll(m);
+    const bool big = large && split && v[k] >= p.big_min;
+    isbig[k] = big;
+    const uint64_t xm = large && !big ? v[k] : 0, xb = big ? v[k] : 0;
+    const uint64_t im = wave_incl_scan(xm), ib = wave_incl_scan(xb);
+    exm[k] = cmry + im - xm;
+    exb[k] = cbry + ib - xb;
+    cmry += rdlane64(im, 63);
+    cbry += rdlane64(ib, 63);
+    const uint64_t mm = __ballot(large && !big), mb = __ballot(big);
+    cxm[k] = ccm + (uint32_t)__popcll(mm & lt);
+    cxb[k] = ccb + (uint32_t)__popcll(mb & lt);
+    ccm += (uint32_t)__popcll(mm);
+    ccb += (uint32_t)__popcll(mb);
     // small: rank among this (wave, k) group's lanes of the same class
     cls[k] = in && !large ? size_class(v[k]) : 63u;
     rank[k] = 0;
@@ -289,15 +309,18 @@ __global__ __launch_bounds__(1024) void plan_split_scatter(SplitPlan p) {
       if (cls[k] < kSizeClasses && rank[k] == 0) s_cls[cls[k] * kGroups + wv * kPlanPerThread + k] = (uint32_t)__popcll(match);
     }
   }
-  if (lane == 0) s_wb[wv] = bcarry, s_wc[wv] = ccarry;
+  if (lane == 0) s_wb[wv][0] = cmry, s_wb[wv][1] = cbry, s_wc[wv][0] = ccm, s_wc[wv][1] = ccb;
   __syncthreads();
   if (p.stamps) st[3] = __builtin_amdgcn_s_memrealtime();
-  uint64_t boff = 0;
-  uint32_t coff = 0;
-  for (uint32_t j = 0; j < wv; j++) boff += s_wb[j], coff += s_wc[j];
-  const uint64_t b0 = (split ? s_tw[0][0] : s_tw[0][0] + s_tw[1][0]) + boff;  // earlier tiles + earlier waves
-  const uint64_t pc = s_tw[2][0];
-  const uint64_t c0 = (split ? (pc & 0xFFFFFFFFull) : (uint64_t)blockIdx.x * kPlanTile) + coff;
+  uint64_t bom = 0, bob = 0;
+  uint32_t com = 0, cob = 0;
+  for (uint32_t j = 0; j < wv; j++) bom += s_wb[j][0], bob += s_wb[j][1], com += s_wc[j][0], cob += s_wc[j][1];
+  // first position and byte of this wave's medium (or, unsplit, all) and big buffers
+  const uint64_t ec = s_tw[3][0];  // earlier tiles' medium | big counts
+  const uint64_t bm0 = (split ? s_tw[0][0] : s_tw[0][0] + s_tw[1][0] + s_tw[2][0]) + bom;
+  const uint64_t cm0 = (split ? (ec & 0xFFFFFFFFull) : (uint64_t)blockIdx.x * kPlanTile) + com;
+  const uint64_t bb0 = am + s_tw[1][0] + bob;
+  const uint64_t cb0 = n_med + (ec >> 32) + cob;
   if (split) {
     // exclusive positions over (class, wave, k): thread t scans 5 consecutive entries
     constexpr uint32_t kPer = (kSizeClasses * kGroups + 1023) / 1024;
@@ -320,14 +343,14 @@ __global__ __launch_bounds__(1024) void plan_split_scatter(SplitPlan p) {
     __syncthreads();
   }
   if (p.stamps) st[4] = __builtin_amdgcn_s_memrealtime();
-  const uint64_t s0 = pc >> 32;  // earlier tiles' small buffers
+  const uint64_t s0 = s_tw[4][0];  // earlier tiles' small buffers
 #pragma unroll
   for (uint32_t k = 0; k < kPlanPerThread; k++) {
     const uint64_t idx = base + 64u * k;
     if (idx >= p.n) break;
     if (cls[k] == 63u) {  // batch kernel
-      const uint64_t j = c0 + cx[k];
-      p.prefix_c[j] = b0 + ex[k];
+      const uint64_t j = isbig[k] ? cb0 + cxb[k] : cm0 + cxm[k];
+      p.prefix_c[j] = isbig[k] ? bb0 + exb[k] : bm0 + exm[k];
       if (split) {
         p.ptrs_c[j] = pv[k];
         if (p.seeds) p.seeds_c[j] = sv[k];

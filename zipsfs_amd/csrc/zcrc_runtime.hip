@@ -371,6 +371,15 @@ uint32_t small_cost() {
   return v;
 }
 
+// Measurement knob: ZCRC_BIG_MIN (bytes, read per call) = where the split
+// plan's big class starts (kBigMin; a value above every length keeps index
+// order)
+uint64_t big_min() {
+  const char *e = getenv("ZCRC_BIG_MIN");
+  const unsigned long long v = e ? strtoull(e, nullptr, 0) : 0;
+  return v ? (uint64_t)v : kBigMin;
+}
+
 // ZCRC_SMALL=2: the split plan splits whenever there is a small buffer (tests)
 bool split_forced() {
   const char *e = getenv("ZCRC_SMALL");
@@ -408,6 +417,7 @@ int batch_device_split(const DeviceCtx &dc, const void *const *d_ptrs, const uin
   p.force = split_forced();
   p.grid = (uint32_t)dc.num_cus;
   p.small_cost = small_cost();
+  p.big_min = big_min();
   BatchArgs a{};
   a.ptrs = p.ptrs;
   a.seeds = d_seeds;
