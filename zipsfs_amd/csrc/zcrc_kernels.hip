@@ -211,17 +211,13 @@ __global__ __launch_bounds__(1024) void plan_split_scatter(SplitPlan p) {
   if (p.stamps) st[0] = __builtin_amdgcn_s_memrealtime();
   if (blockIdx.x == 0 && tid == 0) p.ctr[0] = 0u, p.ctr[kFaultByte / 4] = 0u;  // work counter, fault word
   const uint64_t base = (uint64_t)blockIdx.x * kPlanTile + 512u * wv + lane;
-  // this thread's lengths, pointers and seeds first (coalesced)
+  // this thread's lengths first (coalesced); pointers and seeds are loaded
+  // for the stores at the end (holding them from here spilled 61 VGPRs)
   uint64_t v[kPlanPerThread];
-  const uint8_t *pv[kPlanPerThread];
-  uint32_t sv[kPlanPerThread];
 #pragma unroll
   for (uint32_t k = 0; k < kPlanPerThread; k++) {
     const uint64_t idx = base + 64u * k;
-    const bool in = idx < p.n;
-    v[k] = in ? p.lens[idx] : 0;
-    pv[k] = in ? p.ptrs[idx] : nullptr;
-    sv[k] = in && p.seeds ? p.seeds[idx] : 0u;
+    v[k] = idx < p.n ? p.lens[idx] : 0;
   }
   // earlier tiles' and all tiles' sums
   if (p.tile_pre) {
@@ -274,40 +270,40 @@ __global__ __launch_bounds__(1024) void plan_split_scatter(SplitPlan p) {
   const bool split = s_mode != 0;
   // byte prefixes of this tile's batch-kernel buffers, per class (without a
   // split: all of them as one class), along (k, lane) = index order, wave
-  // carries; their counts from ballots
-  uint64_t exm[kPlanPerThread], exb[kPlanPerThread], cmry = 0, cbry = 0;
-  uint32_t cxm[kPlanPerThread], cxb[kPlanPerThread], ccm = 0, ccb = 0, rank[kPlanPerThread], cls[kPlanPerThread];
-  bool isbig[kPlanPerThread];
+  // carries; their counts from ballots.  Per (thread, k) one byte offset
+  // within the wave's class and one packed word: the count offset within
+  // the wave's class (bits 0-9), the size class (10-15; 63: the batch
+  // kernel's), the rank within the (wave, k) group's class (16-21), big (22).
+  uint64_t ex[kPlanPerThread], cmry = 0, cbry = 0;
+  uint32_t meta[kPlanPerThread], ccm = 0, ccb = 0;
 #pragma unroll
   for (uint32_t k = 0; k < kPlanPerThread; k++) {
     const bool in = base + 64u * k < p.n;
     const bool large = in && (!split || v[k] > kSmallMax);
     const bool big = large && split && v[k] >= p.big_min;
-    isbig[k] = big;
     const uint64_t xm = large && !big ? v[k] : 0, xb = big ? v[k] : 0;
     const uint64_t im = wave_incl_scan(xm), ib = wave_incl_scan(xb);
-    exm[k] = cmry + im - xm;
-    exb[k] = cbry + ib - xb;
+    ex[k] = big ? cbry + ib - xb : cmry + im - xm;
     cmry += rdlane64(im, 63);
     cbry += rdlane64(ib, 63);
     const uint64_t mm = __ballot(large && !big), mb = __ballot(big);
-    cxm[k] = ccm + (uint32_t)__popcll(mm & lt);
-    cxb[k] = ccb + (uint32_t)__popcll(mb & lt);
+    const uint32_t cx = big ? ccb + (uint32_t)__popcll(mb & lt) : ccm + (uint32_t)__popcll(mm & lt);
     ccm += (uint32_t)__popcll(mm);
     ccb += (uint32_t)__popcll(mb);
     // small: rank among this (wave, k) group's lanes of the same class
-    cls[k] = in && !large ? size_class(v[k]) : 63u;
-    rank[k] = 0;
+    const uint32_t cls = in && !large ? size_class(v[k]) : 63u;
+    uint32_t rank = 0;
     if (split) {  // uniform: without a split every buffer is the batch kernel's
       uint64_t match = ~0ull;
 #pragma unroll
       for (int bit = 0; bit < 6; bit++) {
-        const uint64_t b = __ballot((cls[k] >> bit) & 1u);
-        match &= ((cls[k] >> bit) & 1u) ? b : ~b;
+        const uint64_t b = __ballot((cls >> bit) & 1u);
+        match &= ((cls >> bit) & 1u) ? b : ~b;
       }
-      rank[k] = (uint32_t)__popcll(match & lt);
-      if (cls[k] < kSizeClasses && rank[k] == 0) s_cls[cls[k] * kGroups + wv * kPlanPerThread + k] = (uint32_t)__popcll(match);
+      rank = (uint32_t)__popcll(match & lt);
+      if (cls < kSizeClasses && rank == 0) s_cls[cls * kGroups + wv * kPlanPerThread + k] = (uint32_t)__popcll(match);
     }
+    meta[k] = cx | (cls << 10) | (rank << 16) | ((uint32_t)big << 22);
   }
   if (lane == 0) s_wb[wv][0] = cmry, s_wb[wv][1] = cbry, s_wc[wv][0] = ccm, s_wc[wv][1] = ccb;
   __syncthreads();
@@ -344,24 +340,43 @@ __global__ __launch_bounds__(1024) void plan_split_scatter(SplitPlan p) {
   }
   if (p.stamps) st[4] = __builtin_amdgcn_s_memrealtime();
   const uint64_t s0 = s_tw[4][0];  // earlier tiles' small buffers
+  if (split) {  // pointers and seeds of the compacted batch and the small list
+    const uint8_t *pv[kPlanPerThread];
+    uint32_t sv[kPlanPerThread];
 #pragma unroll
-  for (uint32_t k = 0; k < kPlanPerThread; k++) {
-    const uint64_t idx = base + 64u * k;
-    if (idx >= p.n) break;
-    if (cls[k] == 63u) {  // batch kernel
-      const uint64_t j = isbig[k] ? cb0 + cxb[k] : cm0 + cxm[k];
-      p.prefix_c[j] = isbig[k] ? bb0 + exb[k] : bm0 + exm[k];
-      if (split) {
+    for (uint32_t k = 0; k < kPlanPerThread; k++) {
+      const uint64_t idx = base + 64u * k;
+      const bool in = idx < p.n;
+      pv[k] = in ? p.ptrs[idx] : nullptr;
+      sv[k] = in && p.seeds ? p.seeds[idx] : 0u;
+    }
+#pragma unroll
+    for (uint32_t k = 0; k < kPlanPerThread; k++) {
+      const uint64_t idx = base + 64u * k;
+      if (idx >= p.n) break;
+      const uint32_t cx = meta[k] & 0x3FFu, cls = (meta[k] >> 10) & 63u, rank = (meta[k] >> 16) & 63u;
+      const bool big = (meta[k] >> 22) & 1u;
+      if (cls == 63u) {  // batch kernel
+        const uint64_t j = big ? cb0 + cx : cm0 + cx;
+        p.prefix_c[j] = (big ? bb0 : bm0) + ex[k];
         p.ptrs_c[j] = pv[k];
         if (p.seeds) p.seeds_c[j] = sv[k];
         p.oidx[j] = (uint32_t)idx;
+        p.out[idx] = 0u;  // split pieces xor into it
+      } else {
+        // the small list's descriptor: pointer (48-bit VA) | length << 48, index, seed
+        const uint64_t pw = reinterpret_cast<uint64_t>(pv[k]) | (v[k] << 48);
+        p.sdesc[s0 + s_cls[cls * kGroups + wv * kPlanPerThread + k] + rank] =
+            make_uint4((uint32_t)pw, (uint32_t)(pw >> 32), (uint32_t)idx, sv[k]);
       }
-      p.out[idx] = 0u;  // split pieces xor into it
-    } else {
-      // the small list's descriptor: pointer (48-bit VA) | length << 48, index, seed
-      const uint64_t pw = reinterpret_cast<uint64_t>(pv[k]) | (v[k] << 48);
-      p.sdesc[s0 + s_cls[cls[k] * kGroups + wv * kPlanPerThread + k] + rank[k]] =
-          make_uint4((uint32_t)pw, (uint32_t)(pw >> 32), (uint32_t)idx, sv[k]);
+    }
+  } else {  // the plain prefix of every buffer, in index order
+#pragma unroll
+    for (uint32_t k = 0; k < kPlanPerThread; k++) {
+      const uint64_t idx = base + 64u * k;
+      if (idx >= p.n) break;
+      p.prefix_c[cm0 + (meta[k] & 0x3FFu)] = bm0 + ex[k];
+      p.out[idx] = 0u;
     }
   }
   if (p.stamps && tid == 0) {
