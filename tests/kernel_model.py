@@ -92,6 +92,8 @@ class Tables:
         self.braid256 = mct(xpow8(256))  # the small-buffer kernel's table
         self.comb = [mct(xinvpow8(b)) for b in (4, 8, 16, 32, 64, 128, 256, 512)]
         self.tshift = [mct(xinvpow8(t)) for t in range(16)]
+        # r * x^-8 = (r << 8) ^ xinv8[r >> 24] (zcrc_gf2.h build_xinv8_table)
+        self.xinv8 = np.zeros(256, dtype=np.uint32)
         std = np.zeros(256, dtype=np.uint32)
         for v in range(256):
             r = v
@@ -99,6 +101,8 @@ class Tables:
                 r = times_x(r)
             std[v] = r
         self.stdtab = std
+        for v in range(256):
+            self.xinv8[int(std[v]) >> 24] = ((int(std[v]) << 8) & 0xFFFFFFFF) | v
 
 
 _TABLES = None
@@ -386,8 +390,8 @@ def crc_small_group(mem: np.ndarray, pstart: int, length: int, seed: int, G: int
     for b in (1, 0):
         if tpad >> 2 & (1 << b):
             r0 = int(mct_apply(T.comb[b], np.array([r0], dtype=np.uint32))[0])
-    for _ in range(8 * (tpad & 3)):
-        r0 = times_xinv(r0)
+    for _ in range(tpad & 3):  # the x^-8 byte table (zcrc_small_kernel.h)
+        r0 = ((r0 << 8) & 0xFFFFFFFF) ^ int(T.xinv8[r0 >> 24])
     return (~r0) & 0xFFFFFFFF
 
 

@@ -249,3 +249,22 @@ def test_per_buffer_flags_sit_on_zero_combine_words():
         c, j, v = chunk >> 8, (chunk >> 6) & 3, 4 * (chunk & 63)
         assert (c, j, v) == (s >> 2, s & 3, 0)
         assert comb[256 * s] == 0 and T.comb[c][j, 0] == 0
+
+
+def test_xinv8_byte_table_inverts_one_zero_byte():
+    """The small body's trailing-padding step r * x^-8 = (r << 8) ^ xinv8[r >> 24]
+    (zcrc_gf2.h build_xinv8_table): the top bytes of the standard table are a
+    permutation, so the step is defined for every r and equals 8 exact x^-1
+    steps; it undoes one zero byte fed through the register."""
+    T = km.tables()
+    assert sorted(int(t) >> 24 for t in T.stdtab) == list(range(256))
+    rng = np.random.default_rng(3)
+    for r in [0, 1, 0x80000000, 0xFFFFFFFF] + [int(x) for x in rng.integers(0, 1 << 32, 2000, dtype=np.uint64)]:
+        w = ((r << 8) & 0xFFFFFFFF) ^ int(T.xinv8[r >> 24])
+        b = r
+        for _ in range(8):
+            b = km.times_xinv(b)
+        assert w == b
+        fwd = (w >> 8) ^ int(T.stdtab[w & 0xFF])  # one zero byte forward
+        assert fwd == r
+

@@ -129,6 +129,16 @@ inline void build_std_table(uint32_t *table /* 256 */) {
   }
 }
 
+// The inverse byte step: r * x^-8 = (r << 8) ^ W[r >> 24].  The forward
+// step is r' = (r >> 8) ^ T[r & 0xFF], and the top bytes of T[0..255] are a
+// permutation, so v = r & 0xFF is the entry whose top byte is r' >> 24, and
+// r = ((r' ^ T[v]) << 8) | v.  W[T[v] >> 24] = (T[v] << 8) | v.
+inline void build_xinv8_table(uint32_t *w /* 256 */) {
+  uint32_t t[256];
+  build_std_table(t);
+  for (uint32_t v = 0; v < 256; v++) w[t[v] >> 24] = (t[v] << 8) | v;
+}
+
 // Host-side combine: zlib crc32_combine semantics.
 //   crc(A || B) = combine(crc(A), crc(B), |B|)
 inline uint32_t gf2_crc_combine(const XPowTable &t, uint32_t crc_a, uint32_t crc_b, uint64_t len_b) {

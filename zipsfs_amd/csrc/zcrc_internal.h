@@ -27,7 +27,7 @@ constexpr uint64_t kPlanTile = 1024 * kPlanPerThread;
 // one launch covers at most this many bytes (keeps every piece < 2 GiB)
 constexpr uint64_t kMaxLaunchBytes = 1ull << 42;
 
-// Multiply-by-constant tables, uploaded once per device (~101 KiB).
+// Multiply-by-constant tables, uploaded once per device (~106 KiB).
 struct TableBlob {
   uint32_t braid[4 * 256];       // MCT(x^(8*1024)): the hot-loop table
   uint32_t comb[8 * 4 * 256];    // x^-32, x^-64, x^-128 .. x^-4096 (combine tree)
@@ -35,6 +35,7 @@ struct TableBlob {
   uint32_t stdtab[256];          // standard byte table (buffers < 4 bytes)
   uint32_t x8pow[64];            // x^(8 * 2^k)
   uint32_t braid256[4 * 256];    // MCT(x^(8*256)): the small-buffer kernel's table
+  uint32_t xinv8[256];           // r * x^-8 = (r << 8) ^ xinv8[r >> 24] (one zero byte taken off)
 };
 
 struct BatchArgs {

@@ -17,7 +17,8 @@
 //     domain, as in the batch kernel);
 //   * fold: log2(4C) in-lane levels, log2(G) cross-lane levels (combine
 //     tables x^-32 .. x^-1024, TableBlob::comb 0..5), then the trailing
-//     padding is undone (x^-32/x^-64 tables, exact x^-1 steps);
+//     padding is undone (x^-32/x^-64 tables, then the x^-8 byte table in
+//     table 7's unused LDS);
 //   * up to kD blocks of loads are in flight before their braid steps, and
 //     the next group's descriptor is loaded while the current one runs.
 // Persistent: one 1024-thread workgroup per CU, waves walk groups of buffers
@@ -35,6 +36,9 @@ typedef unsigned int small_v4u __attribute__((ext_vector_type(4)));
 
 // Workgroup blk of nblk (the persistent grid, or the batch kernel's
 // workgroups that the split plan gave to the small list).
+// chunk of the combine area where the x^-8 byte table goes (table 7's)
+constexpr uint32_t kXinv8Chunk = 7u * 256u;
+
 template <bool kStrided, int G, int kD>
 __device__ __forceinline__ void small_body(const SmallArgs &a, uint32_t *s_lds, uint64_t n, uint32_t blk,
                                            uint32_t nblk) {
@@ -82,10 +86,14 @@ __device__ __forceinline__ void small_body(const SmallArgs &a, uint32_t *s_lds, 
       const uint32_t v = b[(((o >> 16) << 1) | ((o >> 7) & 1u)) * 256u + ((o >> 8) & 255u)];
       dst[tid + 1024u * k] = make_uint4(v, v, v, v);
     }
+    // combine tables 0..5 (6 and 7 are not used here); the first 256 words of
+    // table 7's area hold the x^-8 byte table for the trailing padding
     const uint4 *cs = reinterpret_cast<const uint4 *>(a.tab->comb);
     uint4 *cd = reinterpret_cast<uint4 *>(s_lds + kLdsCombDword);
     cd[tid] = cs[tid];
-    cd[tid + 1024u] = cs[tid + 1024u];
+    cd[tid + 1024u] = tid >= kXinv8Chunk - 1024u && tid < kXinv8Chunk - 1024u + 64u
+                          ? reinterpret_cast<const uint4 *>(a.tab->xinv8)[tid - (kXinv8Chunk - 1024u)]
+                          : cs[tid + 1024u];
   }
   __syncthreads();
   const uint32_t lo0 = (lane & 31u) * 4u;
@@ -150,9 +158,11 @@ __device__ __forceinline__ void small_body(const SmallArgs &a, uint32_t *s_lds, 
     const uint32_t tpad = (uint32_t)(span - re), a4 = tpad >> 2;
     if (a4 & 2u) r = comb_apply(s_lds, 1, r);
     if (a4 & 1u) r = comb_apply(s_lds, 0, r);
-    const uint32_t nbits = 8u * (tpad & 3u);
-    for (uint32_t b = 0; b < 24u; b++)
-      if (b < nbits) r = gf2_times_xinv(r);
+    // the last 0-3 bytes: one x^-8 byte-table step each (24 bit steps before:
+    // ~100 VALU per buffer group, as much as a 1 KiB buffer's braid steps)
+    const uint32_t *xinv8 = s_lds + kLdsCombDword + 4u * kXinv8Chunk;
+    for (uint32_t b = 0; b < 3u; b++)
+      if (b < (tpad & 3u)) r = (r << 8) ^ xinv8[r >> 24];
     if (active && lg == 0) {
       if (tiny) {
         const uint8_t *bp = reinterpret_cast<const uint8_t *>(pstart);

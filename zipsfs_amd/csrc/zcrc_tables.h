@@ -9,6 +9,7 @@ namespace zcrc {
 // braid256 = MCT(x^(8*256))           small-buffer kernel: 256 B per step
 // comb   = MCT(x^-32 .. x^-4096)      in-lane and cross-lane combine tree
 // tshift = MCT(x^(-8t)), t < 16       16-B alignment padding at a piece end
+// xinv8  = r * x^-8 byte table         the small-buffer kernel's last 0-3 padding bytes
 inline void build_tables(TableBlob &tb) {
   XPowTable xp;
   build_xpow_table(xp);
@@ -18,6 +19,7 @@ inline void build_tables(TableBlob &tb) {
   for (int c = 0; c < 8; c++) build_mct(gf2_xinvpow8_small(comb_bytes[c]), tb.comb + c * 1024);
   for (int t = 0; t < 16; t++) build_mct(gf2_xinvpow8_small((uint32_t)t), tb.tshift + t * 1024);
   build_std_table(tb.stdtab);
+  build_xinv8_table(tb.xinv8);
   for (int k = 0; k < 64; k++) tb.x8pow[k] = xp.x2k[k + 3];
 }
 
