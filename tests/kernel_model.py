@@ -401,7 +401,7 @@ K_SMALL_COST = 14  # zcrc_internal.h kSmallCostDefault (quarters of a batch-kern
 K_BIG_MIN = 1 << 20  # zcrc_internal.h kBigMin
 
 
-def split_plan(lens, grid: int = 256, force: bool = False, small_cost: int = K_SMALL_COST):
+def split_plan(lens, grid: int = 256, force: bool = False, small_cost: int = K_SMALL_COST, direct_ok: bool = True):
     """zcrc_kernels.hip plan_split_scatter's decisions and lists: (split,
     large list -- on a split, buffers below kBigMin first, then the others,
     each in index order -- with its prefix, small list tile by tile (8192
@@ -423,6 +423,10 @@ def split_plan(lens, grid: int = 256, force: bool = False, small_cost: int = K_S
         return dict(split=False, large=list(range(len(lens))), small=[], wgs=wgs, lanes=16)
     by_class = sorted(small, key=lambda i: (i // 8192, (lens[i] + 255) >> 8, i))
     lanes = 8 if as_ <= 2048 * len(small) else 16
+    if not large and direct_ok:  # mode 2: about equal small buffers, walked in index order without lists
+        mean = as_ / len(small)
+        if sum(lens[i] * lens[i] for i in small) / len(small) - mean * mean <= 128.0 * 128.0:
+            return dict(split=True, direct=True, large=[], small=list(small), wgs=grid, lanes=lanes)
     # round 4: the batch kernel's buffers medium first, then big (>= kBigMin), each in index order
     large = [i for i in large if lens[i] < K_BIG_MIN] + [i for i in large if lens[i] >= K_BIG_MIN]
     return dict(split=True, large=large, small=by_class, wgs=wgs, lanes=lanes)

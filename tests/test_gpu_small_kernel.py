@@ -158,6 +158,26 @@ def test_device_split_plan(shape, small, monkeypatch):
     np.testing.assert_array_equal(got, _oracle(host, offs, lens, seeds_np))
 
 
+@pytest.mark.parametrize("direct", ["1", "0"])
+@pytest.mark.parametrize("lens_kind", ["uniform_1k", "near_uniform", "uniform_tiny"])
+def test_device_split_plan_direct_mode(lens_kind, direct, monkeypatch):
+    """The split plan's mode 2 (round 4): a batch of about equal small
+    buffers is walked in place by the small body (the caller's ptrs, lens and
+    seeds, index order, no lists); ZCRC_SMALL_DIRECT=0 keeps the lists.
+    Unaligned starts, seeds, results against the oracle."""
+    monkeypatch.setenv("ZCRC_SMALL_DIRECT", direct)
+    rnd = random.Random(len(lens_kind) * 11 + int(direct))
+    n = 30_000
+    lens = {"uniform_1k": [1024] * n, "near_uniform": [rnd.randint(900, 1200) for _ in range(n)],
+            "uniform_tiny": [rnd.choice([0, 1, 2, 3, 5]) for _ in range(n)]}[lens_kind]
+    mem, offs, ptrs, lt = _device_batch(rnd, lens)
+    host = mem.cpu().numpy()
+    seeds_np, seeds = _seeds(rnd, n)
+    np.testing.assert_array_equal(u32(z.crc32_batch_device(ptrs, lt, seeds=seeds)), _oracle(host, offs, lens, seeds_np))
+    np.testing.assert_array_equal(u32(z.crc32_batch_device(ptrs, lt)),
+                                  _oracle(host, offs, lens, np.zeros(n, np.uint32)))
+
+
 def test_config4_golden_replicated_through_split_plan(golden):
     """The config-4 golden sample repeated 9 times (> kFusedMaxN buffers, so
     the device split plan runs): every CRC equals the reference's."""
@@ -291,8 +311,8 @@ def _split_lists(scratch, n):
     T = -(-n // 8192)
     prefix = 256
     tiles = prefix + 8 * (n + 1)
-    tile_pre = tiles + 40 * T  # kTileWords = 5
-    ptrs = tile_pre + 40 * (T + 1)
+    tile_pre = tiles + 48 * T  # kTileWords = 6
+    ptrs = tile_pre + 48 * (T + 1)
     seeds = ptrs + 8 * n
     oidx = seeds + 4 * n
     sdesc = (oidx + 4 * n + 15) // 16 * 16
@@ -302,7 +322,8 @@ def _split_lists(scratch, n):
 
 
 @pytest.mark.parametrize("n,shape", [(20_000, "mixed"), (50_000, "all_small"), (4_200_000, "mixed"),
-                                     (4_300_000, "all_small"), (20_000, "mixed_big"), (60_000, "mixed_big")])
+                                     (4_300_000, "all_small"), (20_000, "mixed_big"), (60_000, "mixed_big"),
+                                     (30_000, "uniform_small"), (600_000, "near_uniform_small")])
 def test_split_plan_lists_equal_the_model(n, shape):
     """The plan's decision, the compacted batch (order and byte prefix) and the
     small list (tile by tile, by size class, index order within a class) equal
@@ -313,6 +334,10 @@ def test_split_plan_lists_equal_the_model(n, shape):
     top = SMALL_MAX + 1 if n < 1_000_000 else 600  # keep the 4M-buffer batches near 1 GiB
     if shape == "all_small":
         lens = rng.integers(0, min(top, 700), n)
+    elif shape == "uniform_small":  # the split plan's mode 2 (direct): no lists
+        lens = np.full(n, 1024)
+    elif shape == "near_uniform_small":
+        lens = rng.integers(1000, 1300, n)
     elif shape == "mixed":  # ZIP-entry-like: most small, some large
         lens = np.where(rng.random(n) < 0.995, rng.integers(0, top, n), rng.integers(SMALL_MAX + 1, 40_000, n))
     else:  # mixed_big: medium and big (>= 1 MiB, kBigMin) batch-kernel buffers interleaved (round-4 order)
@@ -331,7 +356,10 @@ def test_split_plan_lists_equal_the_model(n, shape):
     counts, prefix, oidx, sdesc = _split_lists(scratch, n)
     model = km.split_plan(lens.tolist(), grid=z.device_info()["num_cus"])
     assert bool(counts[2]) == model["split"], counts
-    if model["split"]:
+    assert (int(counts[2]) == 2) == model.get("direct", False), counts
+    if model.get("direct"):
+        assert int(counts[1]) == n and int(counts[0]) == 0 and int(counts[4]) == z.device_info()["num_cus"]
+    elif model["split"]:
         nl, ns = int(counts[0]), int(counts[1])
         assert (nl, ns) == (len(model["large"]), len(model["small"]))
         np.testing.assert_array_equal(oidx[:nl], np.array(model["large"], dtype=np.uint32))

@@ -196,7 +196,9 @@ def test_split_plan_model_lists():
     # all large: nothing to split; all small: every workgroup takes the small list
     assert not km.split_plan([70000] * 10000)["split"]
     q = km.split_plan([1000] * 10000)
-    assert q["split"] and q["wgs"] == 256 and q["lanes"] == 8
+    assert q["split"] and q["wgs"] == 256 and q["lanes"] == 8 and q["direct"]  # mode 2: no lists
+    assert not km.split_plan([1000] * 10000, direct_ok=False).get("direct")
+    assert not km.split_plan(list(range(100, 8100)) * 2).get("direct")  # ragged small: the class-ordered list
     # a handful of small buffers among large ones is not worth two workgroups
     few = [1 << 20] * 9000 + [100] * 5
     assert not km.split_plan(few)["split"] and km.split_plan(few, force=True)["split"]

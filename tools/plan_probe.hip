@@ -75,6 +75,7 @@ int main(int argc, char **argv) {
   p.grid = (uint32_t)cus;
   p.small_cost = kSmallCostDefault;
   p.big_min = kBigMin;
+  p.direct_ok = getenv("ZCRC_SMALL_DIRECT") == nullptr || getenv("ZCRC_SMALL_DIRECT")[0] != '0';
   for (int r = 0; r < 5; r++) CK(launch_plan_split(p, 0));
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0));

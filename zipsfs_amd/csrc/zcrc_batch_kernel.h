@@ -825,7 +825,7 @@ __global__ __launch_bounds__(kThreads) void crc32_batch_kernel(BatchArgs args) {
         SmallArgs sa{};
         sa.ptrs = args.ptrs;
         sa.lens = args.lens;
-        sa.sdesc = args.sdesc;
+        sa.sdesc = uni64(args.n_dev[2]) == 2 ? nullptr : args.sdesc;  // direct: the caller's arrays
         sa.seeds = args.seeds;
         sa.out = args.out;
         sa.tab = args.tab;

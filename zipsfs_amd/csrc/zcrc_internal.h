@@ -131,24 +131,27 @@ struct SplitPlan {
   const uint64_t *lens;
   const uint32_t *seeds;  // nullable
   uint64_t n;
-  uint64_t *tile_sum;     // kTileWords per tile: medium, big, small bytes, medium | big << 32 counts, small count
+  uint64_t *tile_sum;     // kTileWords per tile: medium, big, small bytes, medium | big << 32 counts, small count,
+                          // small lengths' sum of squares
   uint64_t *tile_pre;     // kTileWords x (tiles + 1): exclusive tile prefixes + totals (above kPlanDirectTiles)
   uint64_t *prefix_c;     // n + 1
   const uint8_t **ptrs_c;
   uint32_t *seeds_c;      // written when seeds != nullptr
   uint32_t *oidx, *out;
   uint4 *sdesc;           // the small list, one 16-B descriptor per entry (SmallArgs::sdesc)
-  uint64_t *counts;       // [0] n_large, [1] n_small, [2] split, [3] small lanes per buffer, [4] small workgroups
+  uint64_t *counts;       // [0] n_large, [1] n_small, [2] split (1; 2: direct, the small body walks ptrs/lens in
+                          // index order), [3] small lanes per buffer, [4] small workgroups
   uint32_t grid;          // the batch kernel's workgroups
   uint32_t small_cost;    // CU time of a small-list byte, in quarters of a batch-kernel byte
   uint32_t force;
   uint32_t *ctr;          // the batch kernel's work counter (zeroed)
   uint64_t big_min;       // on a split, buffers of at least this go after the others (kBigMin)
+  uint32_t direct_ok;     // a batch of about equal small buffers may skip the lists (mode 2)
   uint64_t *stamps;       // diagnostics (tools/plan_probe): 8 s_memrealtime stamps per scatter workgroup, or null
 };
 hipError_t launch_plan_split(const SplitPlan &p, hipStream_t stream);
 constexpr uint32_t kSizeClasses = kSmallMax / 256 + 1;  // small list order: 256-B block count
-constexpr uint32_t kTileWords = 5;
+constexpr uint32_t kTileWords = 6;
 constexpr uint64_t kBigMin = 1ull << 20;  // split plan: buffers of at least this go last in the batch kernel's order
 constexpr uint64_t kPlanDirectTiles = 512;  // up to this many tiles each scatter workgroup sums the tile words itself
 constexpr uint32_t kSmallCostDefault = 14;  // 3.5 batch-kernel bytes (zcrc_kernels.hip, plan_split_scatter)

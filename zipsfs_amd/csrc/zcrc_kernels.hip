@@ -121,7 +121,9 @@ __global__ __launch_bounds__(1024) void plan_one_tile(const uint64_t *lens, uint
 // l takes 512w + 64k + l for k < 8.  Buffers fall into three classes: small
 // (<= kSmallMax), big (>= kBigMin) and medium (between).  Per tile
 // (kTileWords): medium bytes, big bytes, small bytes, the medium and big
-// counts packed (low / high half) and the small count.  The scatter decides
+// counts packed (low / high half), the small count and the small lengths'
+// sum of squares (round 4: a batch of about equal small buffers is walked in
+// place by the small body, without lists -- mode 2).  The scatter decides
 // for the whole launch (every workgroup reads the same tile sums, so all
 // decide alike): split when the small list is worth at least two of the batch
 // kernel's workgroups (or p.force and there is any small buffer); otherwise
@@ -152,12 +154,12 @@ __global__ __launch_bounds__(1024) void plan_split_count(SplitPlan p) {
     const uint64_t idx = base + 64u * k;
     lv[k] = idx < p.n ? p.lens[idx] : ~0ull;  // ~0: absent
   }
-  uint64_t bm = 0, bb = 0, bs = 0, cmb = 0, cs = 0;
+  uint64_t bm = 0, bb = 0, bs = 0, cmb = 0, cs = 0, sq = 0;
 #pragma unroll
   for (uint32_t k = 0; k < kPlanPerThread; k++) {
     const uint64_t L = lv[k];
     if (L == ~0ull) continue;
-    if (L <= kSmallMax) bs += L, cs += 1;
+    if (L <= kSmallMax) bs += L, cs += 1, sq += L * L;
     else if (L >= p.big_min) bb += L, cmb += 1ull << 32;
     else bm += L, cmb += 1;
   }
@@ -167,7 +169,8 @@ __global__ __launch_bounds__(1024) void plan_split_count(SplitPlan p) {
   bs = rdlane64(wave_incl_scan(bs), 63);
   cmb = rdlane64(wave_incl_scan(cmb), 63);
   cs = rdlane64(wave_incl_scan(cs), 63);
-  if (lane == 0) s_w[wv][0] = bm, s_w[wv][1] = bb, s_w[wv][2] = bs, s_w[wv][3] = cmb, s_w[wv][4] = cs;
+  sq = rdlane64(wave_incl_scan(sq), 63);
+  if (lane == 0) s_w[wv][0] = bm, s_w[wv][1] = bb, s_w[wv][2] = bs, s_w[wv][3] = cmb, s_w[wv][4] = cs, s_w[wv][5] = sq;
   __syncthreads();
   if (threadIdx.x < kTileWords) {
     uint64_t v = 0;
@@ -252,8 +255,17 @@ __global__ __launch_bounds__(1024) void plan_split_scatter(SplitPlan p) {
     if (n_large) wgs = ws ? (p.grid * ws + ws + wl - 1) / (ws + wl) : 0;
     // split when the small list is worth at least two workgroups (a
     // workgroup given to a handful of small buffers would idle a CU)
-    const uint32_t mode = n_small && (p.force || wgs >= 2);
+    uint32_t mode = n_small && (p.force || wgs >= 2);
     if (n_large) wgs = wgs < 1 ? 1 : (wgs > p.grid - 1 ? p.grid - 1 : wgs);
+    // direct (mode 2): every buffer is small and their lengths are about equal
+    // (standard deviation at most 128 B: a size class or two): the small body
+    // walks the caller's arrays in index order, no lists are written (the
+    // size-class order buys nothing on such a batch)
+    if (mode && !n_large && p.direct_ok) {
+      const double mean = (double)as / (double)n_small;
+      const double var = (double)s_tw[5][1] / (double)n_small - mean * mean;
+      if (var <= 128.0 * 128.0) mode = 2;
+    }
     s_mode = mode;
     if (blockIdx.x == 0) {  // totals: the batch kernel's count, prefix end and the small list
       const uint64_t nl = mode ? n_large : p.n;
@@ -267,6 +279,7 @@ __global__ __launch_bounds__(1024) void plan_split_scatter(SplitPlan p) {
   }
   __syncthreads();
   if (p.stamps) st[2] = __builtin_amdgcn_s_memrealtime();
+  if (s_mode == 2) return;  // direct: nothing to list (workgroup-uniform)
   const bool split = s_mode != 0;
   // byte prefixes of this tile's batch-kernel buffers, per class (without a
   // split: all of them as one class), along (k, lane) = index order, wave

@@ -380,6 +380,13 @@ uint64_t big_min() {
   return v ? (uint64_t)v : kBigMin;
 }
 
+// Measurement knob: ZCRC_SMALL_DIRECT=0 (read per call) keeps the lists for
+// batches of about equal small buffers (the split plan's mode 2 off)
+bool small_direct() {
+  const char *e = getenv("ZCRC_SMALL_DIRECT");
+  return !(e && e[0] == '0');
+}
+
 // ZCRC_SMALL=2: the split plan splits whenever there is a small buffer (tests)
 bool split_forced() {
   const char *e = getenv("ZCRC_SMALL");
@@ -418,6 +425,7 @@ int batch_device_split(const DeviceCtx &dc, const void *const *d_ptrs, const uin
   p.grid = (uint32_t)dc.num_cus;
   p.small_cost = small_cost();
   p.big_min = big_min();
+  p.direct_ok = small_direct();
   BatchArgs a{};
   a.ptrs = p.ptrs;
   a.seeds = d_seeds;
