@@ -131,7 +131,12 @@ static int preload_deflated_once(const char *path, off_t st_size, int mode, ref_
     void *dsts[1] = {dst};
     size_t out_len[1] = {0};
     int32_t status[1] = {-1};
-    if (zcrc_inflate_batch(src, src_len, dsts, cap, out_len, status, &gpu_crc, 1, 0) || status[0] != 0) return -1;
+    const int irc = zcrc_inflate_batch(src, src_len, dsts, cap, out_len, status, &gpu_crc, 1, 0);
+    if (irc || status[0] != 0) {
+      fprintf(stderr, "zcrc_inflate_batch: rc %d, status %d, out_len %zu of %zu (%s)\n", irc, (int)status[0],
+              out_len[0], (size_t)st_size, zcrc_last_error());
+      return -1;
+    }
     pthread_mutex_lock(&mutex_fhandle);
     already = (off_t)out_len[0];
     pthread_mutex_unlock(&mutex_fhandle);

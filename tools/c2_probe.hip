@@ -183,9 +183,10 @@ int main(int argc, char **argv) {
   };
   std::vector<hipEvent_t> ev(2 * kBatches);
   for (auto &e : ev) CHECK(hipEventCreate(&e));
-  enum { kProbeWave, kProbeGrid, kCrc, kCrcFused, kCrcFusedR3, kProbePb, kProbePbRot, kProbePbNoPrio, kNumV };
-  const char *names[kNumV] = {"probe-wave", "probe-grid", "crc", "crc-fused", "crc-fused-r3", "probe-pb", "probe-pb-rot",
-                              "probe-pb-np"};
+  enum { kProbeWave, kProbeGrid, kCrc, kCrcFused, kCrcFusedR3, kCrcFused5, kProbePb, kProbePbRot, kProbePbNoPrio,
+         kNumV };
+  const char *names[kNumV] = {"probe-wave", "probe-grid", "crc", "crc-fused", "crc-fused-r3", "crc-fused-5", "probe-pb",
+                              "probe-pb-rot", "probe-pb-np"};
   auto launch = [&](int v, int b, hipEvent_t e0, hipEvent_t e1) {
     const uint8_t *base = data + b * kBatchBytes;
     switch (v) {
@@ -211,6 +212,10 @@ int main(int argc, char **argv) {
       case kCrcFused:
         hipExtLaunchKernelGGL((crc32_batch_kernel<false, kDepth, 0, true, false, 1, kLoadNt, true>), dim3(cus),
                               dim3(kThreads), 0, 0, e0, e1, 0, crc_args(b, true));
+        break;
+      case kCrcFused5:
+        hipExtLaunchKernelGGL((crc32_batch_kernel<false, kDepth, 0, true, false, 1, kLoadNt, true, kWindowed, 5>),
+                              dim3(cus), dim3(kThreads), 0, 0, e0, e1, 0, crc_args(b, true));
         break;
       case kCrcFusedR3:
         hipExtLaunchKernelGGL((crc32_batch_kernel<false, kDepth, 0, true, false, 1, kLoadNt, true, kWindowed, 3>),
@@ -238,10 +243,12 @@ int main(int argc, char **argv) {
   CHECK(hipMemcpy(o1.data(), out, 4 * kN, hipMemcpyDeviceToHost));
   launch(kCrcFused, 0, nullptr, nullptr);
   CHECK(hipMemcpy(o2.data(), out, 4 * kN, hipMemcpyDeviceToHost));
-  std::vector<uint32_t> o3(kN);
+  std::vector<uint32_t> o3(kN), o4(kN);
   launch(kCrcFusedR3, 0, nullptr, nullptr);
   CHECK(hipMemcpy(o3.data(), out, 4 * kN, hipMemcpyDeviceToHost));
-  const bool eq = o1 == o2 && o1 == o3;
+  launch(kCrcFused5, 0, nullptr, nullptr);
+  CHECK(hipMemcpy(o4.data(), out, 4 * kN, hipMemcpyDeviceToHost));
+  const bool eq = o1 == o2 && o1 == o3 && o1 == o4;
   printf("c2_probe: %d CUs, 16 x 256 MiB batches rotated, %d reps; crc forms %s\n", cus, reps,
          eq ? "equal" : "DIFFER");
   for (int v = 0; v < kNumV; v++) {
@@ -254,7 +261,10 @@ int main(int argc, char **argv) {
     BatchArgs a = crc_args(b, fused);
     a.stamps = stamps;
     CHECK(hipMemset(stamps, 0, 64 * (uint64_t)cus * kWaves));
-    if (fused && pb == 3)
+    if (fused && pb == 5)
+      hipExtLaunchKernelGGL((crc32_batch_kernel<false, kDepth, 0, true, true, 1, kLoadNt, true, kWindowed, 5>),
+                            dim3(cus), dim3(kThreads), 0, 0, ev[0], ev[1], 0, a);
+    else if (fused && pb == 3)
       hipExtLaunchKernelGGL((crc32_batch_kernel<false, kDepth, 0, true, true, 1, kLoadNt, true, kWindowed, 3>),
                             dim3(cus), dim3(kThreads), 0, 0, ev[0], ev[1], 0, a);
     else if (fused)
@@ -305,5 +315,6 @@ int main(int argc, char **argv) {
   timeline("crc", false, 3);
   timeline("crc-fused", true, 5);
   timeline("crc-fused-r3", true, 7, 3);
+  timeline("crc-fused-5", true, 9, 5);
   return 0;
 }

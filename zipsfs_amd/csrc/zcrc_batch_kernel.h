@@ -808,8 +808,9 @@ __device__ __forceinline__ void small_body(const SmallArgs &a, uint32_t *s_lds, 
                                            uint32_t nblk);
 
 // kPB: the per-buffer mode's form (fused only): 4 = round 4 (tables built in
-// registers, the decision after the work), 3 = round 3 (tables and lengths
-// in front of the one barrier; kept for same-process A/B in tools/)
+// registers, the decision after the work), 5 = the same with the first
+// payload loads issued before the table build, 3 = round 3 (tables and
+// lengths in front of the one barrier); 3 and 5 are A/B forms for tools/)
 template <bool kStrided, uint32_t kD = kDepth, int kAblate = 0, bool kRotate = true, bool kStamp = false,
           int kPrio = 1, int kAux = kLoadNt, bool kFused = false, bool kWin = kWindowed, int kPB = 4>
 __global__ __launch_bounds__(kThreads) void crc32_batch_kernel(BatchArgs args) {
@@ -930,6 +931,12 @@ __global__ __launch_bounds__(kThreads) void crc32_batch_kernel(BatchArgs args) {
         const uint64_t idx = tid + 1024u * j;
         L[j] = args.lens[idx < args.n ? idx : args.n - 1];
       }
+      const bool own = b < args.n && blen <= kPerBufMax;  // wave-uniform
+      const uint8_t *bptr = reinterpret_cast<const uint8_t *>(bp);
+      uint4 pre[2 * kD];
+      // kPB >= 5: the first payload loads go out as soon as the descriptor is
+      // in, ahead of the table build (A/B form)
+      if (kPB >= 5) piece_preload<kD, kAux>(bptr, 0, blen, lane, own && blen >= 4, pre);
       if (wg_busy) {
         const uint32_t e = braid_gen_lane(lane, slot);
         uint4 *dst = reinterpret_cast<uint4 *>(s_lds);
@@ -948,10 +955,7 @@ __global__ __launch_bounds__(kThreads) void crc32_batch_kernel(BatchArgs args) {
       const uint64_t t_lens = kStamp ? __builtin_amdgcn_s_memrealtime() : 0;  // diagnostic: tables written
       __syncthreads();  // the tables are in LDS
       const uint64_t t_fill = kStamp ? __builtin_amdgcn_s_memrealtime() : 0;
-      const bool own = b < args.n && blen <= kPerBufMax;  // wave-uniform
-      const uint8_t *bptr = reinterpret_cast<const uint8_t *>(bp);
-      uint4 pre[2 * kD];
-      piece_preload<kD, kAux>(bptr, 0, blen, lane, own && blen >= 4, pre);
+      if (kPB < 5) piece_preload<kD, kAux>(bptr, 0, blen, lane, own && blen >= 4, pre);
       bool big = false;
 #pragma unroll
       for (uint32_t j = 0; j < 8; j++) big |= (tid + 1024u * j < args.n) & (L[j] > kPerBufMax);

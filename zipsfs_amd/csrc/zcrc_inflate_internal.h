@@ -80,7 +80,7 @@ hipError_t launch_inflate_split(const uint8_t *src, uint64_t src_len, uint8_t *d
                                 uint64_t *out_len, int32_t *status, InflateSplitShape shape, void *scratch,
                                 int num_cus, hipStream_t stream);
 // purposes of the runtime's per-stream scratch cache (zcrc_runtime.hip)
-enum ScratchUse { kScratchBatch = 0, kScratchInflateOrder = 1, kScratchFused = 2, kScratchInflateSplit = 3 };
+enum ScratchUse { kScratchBatch = 0, kScratchInflateOrder = 1, kScratchFused = 2, kScratchInflateSplit = 3, kScratchStridedCtr = 4 };
 
 
 }  // namespace zcrc

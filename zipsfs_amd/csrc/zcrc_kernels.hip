@@ -433,7 +433,7 @@ const char *product_kernel_name() {
   static char name[160];
   static std::once_flag once;
   std::call_once(once, [] {
-    snprintf(name, sizeof name, "zcrc::crc32_batch_kernel<false, %uu, 0, true, false, 1, %d, false, %s>", kDepth,
+    snprintf(name, sizeof name, "zcrc::crc32_batch_kernel<false, %uu, 0, true, false, 1, %d, false, %s, 4>", kDepth,
              kLoadNt, kWindowed ? "true" : "false");
   });
   return name;
@@ -463,7 +463,7 @@ const char *fused_kernel_name() {
   static char name[160];
   static std::once_flag once;
   std::call_once(once, [] {
-    snprintf(name, sizeof name, "zcrc::crc32_batch_kernel<false, %uu, 0, true, false, 1, %d, true, %s>", kDepth,
+    snprintf(name, sizeof name, "zcrc::crc32_batch_kernel<false, %uu, 0, true, false, 1, %d, true, %s, 4>", kDepth,
              kLoadNt, kWindowed ? "true" : "false");
   });
   return name;

@@ -1449,6 +1449,66 @@ static_assert(kStreamRegions == 4, "zcrc32_stream::staged holds one slot's 4 reg
 
 int set_error(int code, const char *msg) { return fail(code, msg); }
 
+namespace {
+struct TlBufs {
+  struct Buf {
+    int dev = -1;
+    void *p = nullptr;
+    size_t cap = 0;
+  };
+  std::vector<Buf> bufs;  // (device, purpose) pairs, few
+  ~TlBufs() {
+    for (Buf &b : bufs)
+      if (b.p) (void)hipFree(b.p);
+  }
+  Buf &get(int dev, int purpose) {
+    const size_t need = (size_t)(dev + 1) * kTlCount;
+    if (bufs.size() < need) bufs.resize(need);
+    Buf &b = bufs[(size_t)dev * kTlCount + (size_t)purpose];
+    b.dev = dev;
+    return b;
+  }
+};
+thread_local TlBufs t_bufs;
+}  // namespace
+
+int tl_device_buffer(int purpose, size_t bytes, void **out) {
+  int dev = 0;
+  ZCRC_HIP_TRY(hipGetDevice(&dev));
+  TlBufs::Buf &b = t_bufs.get(dev, purpose);
+  if (b.cap < bytes || !b.p) {
+    if (b.p) {
+      ZCRC_HIP_TRY(hipFree(b.p));  // (the thread's earlier calls synchronized before returning)
+      b.p = nullptr;
+      b.cap = 0;
+    }
+    const size_t nb = std::max<size_t>(bytes, 1u << 20);
+    ZCRC_HIP_TRY(hipMalloc(&b.p, nb));
+    b.cap = nb;
+  }
+  *out = b.p;
+  return ZCRC_OK;
+}
+
+void tl_device_trim(int purpose, size_t keep_max) {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return;
+  TlBufs::Buf &b = t_bufs.get(dev, purpose);
+  if (b.p && b.cap > keep_max) {
+    (void)hipFree(b.p);
+    b.p = nullptr;
+    b.cap = 0;
+  }
+}
+
+int with_lease_stream(const std::function<int(hipStream_t)> &fn) {
+  Lease lease;
+  int rc = lease.take(true, false);
+  if (rc) return rc;
+  if (!lease.count) return fail(ZCRC_ERR_HIP, "no staging slot");
+  return fn(lease.slot[0]->stream);
+}
+
 size_t host_shards(uint64_t bytes) {
   const DeviceSet &ds = device_set();
   return shard_count(bytes, ds.phys.empty() ? 1 : ds.phys.size(), shard_min_bytes());
@@ -1823,8 +1883,21 @@ int zcrc32_batch_device_strided(const void *d_base, uint64_t stride, uint64_t le
   // (at least one kDynUnit per wave): one stream-ordered 64-B allocation
   uint32_t *d_ctr = nullptr;
   const uint64_t waves = (uint64_t)dc->num_cus * kWaves;
-  if ((uint64_t)std::min(per, n) * len >> 2 >= waves * kDynUnit)  // len >= 512 KiB: a quarter
-    ZCRC_HIP_TRY(hipMallocAsync(reinterpret_cast<void **>(&d_ctr), kCtrBytes, st));
+  std::unique_lock<std::mutex> lk;  // held until the launches are queued (stream_scratch)
+  hipStreamCaptureStatus capst = hipStreamCaptureStatusNone;
+  ZCRC_HIP_TRY(hipStreamIsCapturing(st, &capst));
+  const bool capturing = capst != hipStreamCaptureStatusNone;
+  if ((uint64_t)std::min(per, n) * len >> 2 >= waves * kDynUnit) {  // len >= 512 KiB: a quarter
+    if (capturing) {  // stream-ordered under graph capture
+      ZCRC_HIP_TRY(hipMallocAsync(reinterpret_cast<void **>(&d_ctr), kCtrBytes, st));
+    } else {  // the stream's cached counter (a per-call hipMallocAsync: DESIGN.md 7d)
+      void *p = nullptr;
+      size_t have = 0;
+      rc = stream_scratch(st, kScratchStridedCtr, kCtrBytes, &p, &have, &lk);
+      if (rc) return rc;
+      d_ctr = static_cast<uint32_t *>(p);
+    }
+  }
   for (size_t first = 0; first < n; first += per) {
     const size_t cnt = std::min(per, n - first);
     BatchArgs a{};
@@ -1844,7 +1917,7 @@ int zcrc32_batch_device_strided(const void *d_base, uint64_t stride, uint64_t le
     rc = launch_main(a, true, *dc, st);
     if (rc) break;
   }
-  if (d_ctr) {
+  if (d_ctr && capturing) {
     const hipError_t e = hipFreeAsync(d_ctr, st);
     if (!rc && e != hipSuccess) return fail(ZCRC_ERR_HIP, std::string("hipFreeAsync: ") + hipGetErrorString(e));
   }
@@ -2013,10 +2086,12 @@ int inflate_host_group(const void *const *src, const size_t *src_len, void *cons
     }
     for (size_t r = 0; r < best_k; r++) run_if[ord[r]] = 0u;
   }
-  void *d_in = nullptr, *d_out = nullptr, *d_desc = nullptr;
-  ZCRC_HIP_TRY(hipMallocAsync(&d_in, in + 16, st));
-  ZCRC_HIP_TRY(hipMallocAsync(&d_out, out + 16, st));
-  ZCRC_HIP_TRY(hipMallocAsync(&d_desc, 8 * 5 * m + 8 * m + 4 * m, st));
+  // one thread-local device buffer: input | output | descriptors (zcrc_runtime.h)
+  const size_t in_b = (in + 16 + 255) & ~size_t(255), out_b = (out + 16 + 255) & ~size_t(255);
+  void *dbuf = nullptr;
+  rc = tl_device_buffer(kTlInflateHost, in_b + out_b + 8 * 5 * m + 8 * m + 4 * m, &dbuf);
+  if (rc) return rc;
+  void *d_in = dbuf, *d_out = static_cast<uint8_t *>(dbuf) + in_b, *d_desc = static_cast<uint8_t *>(dbuf) + in_b + out_b;
   for (size_t j = 0; j < m; j++) {
     h[j] += reinterpret_cast<uint64_t>(d_in);
     h[2 * m + j] += reinterpret_cast<uint64_t>(d_out);
@@ -2051,10 +2126,8 @@ int inflate_host_group(const void *const *src, const size_t *src_len, void *cons
     ZCRC_HIP_TRY(hipMemcpyAsync(stv.data(), d_status, 4 * m, hipMemcpyDeviceToHost, st));
     ZCRC_HIP_TRY(hipMemcpyAsync(crcv.data(), d_crc, 4 * m, hipMemcpyDeviceToHost, st));
   }
-  (void)hipFreeAsync(d_desc, st);
-  (void)hipFreeAsync(d_out, st);
-  (void)hipFreeAsync(d_in, st);
   ZCRC_HIP_TRY(hipStreamSynchronize(st));
+  tl_device_trim(kTlInflateHost, 4ull << 30);  // keep up to 4 GiB for the thread's next call
   if (rc) return rc;
   po = 0;
   jobs.clear();

@@ -173,12 +173,10 @@ int verify_deflated_chunk(const uint8_t *d_archive, zcrc_zip_entry *entries, con
     h[3 * m + j] = inflate_room(E);  // <= kArenaBytes: the chunking below guarantees it
     arena_bytes += h[3 * m + j];
   }
+  // thread-local device buffers (zcrc_runtime.h; this call synchronizes before it returns)
   void *d_arena = nullptr, *d_desc = nullptr;
-  if (hipMallocAsync(&d_arena, arena_bytes + 16, st) != hipSuccess) return zfail("inflate arena allocation failed");
-  if (hipMallocAsync(&d_desc, 8 * 5 * m + 8 * m, st) != hipSuccess) {
-    (void)hipFreeAsync(d_arena, st);
-    return zfail("inflate descriptor allocation failed");
-  }
+  if (zcrc::tl_device_buffer(zcrc::kTlZipArena, arena_bytes + 16, &d_arena)) return zfail("inflate arena allocation failed");
+  if (zcrc::tl_device_buffer(zcrc::kTlZipDesc, 8 * 5 * m + 8 * m, &d_desc)) return zfail("inflate descriptor allocation failed");
   for (size_t j = 0; j < m; j++) h[2 * m + j] += reinterpret_cast<uint64_t>(d_arena);
   uint64_t *dd = static_cast<uint64_t *>(d_desc);
   uint64_t *d_src = dd, *d_srclen = dd + m, *d_dst = dd + 2 * m, *d_cap = dd + 3 * m, *d_olen = dd + 4 * m;
@@ -199,9 +197,8 @@ int verify_deflated_chunk(const uint8_t *d_archive, zcrc_zip_entry *entries, con
               hipMemcpyAsync(status.data(), d_status, 4 * m, hipMemcpyDeviceToHost, st) != hipSuccess ||
               hipMemcpyAsync(crc.data(), d_crc, 4 * m, hipMemcpyDeviceToHost, st) != hipSuccess))
     rc = zfail("result download failed");
-  (void)hipFreeAsync(d_desc, st);
-  (void)hipFreeAsync(d_arena, st);
-  if (!rc && hipStreamSynchronize(st) != hipSuccess) rc = zfail("stream synchronize failed");
+  if (hipStreamSynchronize(st) != hipSuccess && !rc) rc = zfail("stream synchronize failed");
+  zcrc::tl_device_trim(zcrc::kTlZipArena, 1ull << 30);  // arenas above 1 GiB are not kept
   if (rc) return rc;
   for (size_t j = 0; j < m; j++) {
     zcrc_zip_entry &E = entries[idx[a + j]];
@@ -305,7 +302,7 @@ extern "C" int zcrc_zip_extract_stored_device(const void *d_archive, size_t arch
   if (m > 0xFFFFFFFFu || tiles > 0x7FFFFFFFu) return zfail("too many entries for one extraction");
   void *dv = nullptr;
   const size_t bytes = 8 * 3 * m + 4 * m + 8 * tiles + 4 * tiles;
-  if (hipMallocAsync(&dv, bytes, st) != hipSuccess) return zfail("hipMallocAsync failed");
+  if (zcrc::tl_device_buffer(zcrc::kTlZipCopy, bytes, &dv)) return zfail("descriptor allocation failed");
   uint64_t *d_src = static_cast<uint64_t *>(dv), *d_dstp = d_src + m, *d_len = d_dstp + m;
   uint64_t *d_tfirst = d_len + m;
   uint32_t *d_crc = reinterpret_cast<uint32_t *>(d_tfirst + tiles), *d_trange = d_crc + m;
@@ -326,8 +323,7 @@ extern "C" int zcrc_zip_extract_stored_device(const void *d_archive, size_t arch
   if (!rc) rc = zcrc32_batch_device(reinterpret_cast<const void *const *>(d_dstp), d_len, nullptr, d_crc, m, stream);
   if (!rc && hipMemcpyAsync(crc.data(), d_crc, 4 * m, hipMemcpyDeviceToHost, st) != hipSuccess)
     rc = zfail("result download failed");
-  (void)hipFreeAsync(dv, st);
-  if (!rc && hipStreamSynchronize(st) != hipSuccess) rc = zfail("stream synchronize failed");
+  if (hipStreamSynchronize(st) != hipSuccess && !rc) rc = zfail("stream synchronize failed");
   if (rc) return rc;
   finish(entries, idx, crc);
   return ZCRC_OK;
@@ -382,7 +378,7 @@ extern "C" int zcrc_zip_verify_device(const void *d_archive, size_t archive_len,
   if (!idx.empty()) {
     const size_t m = idx.size();
     void *d = nullptr;
-    if (hipMallocAsync(&d, m * 20, st) != hipSuccess) return zfail("hipMallocAsync failed");
+    if (zcrc::tl_device_buffer(zcrc::kTlZipDesc, m * 20, &d)) return zfail("descriptor allocation failed");
     uint64_t *dp = static_cast<uint64_t *>(d), *dl = dp + m;
     uint32_t *dout = reinterpret_cast<uint32_t *>(dl + m);
     int rc = ZCRC_OK;
@@ -392,8 +388,7 @@ extern "C" int zcrc_zip_verify_device(const void *d_archive, size_t archive_len,
     if (!rc) rc = zcrc32_batch_device(reinterpret_cast<const void *const *>(dp), dl, nullptr, dout, m, stream);
     if (!rc && hipMemcpyAsync(crc.data(), dout, 4 * m, hipMemcpyDeviceToHost, st) != hipSuccess)
       rc = zfail("result download failed");
-    (void)hipFreeAsync(d, st);
-    if (!rc && hipStreamSynchronize(st) != hipSuccess) rc = zfail("stream synchronize failed");
+    if (hipStreamSynchronize(st) != hipSuccess && !rc) rc = zfail("stream synchronize failed");
     if (rc) return rc;
   }
   finish(entries, idx, crc);
@@ -429,18 +424,17 @@ int verify_host_run(const uint8_t *archive, zcrc_zip_entry *entries, const std::
     local[k - a] = entries[idx[k]];
     local[k - a].data_offset -= lo;
   }
-  hipStream_t st = nullptr;
-  if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess) return zfail("stream create failed");
   const uint64_t len = hi - lo;
-  void *d = nullptr;
-  int rc = ZCRC_OK;
-  if (hipMallocAsync(&d, len ? len : 1, st) != hipSuccess) rc = zfail("archive allocation failed");
-  if (!rc && len && hipMemcpyAsync(d, archive + lo, len, hipMemcpyHostToDevice, st) != hipSuccess)
-    rc = zfail("archive upload failed");
-  if (!rc) rc = zcrc_zip_verify_device(d, len, local.data(), local.size(), st);
-  if (d) (void)hipFreeAsync(d, st);
-  (void)hipStreamSynchronize(st);
-  (void)hipStreamDestroy(st);
+  const int rc = zcrc::with_lease_stream([&](hipStream_t st) {
+    void *d = nullptr;
+    if (zcrc::tl_device_buffer(zcrc::kTlZipImage, len ? len : 1, &d)) return zfail("archive allocation failed");
+    if (len && hipMemcpyAsync(d, archive + lo, len, hipMemcpyHostToDevice, st) != hipSuccess)
+      return zfail("archive upload failed");
+    const int r = zcrc_zip_verify_device(d, len, local.data(), local.size(), st);
+    (void)hipStreamSynchronize(st);
+    zcrc::tl_device_trim(zcrc::kTlZipImage, 1ull << 30);
+    return r;
+  });
   if (rc) return rc;
   for (size_t k = a; k < b; k++) {
     zcrc_zip_entry &E = entries[idx[k]];
