@@ -329,6 +329,46 @@ def run_batch(batch: Batch, num_cus: int = 256, dyn_shift: int = K_DYN_SHIFT, un
     return out
 
 
+def run_one_launch(batch: Batch, num_cus: int = 256) -> np.ndarray:
+    """The one-launch kernel's round-4 per-buffer mode (zcrc_batch_kernel.h,
+    kPB = 4; n <= 16 x CUs): every buffer of at most kPerBufMax bytes is
+    checksummed whole by its own wave; when any buffer is longer, the
+    in-kernel scan runs over effective lengths (the short buffers count as
+    empty) and its walk skips the short buffers (skip_small), so every
+    buffer is computed exactly once."""
+    assert batch.n <= K_WAVES * num_cus
+    T = tables()
+    out = np.zeros(batch.n, dtype=np.uint32)
+    short = [L <= K_PER_BUF_MAX for L in batch.lens]
+    for i in range(batch.n):
+        if not short[i]:
+            continue
+        n, seed = batch.lens[i], batch.seeds[i]
+        if n < 4:
+            r = (~seed) & 0xFFFFFFFF
+            for p in range(n):
+                r = (r >> 8) ^ int(T.stdtab[(r ^ int(batch.mem[batch.addrs[i] + p])) & 0xFF])
+            out[i] = (~r) & 0xFFFFFFFF
+        else:
+            out[i] = (~crc_piece(batch.mem, batch.addrs[i], batch.addrs[i] + n, (~seed) & 0xFFFFFFFF, T)) & 0xFFFFFFFF
+    if all(short):
+        return out
+    eff = Batch(batch.mem, batch.addrs, [0 if sh else L for sh, L in zip(short, batch.lens)], batch.seeds)
+    for (s0, s1, last) in wave_ranges(eff, num_cus):
+        for (i, rel_lo, rel_hi) in wave_pieces(eff, s0, s1, last):
+            if short[i]:
+                continue  # skip_small
+            n, seed = batch.lens[i], batch.seeds[i]
+            inj = (~seed) & 0xFFFFFFFF if rel_lo == 0 else 0
+            r = crc_piece(batch.mem, batch.addrs[i] + rel_lo, batch.addrs[i] + rel_hi, inj, T)
+            if rel_lo == 0 and rel_hi == n:
+                out[i] = (~r) & 0xFFFFFFFF
+            else:
+                d = n - rel_hi
+                out[i] ^= np.uint32(gf2_mul(xpow8(d), r) if d else r ^ 0xFFFFFFFF)
+    return out
+
+
 # ------------------------------------------------------------ small-buffer kernel
 
 def crc_small_group(mem: np.ndarray, pstart: int, length: int, seed: int, G: int, T: Tables,

@@ -270,3 +270,22 @@ def test_xinv8_byte_table_inverts_one_zero_byte():
         fwd = (w >> 8) ^ int(T.stdtab[w & 0xFF])  # one zero byte forward
         assert fwd == r
 
+
+def test_one_launch_short_buffers_per_wave_long_ones_scanned():
+    """Round-4 per-buffer mode (kernel_model.run_one_launch): short buffers
+    (<= 64 KiB) whole per wave, the long ones through the in-kernel scan over
+    effective lengths with the short ones skipped -- every CRC equals the
+    oracle's, with seeds, tiny and empty buffers, and splits of the long ones."""
+    from oracle import oracle as o
+    rng = np.random.default_rng(11)
+    lens = [0, 1, 3, 4, 100, 65536, 65537, 300_001, 5, 200_000, 70_000, 65535, 17]
+    offs = np.zeros(len(lens), dtype=np.int64)
+    offs[1:] = np.cumsum(np.array(lens) + 5)[:-1]
+    mem = rng.integers(0, 256, int(offs[-1] + lens[-1] + 64), dtype=np.uint8)
+    seeds = [int(x) for x in rng.integers(0, 1 << 32, len(lens), dtype=np.uint64)]
+    b = km.Batch(mem, offs + 3, lens, seeds)
+    got = km.run_one_launch(b, num_cus=4)  # 4 CUs: the long buffers split across waves
+    exp = o.crc32_batch((mem.ctypes.data + offs + 3).astype(np.uint64), np.array(lens, dtype=np.uint64),
+                        np.array(seeds, dtype=np.uint32))
+    np.testing.assert_array_equal(got, exp)
+
