@@ -439,12 +439,14 @@ K_SMALL_MAX = 8192
 K_SIZE_CLASSES = K_SMALL_MAX // 256 + 1
 K_SMALL_COST = 14  # zcrc_internal.h kSmallCostDefault (quarters of a batch-kernel byte)
 K_BIG_MIN = 1 << 20  # zcrc_internal.h kBigMin
+K_SPLIT_PER_THREAD = 8  # zcrc_internal.h kSplitPerThread
+K_SPLIT_TILE = 1024 * K_SPLIT_PER_THREAD  # buffers per split-plan tile (kSplitTile)
 
 
 def split_plan(lens, grid: int = 256, force: bool = False, small_cost: int = K_SMALL_COST, direct_ok: bool = True):
     """zcrc_kernels.hip plan_split_scatter's decisions and lists: (split,
     large list -- on a split, buffers below kBigMin first, then the others,
-    each in index order -- with its prefix, small list tile by tile (8192
+    each in index order -- with its prefix, small list tile by tile (K_SPLIT_TILE
     buffers), by size class within a tile and in index order within a class,
     small workgroups, small lanes)."""
     lens = [int(x) for x in lens]
@@ -461,7 +463,7 @@ def split_plan(lens, grid: int = 256, force: bool = False, small_cost: int = K_S
         wgs = min(max(wgs, 1), grid - 1)
     if not split:
         return dict(split=False, large=list(range(len(lens))), small=[], wgs=wgs, lanes=16)
-    by_class = sorted(small, key=lambda i: (i // 8192, (lens[i] + 255) >> 8, i))
+    by_class = sorted(small, key=lambda i: (i // K_SPLIT_TILE, (lens[i] + 255) >> 8, i))
     lanes = 8 if as_ <= 2048 * len(small) else 16
     if not large and direct_ok:  # mode 2: about equal small buffers, walked in index order without lists
         mean = as_ / len(small)

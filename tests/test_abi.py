@@ -164,9 +164,11 @@ def test_argument_errors_are_reported_not_computed():
     assert lib.zcrc32_checked(None, 10, 0, ctypes.byref(out)) == -2
     assert b"null" in lib.zcrc_last_error()
     assert lib.zcrc32_batch_device_scratch_bytes(8192) == 256 + 8 * 8193 + 8  # counter line | prefix | one plan tile
-    # above kFusedMaxN the split plan's layout: counters | prefix | 6 tile words x 2 tiles | tile prefixes
-    # 6 x (2 + 1) | ptrs | seeds, oidx | small-list descriptors (16 B, 16-B aligned)
-    head = 256 + 8 * 8194 + 8 * 6 * 2 + 8 * 6 * 3 + 8 * 8193 + 8 * 8193
+    # above kFusedMaxN the split plan's layout: counters | prefix | 6 tile words x T tiles | tile prefixes
+    # 6 x (T + 1) | ptrs | seeds, oidx | small-list descriptors (16 B, 16-B aligned)
+    import kernel_model as km
+    T = -(-8193 // km.K_SPLIT_TILE)
+    head = 256 + 8 * 8194 + 8 * 6 * T + 8 * 6 * (T + 1) + 8 * 8193 + 8 * 8193
     assert lib.zcrc32_batch_device_scratch_bytes(8193) == (head + 15) // 16 * 16 + 16 * 8193
 
 

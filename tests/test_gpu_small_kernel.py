@@ -307,8 +307,9 @@ def _split_lists(scratch, n):
     """The split plan's outputs in caller-owned scratch (SplitScratch,
     zcrc_runtime.hip): counts, prefix_c, oidx, and the small list's buffer
     indices (word 2 of each 16-B descriptor), pointers and lengths."""
+    import kernel_model as km
     raw = scratch.cpu().numpy()
-    T = -(-n // 8192)
+    T = -(-n // km.K_SPLIT_TILE)
     prefix = 256
     tiles = prefix + 8 * (n + 1)
     tile_pre = tiles + 48 * T  # kTileWords = 6

@@ -1,6 +1,7 @@
 """CPU checks of the kernel's decomposition (tests/kernel_model.py mirrors
 zcrc_kernels.hip step by step) against the oracle, plus partition
 invariants of the wave-range snapping.  No GPU needed."""
+import os
 import random
 import zlib
 
@@ -289,3 +290,24 @@ def test_one_launch_short_buffers_per_wave_long_ones_scanned():
                         np.array(seeds, dtype=np.uint32))
     np.testing.assert_array_equal(got, exp)
 
+
+
+def test_model_constants_mirror_the_header():
+    """tests/kernel_model.py's K_* constants equal zcrc_internal.h's (the
+    header is parsed as text: `constexpr <type> kName = <expr>;`)."""
+    import re
+    src = open(os.path.join(os.path.dirname(__file__), "..", "zipsfs_amd", "csrc", "zcrc_internal.h")).read()
+    vals = {}
+    for name, expr in re.findall(r"constexpr\s+[\w:]+\s+(k\w+)\s*=\s*([^;]+);", src):
+        e = re.sub(r"(\d+)u?ll|(\d+)u\b", lambda m: m.group(1) or m.group(2), expr)
+        try:
+            vals[name] = eval(e, {}, dict(vals))  # noqa: S307 -- our own header's integer expressions
+        except Exception:
+            pass
+    pairs = {"kWaves": km.K_WAVES, "kMinRange": km.K_MIN_RANGE, "kSplitGrain": km.K_SPLIT_GRAIN,
+             "kSplitMin": km.K_SPLIT_MIN, "kMinPiece": km.K_MIN_PIECE, "kDynUnit": km.K_DYN_UNIT,
+             "kDynAuto": km.K_DYN_AUTO, "kDynSmallAvg": km.K_DYN_SMALL_AVG, "kSmallMax": km.K_SMALL_MAX,
+             "kBigMin": km.K_BIG_MIN, "kSmallCostDefault": km.K_SMALL_COST,
+             "kSplitPerThread": km.K_SPLIT_PER_THREAD, "kSplitTile": km.K_SPLIT_TILE}
+    for name, model in pairs.items():
+        assert vals.get(name) == model, (name, vals.get(name), model)

@@ -75,10 +75,17 @@ __global__ __launch_bounds__(1024) void probe_wave(const uint8_t *base, uint64_t
 // s * grid + g), 2 x 4 KiB ping-pong like the CRC loop; kRot: each wave
 // starts at a hashed block of its buffer and wraps (the pure-read cost of a
 // de-phased visit order)
-template <bool kRot, bool kPrio = true>
+// kFat: ~kFat straight-line VALU instructions (no memory) before the first
+// load -- does a long prologue of code alone delay a launch's first loads
+// (instruction fetch from a cold instruction cache)?
+template <bool kRot, bool kPrio = true, int kFat = 0>
 __global__ __launch_bounds__(1024) void probe_pb(const uint8_t *base, uint64_t per, uint32_t *out) {
   const uint32_t lane = threadIdx.x & 63u, slot = threadIdx.x >> 6;
   const uint64_t w = (uint64_t)slot * gridDim.x + blockIdx.x;
+  uint32_t fat = lane;
+#pragma unroll
+  for (int f = 0; f < kFat; f++) fat = __builtin_amdgcn_alignbit(fat, fat ^ (uint32_t)(0x9E3779B9u * (f + 1)), 7);
+  if (kFat && fat == 0x12345678u) out[w ^ 1] = fat;  // keep it
   if (kPrio) {
     if (slot >= 12) __builtin_amdgcn_s_setprio(3);
     else if (slot >= 8) __builtin_amdgcn_s_setprio(2);
@@ -184,9 +191,9 @@ int main(int argc, char **argv) {
   std::vector<hipEvent_t> ev(2 * kBatches);
   for (auto &e : ev) CHECK(hipEventCreate(&e));
   enum { kProbeWave, kProbeGrid, kCrc, kCrcFused, kCrcFusedR3, kCrcFused5, kProbePb, kProbePbRot, kProbePbNoPrio,
-         kNumV };
+         kProbePbFat, kNumV };
   const char *names[kNumV] = {"probe-wave", "probe-grid", "crc", "crc-fused", "crc-fused-r3", "crc-fused-5", "probe-pb",
-                              "probe-pb-rot", "probe-pb-np"};
+                              "probe-pb-rot", "probe-pb-np", "probe-pb-fat"};
   auto launch = [&](int v, int b, hipEvent_t e0, hipEvent_t e1) {
     const uint8_t *base = data + b * kBatchBytes;
     switch (v) {
@@ -204,6 +211,9 @@ int main(int argc, char **argv) {
         break;
       case kProbePbNoPrio:
         hipExtLaunchKernelGGL((probe_pb<false, false>), dim3(cus), dim3(1024), 0, 0, e0, e1, 0, base, kLen, out);
+        break;
+      case kProbePbFat:  // ~600 instructions (~5 KB of code) in front of the loads
+        hipExtLaunchKernelGGL((probe_pb<false, true, 600>), dim3(cus), dim3(1024), 0, 0, e0, e1, 0, base, kLen, out);
         break;
       case kCrc:
         hipExtLaunchKernelGGL((crc32_batch_kernel<false, kDepth, 0>), dim3(cus), dim3(kThreads), 0, 0, e0, e1, 0,

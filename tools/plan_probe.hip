@@ -4,8 +4,10 @@
 // launches (events around the loop), then one launch with the scatter's
 // diagnostic phase stamps (SplitPlan::stamps, s_memrealtime at 100 MHz):
 // loads + tile sums | decision | scans and ballots | class scan | stores.
+// One JSON line per tile size (1024 x per buffers per workgroup, per = 8, 4,
+// 2, 1; the product's is kSplitPerThread), interleaved over `rounds`.
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 -o plan_probe plan_probe.hip
-//   plan_probe [n] [len|0=config-4 law] [reps]
+//   plan_probe [n] [len|0=config-4 law] [reps] [rounds]
 #include "../zipsfs_amd/csrc/zcrc_kernels.hip"
 
 #include <vector>
@@ -35,6 +37,7 @@ int main(int argc, char **argv) {
   const uint64_t n = argc > 1 ? strtoull(argv[1], 0, 0) : 100000;
   const uint64_t len = argc > 2 ? strtoull(argv[2], 0, 0) : 0;
   const int reps = argc > 3 ? atoi(argv[3]) : 50;
+  const int rounds = argc > 4 ? atoi(argv[4]) : 1;
   std::vector<uint64_t> lens(n), ptrs(n);
   uint64_t off = 0;
   for (uint64_t i = 0; i < n; i++) {
@@ -42,7 +45,7 @@ int main(int argc, char **argv) {
     ptrs[i] = 0x100000000ull + off;  // never dereferenced by the plan
     off += (lens[i] + 15) & ~15ull;
   }
-  const uint64_t tiles = plan_tiles(n);
+  const uint64_t tiles = n == 0 ? 1 : (n + 1023) / 1024;  // the most tiles (per = 1): scratch and stamps
   uint64_t *d_lens, *d_ptrs, *d_stamps;
   uint8_t *scratch;
   uint32_t *d_out;
@@ -76,35 +79,51 @@ int main(int argc, char **argv) {
   p.small_cost = kSmallCostDefault;
   p.big_min = kBigMin;
   p.direct_ok = getenv("ZCRC_SMALL_DIRECT") == nullptr || getenv("ZCRC_SMALL_DIRECT")[0] != '0';
-  for (int r = 0; r < 5; r++) CK(launch_plan_split(p, 0));
-  hipEvent_t e0, e1;
-  CK(hipEventCreate(&e0));
-  CK(hipEventCreate(&e1));
-  CK(hipEventRecord(e0, 0));
-  for (int r = 0; r < reps; r++) CK(launch_plan_split(p, 0));
-  CK(hipEventRecord(e1, 0));
-  CK(hipEventSynchronize(e1));
-  float ms = 0;
-  CK(hipEventElapsedTime(&ms, e0, e1));
-  p.stamps = d_stamps;
-  CK(launch_plan_split(p, 0));
-  CK(hipDeviceSynchronize());
-  std::vector<uint64_t> st(8 * tiles);
-  CK(hipMemcpy(st.data(), d_stamps, 64 * tiles, hipMemcpyDeviceToHost));
-  uint64_t t0 = ~0ull, tend = 0;
-  double ph[5] = {0, 0, 0, 0, 0};
-  for (uint64_t b = 0; b < tiles; b++) {
-    t0 = std::min(t0, st[8 * b]);
-    tend = std::max(tend, st[8 * b + 5]);
-    for (int i = 0; i < 5; i++) ph[i] += (double)(st[8 * b + i + 1] - st[8 * b + i]) * 0.01 / tiles;  // 100 MHz -> us
-  }
-  uint64_t counts[5];
-  CK(hipMemcpy(counts, scratch + 128, 40, hipMemcpyDeviceToHost));
-  printf("{\"n\": %llu, \"len\": %llu, \"tiles\": %llu, \"plan_us\": %.2f, \"split\": %llu, \"n_large\": %llu, "
-         "\"n_small\": %llu, \"scatter_span_us\": %.2f, \"phase_us\": {\"loads_tiles\": %.2f, \"decision\": %.2f, "
-         "\"scans_ballots\": %.2f, \"class_scan\": %.2f, \"stores\": %.2f}}\n",
-         (unsigned long long)n, (unsigned long long)len, (unsigned long long)tiles, ms * 1e3 / reps,
-         (unsigned long long)counts[2], (unsigned long long)counts[0], (unsigned long long)counts[1],
-         (double)(tend - t0) * 0.01, ph[0], ph[1], ph[2], ph[3], ph[4]);
+  auto run = [&](int per) {
+    auto launch = [&]() {
+      switch (per) {
+        case 8: CK(launch_plan_split_t<8>(p, 0)); break;
+        case 4: CK(launch_plan_split_t<4>(p, 0)); break;
+        case 2: CK(launch_plan_split_t<2>(p, 0)); break;
+        default: CK(launch_plan_split_t<1>(p, 0)); break;
+      }
+    };
+    const uint64_t nt = n == 0 ? 1 : (n + 1024u * per - 1) / (1024u * per);
+    p.stamps = nullptr;
+    for (int r = 0; r < 5; r++) launch();
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+    CK(hipEventRecord(e0, 0));
+    for (int r = 0; r < reps; r++) launch();
+    CK(hipEventRecord(e1, 0));
+    CK(hipEventSynchronize(e1));
+    float ms = 0;
+    CK(hipEventElapsedTime(&ms, e0, e1));
+    p.stamps = d_stamps;
+    launch();
+    CK(hipDeviceSynchronize());
+    std::vector<uint64_t> st(8 * nt);
+    CK(hipMemcpy(st.data(), d_stamps, 64 * nt, hipMemcpyDeviceToHost));
+    uint64_t t0 = ~0ull, tend = 0;
+    double ph[5] = {0, 0, 0, 0, 0};
+    for (uint64_t b = 0; b < nt; b++) {
+      t0 = std::min(t0, st[8 * b]);
+      tend = std::max(tend, st[8 * b + 5]);
+      for (int i = 0; i < 5; i++) ph[i] += (double)(st[8 * b + i + 1] - st[8 * b + i]) * 0.01 / nt;  // 100 MHz -> us
+    }
+    uint64_t counts[5];
+    CK(hipMemcpy(counts, scratch + 128, 40, hipMemcpyDeviceToHost));
+    printf("{\"n\": %llu, \"len\": %llu, \"per\": %d, \"tiles\": %llu, \"plan_us\": %.2f, \"split\": %llu, "
+           "\"n_large\": %llu, \"n_small\": %llu, \"scatter_span_us\": %.2f, \"phase_us\": {\"loads_tiles\": %.2f, "
+           "\"decision\": %.2f, \"scans_ballots\": %.2f, \"class_scan\": %.2f, \"stores\": %.2f}}\n",
+           (unsigned long long)n, (unsigned long long)len, per, (unsigned long long)nt, ms * 1e3 / reps,
+           (unsigned long long)counts[2], (unsigned long long)counts[0], (unsigned long long)counts[1],
+           (double)(tend - t0) * 0.01, ph[0], ph[1], ph[2], ph[3], ph[4]);
+    CK(hipEventDestroy(e0));
+    CK(hipEventDestroy(e1));
+  };
+  for (int r = 0; r < rounds; r++)
+    for (int per : {8, 4, 2, 1}) run(per);
   return 0;
 }

@@ -27,9 +27,11 @@ step harness_text17.log 200 env ZCRC_SPLIT_TRACE=1 ZCRC_PRELOAD_DEFLATED=$USIZE 
 PYT="python3 -u -m pytest -x -v --timeout 300 --timeout-method thread"
 step pytest_focus.log 600 $PYT tests/test_gpu_preload.py tests/test_gpu_inflate.py tests/test_gpu_inflate_split.py tests/test_gpu_small_kernel.py tests/test_gpu_parity.py -k "deflated or inflate or zip or direct or split_plan or strided or per_buffer or fused"
 step pytest_gpu.log 900 $PYT tests -m gpu
+step c4_probe_first.txt 240 tools/c4_probe 2 20
 step c2_probe.txt 120 tools/c2_probe 48
 for r in 1 2; do
   step small_pre_$r.jsonl 300 python3 tools/run_with_lib.py ablibs/pre/zipsfs_amd/libzcrc.so tools/small_batches.py 10 1024,2048,3000,4096
   step small_nodirect_$r.jsonl 300 env ZCRC_SMALL_DIRECT=0 python3 tools/small_batches.py 10 1024,2048,3000,4096
   step small_new_$r.jsonl 300 python3 tools/small_batches.py 10 1024,2048,3000,4096
 done
+step c4_probe.txt 240 tools/c4_probe 4 20

@@ -832,8 +832,15 @@ __global__ __launch_bounds__(kThreads) void crc32_batch_kernel(BatchArgs args) {
         sa.tab = args.tab;
         const uint64_t ns = uni64(args.n_dev[1]);
         const uint32_t blk = blockIdx.x - (gridDim.x - nsm);
+        const uint64_t t_small = kStamp ? __builtin_amdgcn_s_memrealtime() : 0;
         if (uni64(args.n_dev[3]) == 8) small_body<false, 8, 4>(sa, s_lds, ns, blk, nsm);
         else small_body<false, 16, 8>(sa, s_lds, ns, blk, nsm);
+        if (kStamp && (threadIdx.x & 63u) == 0) {  // diagnostic build: a small-list wave (npieces ~0)
+          const uint64_t w = (uint64_t)blockIdx.x * kWaves + (threadIdx.x >> 6);
+          args.stamps[8 * w + 0] = args.stamps[8 * w + 4] = t_small;
+          args.stamps[8 * w + 1] = __builtin_amdgcn_s_memrealtime();
+          args.stamps[8 * w + 2] = ~0ull;
+        }
         return;  // uniform per workgroup: no barrier is skipped
       }
       grid -= nsm;
@@ -1178,8 +1185,8 @@ __global__ __launch_bounds__(kThreads) void crc32_batch_kernel(BatchArgs args) {
   // held-but-unstarted unit would become a straggler.
   uint32_t u = 0, nx = 0;
   bool have_next = false, first_claim = true;
-  uint64_t t_unit_search = 0, t_unit_drain = 0;  // diagnostic build: time in the unit range searches
-  uint64_t t_tail = 0;                              // ... and in the alignment-padding MCTs
+  uint64_t t_tail = 0;                 // diagnostic build: time in the alignment-padding MCTs (unused)
+  uint64_t t_static_end = 0, n_dyn = 0;  // ... the static range's end, dynamic units taken
   for (;;) {
     if (!band && u + 2 * (uint32_t)W < units) {
       if (lane == 0) nx = (uint32_t)W + atomicAdd(args.ctr, 1u);
@@ -1188,6 +1195,7 @@ __global__ __launch_bounds__(kThreads) void crc32_batch_kernel(BatchArgs args) {
     if (S0 < S1 || last)
       npieces += process_range<kStrided, kD, kAblate, kRotate, kPrio, kAux, kStamp, kFused, kWin>(
           args, bv, s_lds, tab, S0, S1, last, salt, lane, band, f0, lb1, &t_tail, perbuf_done);
+    if (kStamp && first_claim) t_static_end = __builtin_amdgcn_s_memrealtime();
     if (!units) break;
     if (first_claim) {
       nx = (uint32_t)w;  // units >= W whenever the dynamic part is on
@@ -1202,15 +1210,8 @@ __global__ __launch_bounds__(kThreads) void crc32_batch_kernel(BatchArgs args) {
     if (u >= units) break;
     const uint64_t t0 = Ts + (uint64_t)u * unit;
     last = (u + 1 == units);
-    uint64_t ts0 = 0;
-    if (kStamp) {  // split the search time into draining the previous piece's stores/atomics and the search
-      const uint64_t tw = __builtin_amdgcn_s_memrealtime();
-      __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
-      ts0 = __builtin_amdgcn_s_memrealtime();
-      t_unit_drain += ts0 - tw;
-    }
+    if (kStamp) n_dyn++;
     bv.range(t0, t0 + unit, last, S0, S1, f0, lb1);
-    if (kStamp) t_unit_search += __builtin_amdgcn_s_memrealtime() - ts0;
     salt = u ^ 0x9E3779B9u;
     if (kPrio && band) __builtin_amdgcn_s_setprio(0);
     band = false;
@@ -1224,16 +1225,15 @@ __global__ __launch_bounds__(kThreads) void crc32_batch_kernel(BatchArgs args) {
       atomicExch(args.done, 0u);
     }
   }
-  if (kStamp && lane == 0) {
+  if (kStamp && lane == 0) {  // (tools/c2_probe, tools/c4_probe)
     args.stamps[8 * w + 0] = t_begin;
     args.stamps[8 * w + 1] = __builtin_amdgcn_s_memrealtime();
     args.stamps[8 * w + 2] = npieces;
-    args.stamps[8 * w + 3] = static_bytes;
+    args.stamps[8 * w + 3] = t_static_end;
     args.stamps[8 * w + 4] = t_entry;
     args.stamps[8 * w + 5] = t_search;
-    args.stamps[8 * w + 6] = t_unit_search;
-    args.stamps[8 * w + 7] = t_unit_drain;
-    args.stamps[8 * w + 3] = t_tail;  // (replaces the static byte count in this build)
+    args.stamps[8 * w + 6] = n_dyn;
+    args.stamps[8 * w + 7] = static_bytes;
   }
 }
 

@@ -154,6 +154,12 @@ constexpr uint32_t kSizeClasses = kSmallMax / 256 + 1;  // small list order: 256
 constexpr uint32_t kTileWords = 6;
 constexpr uint64_t kBigMin = 1ull << 20;  // split plan: buffers of at least this go last in the batch kernel's order
 constexpr uint64_t kPlanDirectTiles = 512;  // up to this many tiles each scatter workgroup sums the tile words itself
+// split plan tiles: 1024 * kSplitPerThread buffers per plan_split_count /
+// plan_split_scatter workgroup (the small list is ordered by size class
+// tile by tile)
+constexpr uint32_t kSplitPerThread = 8;
+constexpr uint64_t kSplitTile = 1024u * kSplitPerThread;
+inline uint64_t split_tiles(uint64_t n) { return n == 0 ? 1 : (n + kSplitTile - 1) / kSplitTile; }
 constexpr uint32_t kSmallCostDefault = 14;  // 3.5 batch-kernel bytes (zcrc_kernels.hip, plan_split_scatter)
 
 }  // namespace zcrc

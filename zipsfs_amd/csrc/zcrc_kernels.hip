@@ -144,19 +144,20 @@ __global__ __launch_bounds__(1024) void plan_one_tile(const uint64_t *lens, uint
 
 __device__ __forceinline__ uint32_t size_class(uint64_t len) { return (uint32_t)((len + 255) >> 8); }  // 256-B blocks
 
+template <uint32_t kPer>
 __global__ __launch_bounds__(1024) void plan_split_count(SplitPlan p) {
   __shared__ uint64_t s_w[16][kTileWords];
   const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
-  const uint64_t base = (uint64_t)blockIdx.x * kPlanTile + 512u * wv + lane;
-  uint64_t lv[kPlanPerThread];
+  const uint64_t base = (uint64_t)blockIdx.x * (1024u * kPer) + 64u * kPer * wv + lane;
+  uint64_t lv[kPer];
 #pragma unroll
-  for (uint32_t k = 0; k < kPlanPerThread; k++) {
+  for (uint32_t k = 0; k < kPer; k++) {
     const uint64_t idx = base + 64u * k;
     lv[k] = idx < p.n ? p.lens[idx] : ~0ull;  // ~0: absent
   }
   uint64_t bm = 0, bb = 0, bs = 0, cmb = 0, cs = 0, sq = 0;
 #pragma unroll
-  for (uint32_t k = 0; k < kPlanPerThread; k++) {
+  for (uint32_t k = 0; k < kPer; k++) {
     const uint64_t L = lv[k];
     if (L == ~0ull) continue;
     if (L <= kSmallMax) bs += L, cs += 1, sq += L * L;
@@ -200,8 +201,9 @@ __global__ __launch_bounds__(1024) void plan_split_tiles(SplitPlan p, uint32_t t
   }
 }
 
+template <uint32_t kPer>
 __global__ __launch_bounds__(1024) void plan_split_scatter(SplitPlan p) {
-  constexpr uint32_t kGroups = 16 * kPlanPerThread;  // (wave, k) groups of 64 buffers per tile
+  constexpr uint32_t kGroups = 16 * kPer;  // (wave, k) groups of 64 buffers per tile
   __shared__ uint64_t s_tw[kTileWords][2];           // tile words: earlier tiles, all tiles
   __shared__ uint64_t s_wb[16][2];                   // wave byte totals: medium, big
   __shared__ uint32_t s_wc[16][2];                   // wave counts: medium, big
@@ -213,12 +215,12 @@ __global__ __launch_bounds__(1024) void plan_split_scatter(SplitPlan p) {
   uint64_t st[6] = {0, 0, 0, 0, 0, 0};  // diagnostics: phase stamps (p.stamps)
   if (p.stamps) st[0] = __builtin_amdgcn_s_memrealtime();
   if (blockIdx.x == 0 && tid == 0) p.ctr[0] = 0u, p.ctr[kFaultByte / 4] = 0u;  // work counter, fault word
-  const uint64_t base = (uint64_t)blockIdx.x * kPlanTile + 512u * wv + lane;
+  const uint64_t base = (uint64_t)blockIdx.x * (1024u * kPer) + 64u * kPer * wv + lane;
   // this thread's lengths first (coalesced); pointers and seeds are loaded
   // for the stores at the end (holding them from here spilled 61 VGPRs)
-  uint64_t v[kPlanPerThread];
+  uint64_t v[kPer];
 #pragma unroll
-  for (uint32_t k = 0; k < kPlanPerThread; k++) {
+  for (uint32_t k = 0; k < kPer; k++) {
     const uint64_t idx = base + 64u * k;
     v[k] = idx < p.n ? p.lens[idx] : 0;
   }
@@ -287,10 +289,10 @@ __global__ __launch_bounds__(1024) void plan_split_scatter(SplitPlan p) {
   // within the wave's class and one packed word: the count offset within
   // the wave's class (bits 0-9), the size class (10-15; 63: the batch
   // kernel's), the rank within the (wave, k) group's class (16-21), big (22).
-  uint64_t ex[kPlanPerThread], cmry = 0, cbry = 0;
-  uint32_t meta[kPlanPerThread], ccm = 0, ccb = 0;
+  uint64_t ex[kPer], cmry = 0, cbry = 0;
+  uint32_t meta[kPer], ccm = 0, ccb = 0;
 #pragma unroll
-  for (uint32_t k = 0; k < kPlanPerThread; k++) {
+  for (uint32_t k = 0; k < kPer; k++) {
     const bool in = base + 64u * k < p.n;
     const bool large = in && (!split || v[k] > kSmallMax);
     const bool big = large && split && v[k] >= p.big_min;
@@ -314,7 +316,7 @@ __global__ __launch_bounds__(1024) void plan_split_scatter(SplitPlan p) {
         match &= ((cls >> bit) & 1u) ? b : ~b;
       }
       rank = (uint32_t)__popcll(match & lt);
-      if (cls < kSizeClasses && rank == 0) s_cls[cls * kGroups + wv * kPlanPerThread + k] = (uint32_t)__popcll(match);
+      if (cls < kSizeClasses && rank == 0) s_cls[cls * kGroups + wv * kPer + k] = (uint32_t)__popcll(match);
     }
     meta[k] = cx | (cls << 10) | (rank << 16) | ((uint32_t)big << 22);
   }
@@ -327,25 +329,25 @@ __global__ __launch_bounds__(1024) void plan_split_scatter(SplitPlan p) {
   // first position and byte of this wave's medium (or, unsplit, all) and big buffers
   const uint64_t ec = s_tw[3][0];  // earlier tiles' medium | big counts
   const uint64_t bm0 = (split ? s_tw[0][0] : s_tw[0][0] + s_tw[1][0] + s_tw[2][0]) + bom;
-  const uint64_t cm0 = (split ? (ec & 0xFFFFFFFFull) : (uint64_t)blockIdx.x * kPlanTile) + com;
+  const uint64_t cm0 = (split ? (ec & 0xFFFFFFFFull) : (uint64_t)blockIdx.x * (1024u * kPer)) + com;
   const uint64_t bb0 = am + s_tw[1][0] + bob;
   const uint64_t cb0 = n_med + (ec >> 32) + cob;
   if (split) {
-    // exclusive positions over (class, wave, k): thread t scans 5 consecutive entries
-    constexpr uint32_t kPer = (kSizeClasses * kGroups + 1023) / 1024;
-    uint32_t loc[kPer];
+    // exclusive positions over (class, wave, k): thread t scans kEnt consecutive entries
+    constexpr uint32_t kEnt = (kSizeClasses * kGroups + 1023) / 1024;
+    uint32_t loc[kEnt];
     uint64_t sum = 0;
 #pragma unroll
-    for (uint32_t e = 0; e < kPer; e++) {
-      const uint32_t i = tid * kPer + e;
+    for (uint32_t e = 0; e < kEnt; e++) {
+      const uint32_t i = tid * kEnt + e;
       loc[e] = i < kSizeClasses * kGroups ? s_cls[i] : 0u;
       sum += loc[e];
     }
     uint64_t tot;
     uint64_t run = block_excl_scan(sum, s_tmp, &tot);  // (its barriers order the reads above)
 #pragma unroll
-    for (uint32_t e = 0; e < kPer; e++) {
-      const uint32_t i = tid * kPer + e;
+    for (uint32_t e = 0; e < kEnt; e++) {
+      const uint32_t i = tid * kEnt + e;
       if (i < kSizeClasses * kGroups) s_cls[i] = (uint32_t)run;
       run += loc[e];
     }
@@ -354,17 +356,17 @@ __global__ __launch_bounds__(1024) void plan_split_scatter(SplitPlan p) {
   if (p.stamps) st[4] = __builtin_amdgcn_s_memrealtime();
   const uint64_t s0 = s_tw[4][0];  // earlier tiles' small buffers
   if (split) {  // pointers and seeds of the compacted batch and the small list
-    const uint8_t *pv[kPlanPerThread];
-    uint32_t sv[kPlanPerThread];
+    const uint8_t *pv[kPer];
+    uint32_t sv[kPer];
 #pragma unroll
-    for (uint32_t k = 0; k < kPlanPerThread; k++) {
+    for (uint32_t k = 0; k < kPer; k++) {
       const uint64_t idx = base + 64u * k;
       const bool in = idx < p.n;
       pv[k] = in ? p.ptrs[idx] : nullptr;
       sv[k] = in && p.seeds ? p.seeds[idx] : 0u;
     }
 #pragma unroll
-    for (uint32_t k = 0; k < kPlanPerThread; k++) {
+    for (uint32_t k = 0; k < kPer; k++) {
       const uint64_t idx = base + 64u * k;
       if (idx >= p.n) break;
       const uint32_t cx = meta[k] & 0x3FFu, cls = (meta[k] >> 10) & 63u, rank = (meta[k] >> 16) & 63u;
@@ -379,13 +381,13 @@ __global__ __launch_bounds__(1024) void plan_split_scatter(SplitPlan p) {
       } else {
         // the small list's descriptor: pointer (48-bit VA) | length << 48, index, seed
         const uint64_t pw = reinterpret_cast<uint64_t>(pv[k]) | (v[k] << 48);
-        p.sdesc[s0 + s_cls[cls * kGroups + wv * kPlanPerThread + k] + rank] =
+        p.sdesc[s0 + s_cls[cls * kGroups + wv * kPer + k] + rank] =
             make_uint4((uint32_t)pw, (uint32_t)(pw >> 32), (uint32_t)idx, sv[k]);
       }
     }
   } else {  // the plain prefix of every buffer, in index order
 #pragma unroll
-    for (uint32_t k = 0; k < kPlanPerThread; k++) {
+    for (uint32_t k = 0; k < kPer; k++) {
       const uint64_t idx = base + 64u * k;
       if (idx >= p.n) break;
       p.prefix_c[cm0 + (meta[k] & 0x3FFu)] = bm0 + ex[k];
@@ -399,14 +401,20 @@ __global__ __launch_bounds__(1024) void plan_split_scatter(SplitPlan p) {
   }
 }
 
-hipError_t launch_plan_split(const SplitPlan &p, hipStream_t stream) {
-  const uint64_t tiles = plan_tiles(p.n);
+template <uint32_t kPer>
+hipError_t launch_plan_split_t(const SplitPlan &p, hipStream_t stream) {
+  const uint64_t tiles = p.n == 0 ? 1 : (p.n + 1024u * kPer - 1) / (1024u * kPer);
   SplitPlan q = p;
   q.tile_pre = tiles > kPlanDirectTiles ? p.tile_pre : nullptr;
-  hipLaunchKernelGGL(plan_split_count, dim3((unsigned)tiles), dim3(1024), 0, stream, q);
+  hipLaunchKernelGGL(plan_split_count<kPer>, dim3((unsigned)tiles), dim3(1024), 0, stream, q);
   if (q.tile_pre) hipLaunchKernelGGL(plan_split_tiles, dim3(1), dim3(1024), 0, stream, q, (uint32_t)tiles);
-  hipLaunchKernelGGL(plan_split_scatter, dim3((unsigned)tiles), dim3(1024), 0, stream, q);
+  hipLaunchKernelGGL(plan_split_scatter<kPer>, dim3((unsigned)tiles), dim3(1024), 0, stream, q);
   return hipGetLastError();
+}
+
+hipError_t launch_plan_split(const SplitPlan &p, hipStream_t stream) {
+  static_assert(kSplitTile == 1024u * kSplitPerThread, "split tile: 16 waves x 64 lanes x kSplitPerThread");
+  return launch_plan_split_t<kSplitPerThread>(p, stream);
 }
 
 // ------------------------------------------------------------ launchers

@@ -348,8 +348,8 @@ struct SplitScratch {
     counts = 128;
     prefix = kCtrBytes;
     tiles = prefix + 8 * (n + 1);
-    tile_pre = tiles + 8 * kTileWords * plan_tiles(n);
-    ptrs = tile_pre + 8 * kTileWords * (plan_tiles(n) + 1);
+    tile_pre = tiles + 8 * kTileWords * split_tiles(n);
+    ptrs = tile_pre + 8 * kTileWords * (split_tiles(n) + 1);
     seeds = ptrs + 8 * n;
     oidx = seeds + 4 * n;
     sdesc = (oidx + 4 * n + 15) & ~size_t(15);
