@@ -519,23 +519,31 @@ def codes_targets(br: Bits, ll, dd, out: list, res: ChunkResult, spec: bool, tar
             out.append(out[s] if s >= 0 else MARKER + WINDOW + s)
 
 
-def inflate_split_parts(data: bytes, cap: int, chunk_bytes: int, parts: int = 8, probe_tokens: int = 64):
+def inflate_split_parts(data: bytes, cap: int, chunk_bytes: int, parts: int = 8, probe_tokens: int = 64,
+                        max_parts: int = 0):
     """The scheme with `parts` items per chunk.  Returns (status, bytes,
-    stats) like inflate_split (status None: the serial decoder runs)."""
+    stats) like inflate_split (status None: the serial decoder runs).
+    max_parts > parts: a chunk with a candidate borrows the items of the
+    candidate-less chunks after it, cutting its block into
+    T = min(max_parts, (kn - k) parts) parts (zcrc_inflate_impl.h owner();
+    the GPU's max_parts is kMaxParts = 64)."""
     cand = find_candidates(data, chunk_bytes)
     nbits = 8 * len(data)
+    max_parts = max(max_parts, parts)
     starts = {}  # (k, j) -> (start, hdr)
     tg = {}      # k -> [(b_m, m)]
     for k, c in enumerate(cand):
         if c is None:
             continue
-        nxt = next((x for x in cand[k + 1:] if x is not None), nbits)
+        kn = next((x for x in range(k + 1, len(cand)) if cand[x] is not None), len(cand))
+        nxt = cand[kn] if kn < len(cand) else nbits
+        T = min(max_parts, (kn - k) * parts)
         starts[(k, 0)] = (c, None)
         bs = []
         if k > 0 or c == 0:
             last = c
-            for m in range(1, parts):
-                b = probe(data, c, c + m * (nxt - c) // parts, probe_tokens)
+            for m in range(1, T):
+                b = probe(data, c, c + m * ((nxt - c) // T), probe_tokens)
                 if b is not None and last < b < nxt:
                     bs.append((b, m))
                     starts[(k, m)] = (b, c)

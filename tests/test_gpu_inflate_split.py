@@ -185,14 +185,38 @@ def test_sp16_matches_just_past_the_ring(monkeypatch, parts):
             assert st == 0 and out == data, (every, chunk)
 
 
+@pytest.mark.parametrize("parts,probe,borrow", [(1, 0, "0"), (1, 0, "1"), (4, 0, "1"), (16, 3, "1"), (2, 0, "1")])
+def test_split_inflate_borrowed_items(monkeypatch, capfd, parts, probe, borrow):
+    """A chunk with a block start takes over the items of the candidate-less
+    chunks after it (its block spans them): with 1-2 KiB chunks a text block
+    spans 15-30 chunks, so up to kMaxParts = 64 parts of one block land on
+    each other (a mask of 64 usable lanes) -- and with unsynchronised probes
+    the parts step over each other's starts."""
+    monkeypatch.setenv("ZCRC_SPLIT_PARTS", str(parts))
+    monkeypatch.setenv("ZCRC_SPLIT_BORROW", borrow)
+    monkeypatch.setenv("ZCRC_SPLIT_TRACE", "1")
+    if probe:
+        monkeypatch.setenv("ZCRC_SPLIT_PROBE", str(probe))
+    for kind, size in (("text", 1 << 20), ("spectrum", 600000), ("far", 400000)):
+        data = S.PAYLOADS[kind](size, 7 + parts)
+        comp = S.deflate(data, 6)
+        for chunk in (1024, 2048):
+            st, out = _run(comp, len(data), chunk)
+            assert st == 0 and out == data, (kind, chunk)
+            line = [l for l in capfd.readouterr().err.splitlines() if l.startswith("[split] src")][-1]
+            assert " serial 0" in line, (kind, chunk, line)  # the chain formed: no serial fall-back
+
+
 def test_finder_finds_every_block_start(monkeypatch, capfd):
     """Every dynamic block start of a zlib stream is found (a missed one only
     costs parallelism, so the parity tests would not notice): with one part
     per chunk and chunks smaller than a block, the chain has one item per
-    block (ZCRC_SPLIT_TRACE prints it)."""
+    block (ZCRC_SPLIT_TRACE prints it; ZCRC_SPLIT_BORROW=0: no chunk takes
+    over the items of the candidate-less chunks after it)."""
     import inflate_split_model as M
     from test_inflate_split_model import _block_starts
     monkeypatch.setenv("ZCRC_SPLIT_PARTS", "1")
+    monkeypatch.setenv("ZCRC_SPLIT_BORROW", "0")
     monkeypatch.setenv("ZCRC_SPLIT_TRACE", "1")
     for kind in ("text", "spectrum"):
         data = S.PAYLOADS[kind](1 << 20, 5)

@@ -157,3 +157,17 @@ def test_near_ring_stream_holds_aliasing_copies(monkeypatch):
             if c is not None:
                 M.spec_decode(comp, c, cand, k, True)
     assert hits
+
+
+@pytest.mark.parametrize("parts,max_parts,probe", [(1, 64, 64), (2, 64, 64), (4, 16, 3)])
+def test_model_borrowed_items_equal_zlib(parts, max_parts, probe):
+    """A chunk with a block start borrows the items of the candidate-less
+    chunks after it: with 1 KiB chunks a text block spans many chunks and is
+    cut into up to max_parts parts."""
+    data = S.text_payload(160 << 10, 31)
+    comp = S.deflate(data, 6)
+    st, out, stats = M.inflate_split_parts(comp, len(data), 1024, parts=parts, probe_tokens=probe,
+                                           max_parts=max_parts)
+    assert stats["fallback"] is None, stats
+    assert st == M.OK and out == data
+    assert stats["items"] > len([c for c in M.find_candidates(comp, 1024) if c is not None]) * parts

@@ -1026,23 +1026,44 @@ __device__ __forceinline__ void next_candidate(const SpecArgs &a, uint64_t k, ui
   cn = kn < a.nchunks ? a.cand[kn] : 8 * a.src_len;
 }
 
-// Chunk k's usable parts: the probed starts that lie strictly after the
-// previous usable one (or the candidate c) and before the next candidate,
-// ascending -- every item of the chunk filters the same way.
-__device__ __forceinline__ uint32_t usable_parts(const SpecArgs &a, uint64_t k, uint64_t c, uint64_t cn,
-                                                 uint64_t *pos, uint32_t *idx) {
-  uint32_t n = 0;
-  uint64_t last = c;
-  for (uint32_t m = 1; m < a.parts; m++) {
-    const uint64_t b = a.part[k * a.parts + m];
-    if (b != kSplitNone && b > last && b < cn) {
-      pos[n] = b;
-      idx[n] = m;
-      n++;
-      last = b;
-    }
+// Item i's owner: the chunk k <= i / parts with a candidate, whose first
+// block the item decodes part j = i - k parts of.  A chunk with a candidate
+// borrows the items of the candidate-less chunks after it -- its block spans
+// them -- for T = (kn - k) parts parts in all, at most a.max_parts.  false:
+// the item has no work.  (Before borrowing, 3 in 4 items of a text stream
+// idled: zlib's blocks span ~4 chunks of 8 KiB, profiles/r03/s32.)
+__device__ __forceinline__ bool owner(const SpecArgs &a, uint64_t i, uint64_t &k, uint32_t &j, uint32_t &T,
+                                      uint64_t &kn, uint64_t &cn) {
+  k = i / a.parts;
+  while (a.cand[k] == kSplitNone) {
+    if (k == 0 || i - (k - 1) * a.parts >= a.max_parts) return false;
+    k--;
   }
-  return n;
+  j = (uint32_t)(i - k * a.parts);
+  next_candidate(a, k, kn, cn);
+  const uint64_t t = (kn - k) * a.parts;
+  T = (uint32_t)(t < a.max_parts ? t : a.max_parts);
+  return j < T;
+}
+
+// The usable parts of chunk k's T, one lane each: the probed starts that lie
+// strictly after the previous usable one (or the candidate c) and before the
+// next candidate -- a probed start is usable when it is above c and above
+// every valid start of a lower part (a prefix max over the wave).  Lane t
+// gets part t's start in b; the mask has bit t set for a usable part t.
+__device__ __forceinline__ uint64_t usable_mask(const SpecArgs &a, uint64_t k, uint32_t T, uint64_t c, uint64_t cn,
+                                                uint64_t &b) {
+  const uint32_t t = threadIdx.x;
+  b = (t > 0 && t < T) ? a.part[k * a.parts + t] : kSplitNone;
+  const bool valid = b != kSplitNone && b < cn;
+  uint64_t m = valid ? b : 0;  // inclusive prefix max
+  for (uint32_t d = 1; d < 64; d <<= 1) {
+    const uint64_t o = __shfl_up(m, d, 64);
+    if (t >= d && o > m) m = o;
+  }
+  uint64_t below = __shfl_up(m, 1, 64);
+  if (t == 0) below = 0;
+  return __ballot(valid && b > c && b > below);
 }
 
 // Reader positioned at bit `bit` of the stream
@@ -1073,15 +1094,13 @@ __device__ __forceinline__ uint64_t reader_bit(const Reader &r) { return ((uint6
 // guess runs into an end of block or an invalid code first.
 __global__ __launch_bounds__(64, ZI_WPE) void inflate_probe_kernel(SpecArgs a) {
   __shared__ __attribute__((aligned(16))) Lds s;
-  const uint64_t i = blockIdx.x, k = i / a.parts;
-  const uint32_t j = (uint32_t)(i % a.parts);
-  if (j == 0) return;
-  const uint64_t c = a.cand[k];
+  const uint64_t i = blockIdx.x;
+  uint64_t k, kn, cn;
+  uint32_t j, T;
   uint64_t out = kSplitNone;
-  if (c != kSplitNone) {
-    uint64_t kn, cn;
-    next_candidate(a, k, kn, cn);
-    const uint64_t guess = c + (uint64_t)j * ((cn - c) / a.parts);
+  if (owner(a, i, k, j, T, kn, cn) && j > 0) {
+    const uint64_t c = a.cand[k];
+    const uint64_t guess = c + (uint64_t)j * ((cn - c) / T);
     Reader r;
     reader_init(r, a);
     LLTab ll;
@@ -1137,38 +1156,41 @@ __global__ __launch_bounds__(64, ZI_WPE) void inflate_probe_kernel(SpecArgs a) {
 // region, which extends over the following items that have no work.
 __global__ __launch_bounds__(64, ZI_WPE) void inflate_spec_kernel(SpecArgs a) {
   __shared__ __attribute__((aligned(16))) Lds s;
-  const uint64_t i = blockIdx.x, k = i / a.parts;
-  const uint32_t j = (uint32_t)(i % a.parts);
-  const uint64_t c = a.cand[k];
+  const uint64_t i = blockIdx.x;
   SpecRec *rec = a.rec + i;
-  uint64_t kn = 0, cn = 0, start = c, vpos[kMaxParts];
-  uint32_t vidx[kMaxParts], np = 0, me = 0;
-  bool work = c != kSplitNone;
+  uint64_t k = 0, kn = 0, cn = 0, c = 0, start = 0, mask = 0, b = kSplitNone;
+  uint32_t j = 0, T = 0, np = 0, me = 0;
+  bool work = owner(a, i, k, j, T, kn, cn);
   if (work) {
-    next_candidate(a, k, kn, cn);
-    np = usable_parts(a, k, c, cn, vpos, vidx);
+    c = a.cand[k];
+    start = c;
+    mask = usable_mask(a, k, T, c, cn, b);
+    np = (uint32_t)__popcll(mask);
     if (j > 0) {
-      work = false;
-      for (uint32_t t = 0; t < np; t++)
-        if (vidx[t] == j) work = true, start = vpos[t], me = t + 1;
+      work = (mask >> j) & 1u;
+      me = (uint32_t)__popcll(mask & ((1ull << j) - 1u)) + 1u;
+      start = a.part[i];
     }
   }
   if (!work) {
     if (threadIdx.x == 0) *rec = SpecRec{0, 0, 0, kSpecSkipped, -1, 0, 0};
     return;
   }
-  // (the compiler keeps the small arrays above in VGPRs: everything taken
-  // from them is made provably uniform before it reaches the decode state,
-  // whose asm wants SGPRs)
+  // (everything below reaches the decode state, whose asm wants SGPRs: made
+  // provably uniform)
+  k = uni64(k);
+  j = uni(j);
+  c = uni64(c);
+  kn = uni64(kn);
   start = uni64(start);
   np = uni(np);
   me = uni(me);
-  // landing targets: the usable parts after this one; the region runs to the
-  // next item with work
-  const uint32_t tn = np - me;
-  if (threadIdx.x < tn) {
-    s.tpos[threadIdx.x] = vpos[me + threadIdx.x];
-    s.titem[threadIdx.x] = (uint32_t)(k * a.parts + vidx[me + threadIdx.x]);
+  // landing targets: the usable parts after this one, ascending
+  const uint32_t tn = np - me, t = threadIdx.x;
+  if (((mask >> t) & 1u) && t > j) {
+    const uint32_t rank = (uint32_t)__popcll(mask & ((1ull << t) - 1u)) - me;
+    s.tpos[rank] = b;
+    s.titem[rank] = (uint32_t)(k * a.parts + t);
   }
   __syncthreads();
   // Region: the chunk owns the elements of its items and of the items of the
@@ -1189,7 +1211,7 @@ __global__ __launch_bounds__(64, ZI_WPE) void inflate_spec_kernel(SpecArgs a) {
   o.al16 = (reinterpret_cast<uint64_t>(o.dst) & 15u) == 0;
   o.reach = 0;
   o.spec = i > 0;
-  o.tpos = uni64(tn ? vpos[me] : kSplitNone);
+  o.tpos = uni64(tn ? s.tpos[0] : kSplitNone);
   o.ti = 0;
   o.tn = tn;
   o.landed = 0;

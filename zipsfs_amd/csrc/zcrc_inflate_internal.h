@@ -31,7 +31,8 @@ constexpr uint32_t kInflateHist = 32768u;
 constexpr uint64_t kSplitNone = ~0ull;  // no candidate block start in the chunk
 constexpr int32_t kSpecSkipped = -1;    // SpecRec::status of an item without work
 constexpr int32_t kSpecLanded = 100;    // codes(): stopped on a later part's start (internal)
-constexpr uint32_t kMaxParts = 16;      // items per chunk (a chunk's first block cut into parts)
+constexpr uint32_t kMaxParts = 64;      // parts of one block: one lane each (a chunk's first block cut into parts)
+constexpr uint32_t kMaxChunkParts = 16; // items per chunk
 struct SpecRec {
   uint64_t region;   // element offset of the item's output in the region array
   uint64_t out_len;  // elements produced
@@ -50,8 +51,9 @@ struct SpecArgs {
   uint64_t region_elems; // [k parts, k' parts) x region_elems up to the next such chunk k', split among its parts
   uint64_t nchunks;
   uint64_t *part;        // per item: the probed start of part j >= 1 (kSplitNone: none)
-  uint32_t parts;        // items per chunk (<= kMaxParts)
+  uint32_t parts;        // items per chunk (<= kMaxChunkParts)
   uint32_t probe_tokens;
+  uint32_t max_parts;    // parts of one chunk's first block, its own items and those it borrows (<= kMaxParts)
 };
 constexpr uint64_t kInflateMaxSrc = 0xF0000000ull;  // 32-bit buffer range and block arithmetic
 // order_scratch: >= 4 * n bytes of device memory for the dispatch order

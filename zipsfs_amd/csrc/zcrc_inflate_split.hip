@@ -523,7 +523,7 @@ InflateSplitShape inflate_split_shape(uint64_t src_len, uint64_t cap, uint64_t w
   const char *fp = getenv("ZCRC_SPLIT_PARTS");  // (read per call: tests set it)
   const int force_parts = fp ? atoi(fp) : 0;
   if (force_parts > 0) parts = (uint64_t)force_parts;
-  if (parts > kMaxParts) parts = kMaxParts;
+  if (parts > kMaxChunkParts) parts = kMaxChunkParts;
   if (parts < 1) parts = 1;
   while (parts > 1 && nch * parts > kChainLds) parts--;
   sh.parts = (uint32_t)parts;
@@ -576,10 +576,13 @@ hipError_t launch_inflate_split(const uint8_t *src, uint64_t src_len, uint8_t *d
   FindArgs fa{src, src_len, chunk, nch, cand, ft ? (uint32_t)atoi(ft) : 0u};
   hipLaunchKernelGGL(inflate_find_kernel, dim3((unsigned)nch), dim3(kFindThreads), 0, stream, fa);
   const char *pt = getenv("ZCRC_SPLIT_PROBE");  // test knob: tokens per probe (a few: unsynchronised part starts)
+  // test knob: ZCRC_SPLIT_BORROW=0 keeps each chunk to its own items
+  const char *bw = getenv("ZCRC_SPLIT_BORROW");
   SpecArgs sa{src, src_len, cand, rec, region, relems, nch, part, shape.parts,
-              pt && atoi(pt) > 0 ? (uint32_t)atoi(pt) : kInflateProbeTokens};
+              pt && atoi(pt) > 0 ? (uint32_t)atoi(pt) : kInflateProbeTokens,
+              bw && atoi(bw) == 0 ? shape.parts : kMaxParts};
   hipError_t e = hipSuccess;
-  if (shape.parts > 1) e = launch_inflate_probe(sa, stream);
+  if (sa.max_parts > 1) e = launch_inflate_probe(sa, stream);
   if (e == hipSuccess) e = launch_inflate_spec(sa, shape.wide, stream);
   if (e != hipSuccess) return e;
   ChainArgs ca{rec, nit, cap, chain, off, run_serial, out_len, status, fb_src, fb_src_len, fb_dst, fb_cap,
