@@ -189,12 +189,13 @@ def device_snap(batch: "Batch", t: int):
     return b0 + q, i, (i - 1 if q < m else i)
 
 
-def wave_ranges(batch: Batch, num_cus: int, dyn_shift: int = K_DYN_SHIFT, unit: int = K_DYN_UNIT):
+def wave_ranges(batch: Batch, num_cus: int, dyn_shift: int = K_DYN_SHIFT, unit: int = K_DYN_UNIT, tail: int = 0):
     """Every (s0, s1, last) range the kernel processes: W static wave ranges
     over the first Ts bytes, then the dynamic units of `unit` nominal bytes
     over the last Td = total >> dyn_shift bytes (zcrc_batch_kernel.h,
-    crc32_batch_kernel).  Which wave claims a unit does not matter for the
-    result, so the model lists them in order."""
+    crc32_batch_kernel) -- with `tail` (BatchArgs::dyn_tail), the last
+    min(Td / 2, tail x W half units) bytes in half units.  Which wave claims
+    a unit does not matter for the result, so the model lists them in order."""
     total = batch.total
     want = max(1, (total + K_MIN_RANGE - 1) // K_MIN_RANGE, batch.n)
     W = min(want, num_cus * K_WAVES)
@@ -213,12 +214,21 @@ def wave_ranges(batch: Batch, num_cus: int, dyn_shift: int = K_DYN_SHIFT, unit: 
         else:
             s1 = batch.snap(q * (w + 1) + (r * (w + 1)) // W)
         out.append((s0, s1, w + 1 == W and not Td))
-    units = (Td + unit - 1) // unit if Td else 0
+    half = unit // 2
+    Ut = min(tail * W * half, Td // 2) // half if Td and tail else 0
+    Tm = total - Ut * half
+    Um = (Tm - Ts + unit - 1) // unit if Td else 0
+    units = Um + Ut
     for u in range(units):
-        t0 = Ts + u * unit
+        if u < Um:
+            t0 = Ts + u * unit
+            t1 = Tm if Ut and u + 1 == Um else t0 + unit
+        else:
+            t0 = Tm + (u - Um) * half
+            t1 = t0 + half
         last = u + 1 == units
         s0 = batch.snap(min(t0, total))
-        s1 = total if last else batch.snap(min(t0 + unit, total))
+        s1 = total if last else batch.snap(min(t1, total))
         out.append((s0, s1, last))
     return out
 
@@ -303,11 +313,12 @@ def crc_piece(mem: np.ndarray, pstart: int, pend: int, inj: int, T: Tables) -> i
     return r0
 
 
-def run_batch(batch: Batch, num_cus: int = 256, dyn_shift: int = K_DYN_SHIFT, unit: int = K_DYN_UNIT) -> np.ndarray:
+def run_batch(batch: Batch, num_cus: int = 256, dyn_shift: int = K_DYN_SHIFT, unit: int = K_DYN_UNIT,
+              tail: int = 0) -> np.ndarray:
     """CRCs of every buffer, computed the way the kernel computes them."""
     T = tables()
     out = np.zeros(batch.n, dtype=np.uint32)
-    for (s0, s1, last) in wave_ranges(batch, num_cus, dyn_shift, unit):
+    for (s0, s1, last) in wave_ranges(batch, num_cus, dyn_shift, unit, tail):
         for (i, rel_lo, rel_hi) in wave_pieces(batch, s0, s1, last):
             n = batch.lens[i]
             seed = batch.seeds[i]
@@ -439,14 +450,22 @@ K_SMALL_MAX = 8192
 K_SIZE_CLASSES = K_SMALL_MAX // 256 + 1
 K_SMALL_COST = 14  # zcrc_internal.h kSmallCostDefault (quarters of a batch-kernel byte)
 K_BIG_MIN = 1 << 20  # zcrc_internal.h kBigMin
-K_SPLIT_PER_THREAD = 8  # zcrc_internal.h kSplitPerThread
-K_SPLIT_TILE = 1024 * K_SPLIT_PER_THREAD  # buffers per split-plan tile (kSplitTile)
+K_SPLIT_MAX_TILES = 256  # zcrc_internal.h kSplitMaxTiles
+
+
+def split_tile(n: int) -> int:
+    """Buffers per split-plan tile (zcrc_internal.h split_per_thread): 1024 x
+    the smallest of 1, 2, 4, 8 that keeps the tiles within kSplitMaxTiles."""
+    per = 1
+    while per < 8 and -(-n // (1024 * per)) > K_SPLIT_MAX_TILES:
+        per *= 2
+    return 1024 * per
 
 
 def split_plan(lens, grid: int = 256, force: bool = False, small_cost: int = K_SMALL_COST, direct_ok: bool = True):
     """zcrc_kernels.hip plan_split_scatter's decisions and lists: (split,
     large list -- on a split, buffers below kBigMin first, then the others,
-    each in index order -- with its prefix, small list tile by tile (K_SPLIT_TILE
+    each in index order -- with its prefix, small list tile by tile (split_tile(n)
     buffers), by size class within a tile and in index order within a class,
     small workgroups, small lanes)."""
     lens = [int(x) for x in lens]
@@ -463,7 +482,8 @@ def split_plan(lens, grid: int = 256, force: bool = False, small_cost: int = K_S
         wgs = min(max(wgs, 1), grid - 1)
     if not split:
         return dict(split=False, large=list(range(len(lens))), small=[], wgs=wgs, lanes=16)
-    by_class = sorted(small, key=lambda i: (i // K_SPLIT_TILE, (lens[i] + 255) >> 8, i))
+    tile = split_tile(len(lens))
+    by_class = sorted(small, key=lambda i: (i // tile, (lens[i] + 255) >> 8, i))
     lanes = 8 if as_ <= 2048 * len(small) else 16
     if not large and direct_ok:  # mode 2: about equal small buffers, walked in index order without lists
         mean = as_ / len(small)

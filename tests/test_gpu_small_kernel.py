@@ -178,9 +178,13 @@ def test_device_split_plan_direct_mode(lens_kind, direct, monkeypatch):
                                   _oracle(host, offs, lens, np.zeros(n, np.uint32)))
 
 
-def test_config4_golden_replicated_through_split_plan(golden):
+@pytest.mark.parametrize("dyn_tail", [None, "2"])
+def test_config4_golden_replicated_through_split_plan(golden, dyn_tail, monkeypatch):
     """The config-4 golden sample repeated 9 times (> kFusedMaxN buffers, so
-    the device split plan runs): every CRC equals the reference's."""
+    the device split plan runs): every CRC equals the reference's -- also with
+    the dynamic part's last units halved (ZCRC_DYN_TAIL, BatchArgs::dyn_tail)."""
+    if dyn_tail:
+        monkeypatch.setenv("ZCRC_DYN_TAIL", dyn_tail)
     cfg = golden["cfg"]
     idx = cfg["cfg4_idx"].astype(np.int64)
     L = cfg["cfg4_len"].astype(np.int64)
@@ -309,7 +313,7 @@ def _split_lists(scratch, n):
     indices (word 2 of each 16-B descriptor), pointers and lengths."""
     import kernel_model as km
     raw = scratch.cpu().numpy()
-    T = -(-n // km.K_SPLIT_TILE)
+    T = -(-n // km.split_tile(n))
     prefix = 256
     tiles = prefix + 8 * (n + 1)
     tile_pre = tiles + 48 * T  # kTileWords = 6

@@ -191,9 +191,10 @@ int main(int argc, char **argv) {
   std::vector<hipEvent_t> ev(2 * kBatches);
   for (auto &e : ev) CHECK(hipEventCreate(&e));
   enum { kProbeWave, kProbeGrid, kCrc, kCrcFused, kCrcFusedR3, kCrcFused5, kProbePb, kProbePbRot, kProbePbNoPrio,
-         kProbePbFat, kNumV };
+         kProbePbFat, kCrcFused14, kCrcFused24, kCrcFused15, kNumV };
   const char *names[kNumV] = {"probe-wave", "probe-grid", "crc", "crc-fused", "crc-fused-r3", "crc-fused-5", "probe-pb",
-                              "probe-pb-rot", "probe-pb-np", "probe-pb-fat"};
+                              "probe-pb-rot", "probe-pb-np", "probe-pb-fat", "crc-fused-14", "crc-fused-24",
+                              "crc-fused-15"};
   auto launch = [&](int v, int b, hipEvent_t e0, hipEvent_t e1) {
     const uint8_t *base = data + b * kBatchBytes;
     switch (v) {
@@ -231,6 +232,18 @@ int main(int argc, char **argv) {
         hipExtLaunchKernelGGL((crc32_batch_kernel<false, kDepth, 0, true, false, 1, kLoadNt, true, kWindowed, 3>),
                               dim3(cus), dim3(kThreads), 0, 0, e0, e1, 0, crc_args(b, true));
         break;
+      case kCrcFused14:
+        hipExtLaunchKernelGGL((crc32_batch_kernel<false, kDepth, 0, true, false, 1, kLoadNt, true, kWindowed, 14>),
+                              dim3(cus), dim3(kThreads), 0, 0, e0, e1, 0, crc_args(b, true));
+        break;
+      case kCrcFused24:
+        hipExtLaunchKernelGGL((crc32_batch_kernel<false, kDepth, 0, true, false, 1, kLoadNt, true, kWindowed, 24>),
+                              dim3(cus), dim3(kThreads), 0, 0, e0, e1, 0, crc_args(b, true));
+        break;
+      case kCrcFused15:
+        hipExtLaunchKernelGGL((crc32_batch_kernel<false, kDepth, 0, true, false, 1, kLoadNt, true, kWindowed, 15>),
+                              dim3(cus), dim3(kThreads), 0, 0, e0, e1, 0, crc_args(b, true));
+        break;
     }
     CHECK(hipGetLastError());
   };
@@ -258,7 +271,12 @@ int main(int argc, char **argv) {
   CHECK(hipMemcpy(o3.data(), out, 4 * kN, hipMemcpyDeviceToHost));
   launch(kCrcFused5, 0, nullptr, nullptr);
   CHECK(hipMemcpy(o4.data(), out, 4 * kN, hipMemcpyDeviceToHost));
-  const bool eq = o1 == o2 && o1 == o3 && o1 == o4;
+  bool eq = o1 == o2 && o1 == o3 && o1 == o4;
+  for (int v : {kCrcFused14, kCrcFused24, kCrcFused15}) {
+    launch(v, 0, nullptr, nullptr);
+    CHECK(hipMemcpy(o4.data(), out, 4 * kN, hipMemcpyDeviceToHost));
+    eq = eq && o1 == o4;
+  }
   printf("c2_probe: %d CUs, 16 x 256 MiB batches rotated, %d reps; crc forms %s\n", cus, reps,
          eq ? "equal" : "DIFFER");
   for (int v = 0; v < kNumV; v++) {
@@ -273,6 +291,12 @@ int main(int argc, char **argv) {
     CHECK(hipMemset(stamps, 0, 64 * (uint64_t)cus * kWaves));
     if (fused && pb == 5)
       hipExtLaunchKernelGGL((crc32_batch_kernel<false, kDepth, 0, true, true, 1, kLoadNt, true, kWindowed, 5>),
+                            dim3(cus), dim3(kThreads), 0, 0, ev[0], ev[1], 0, a);
+    else if (fused && pb == 14)
+      hipExtLaunchKernelGGL((crc32_batch_kernel<false, kDepth, 0, true, true, 1, kLoadNt, true, kWindowed, 14>),
+                            dim3(cus), dim3(kThreads), 0, 0, ev[0], ev[1], 0, a);
+    else if (fused && pb == 24)
+      hipExtLaunchKernelGGL((crc32_batch_kernel<false, kDepth, 0, true, true, 1, kLoadNt, true, kWindowed, 24>),
                             dim3(cus), dim3(kThreads), 0, 0, ev[0], ev[1], 0, a);
     else if (fused && pb == 3)
       hipExtLaunchKernelGGL((crc32_batch_kernel<false, kDepth, 0, true, true, 1, kLoadNt, true, kWindowed, 3>),
@@ -326,5 +350,7 @@ int main(int argc, char **argv) {
   timeline("crc-fused", true, 5);
   timeline("crc-fused-r3", true, 7, 3);
   timeline("crc-fused-5", true, 9, 5);
+  timeline("crc-fused-14", true, 11, 14);
+  timeline("crc-fused-24", true, 13, 24);
   return 0;
 }

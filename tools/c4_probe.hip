@@ -7,7 +7,7 @@
 // launch, events around `steps` back-to-back steps), the plan alone, and the
 // CRC launch alone (its dispatch packet's timestamps).  Variants move the
 // split's knobs: the small-list workgroups' cost weight (small_cost), the big
-// class edge (big_min) and the dynamic unit.  Then one stamped launch
+// class edge (big_min), the dynamic unit and the tail half units (dyn_tail).  Then one stamped launch
 // (kStamp build, s_memrealtime at 100 MHz): batch waves' entry, static
 // range end and end, small-list waves' end, percentiles; the last 24 waves
 // to finish with their pieces, dynamic units and static bytes; end p50 per
@@ -69,6 +69,7 @@ struct Variant {
   uint32_t small_cost;
   uint64_t big_min;
   uint64_t dyn_unit;  // 0: kDynUnit
+  uint32_t dyn_tail;  // BatchArgs::dyn_tail
 };
 
 int main(int argc, char **argv) {
@@ -94,7 +95,7 @@ int main(int argc, char **argv) {
   uint8_t *data;
   CK(hipMalloc(&data, off + 16));
   for (uint64_t i = 0; i < n; i++) ptrs[i] = (uint64_t)(data + offs[i]);
-  const uint64_t tiles = plan_tiles(n);
+  const uint64_t tiles = split_tiles(n);
   uint64_t *d_lens, *d_ptrs, *d_stamps;
   uint8_t *scratch;
   uint32_t *d_out;
@@ -146,19 +147,19 @@ int main(int argc, char **argv) {
   a.fault = reinterpret_cast<uint32_t *>(scratch + kFaultByte);
 
   const Variant vs[] = {
-      {"default", kSmallCostDefault, kBigMin, 0},
-      {"cost10", 10, kBigMin, 0},
-      {"cost20", 20, kBigMin, 0},
-      {"big256k", kSmallCostDefault, 256ull << 10, 0},
-      {"big4m", kSmallCostDefault, 4ull << 20, 0},
-      {"unit96k", kSmallCostDefault, kBigMin, 96ull << 10},
-      {"unit192k", kSmallCostDefault, kBigMin, 192ull << 10},
+      {"default", kSmallCostDefault, kBigMin, 0, 0},
+      {"tail1", kSmallCostDefault, kBigMin, 0, 1},
+      {"tail2", kSmallCostDefault, kBigMin, 0, 2},
+      {"tail4", kSmallCostDefault, kBigMin, 0, 4},
+      {"u256t4", kSmallCostDefault, kBigMin, 256ull << 10, 4},
+      {"u64k", kSmallCostDefault, kBigMin, 64ull << 10, 0},
   };
   const int nv = (int)(sizeof vs / sizeof vs[0]);
   auto set = [&](const Variant &v) {
     p.small_cost = v.small_cost;
     p.big_min = v.big_min;
     a.dyn_unit = v.dyn_unit;
+    a.dyn_tail = v.dyn_tail;
   };
   hipEvent_t e0, e1, k0, k1;
   CK(hipEventCreate(&e0));
@@ -227,73 +228,77 @@ int main(int argc, char **argv) {
            pm.c_str(), km.c_str(), total / (*std::min_element(step_ms[vi].begin(), step_ms[vi].end()) * 1e-3) / 1e9);
   }
 
-  // ---- stamped launch (default variant)
-  set(vs[0]);
-  CK(launch_plan_split(p, 0));
-  CK(hipMemcpy(counts, scratch + 128, 40, hipMemcpyDeviceToHost));
-  CK(hipMemset(d_stamps, 0, 64 * nw));
-  BatchArgs as = a;
-  as.stamps = d_stamps;
-  hipExtLaunchKernelGGL((crc32_batch_kernel<false, kDepth, 0, true, true>), grid, block, 0, 0, k0, k1, 0, as);
-  CK(hipGetLastError());
-  CK(hipDeviceSynchronize());
-  float ms;
-  CK(hipEventElapsedTime(&ms, k0, k1));
-  CK(hipMemcpy(got.data(), d_out, 4 * n, hipMemcpyDeviceToHost));
-  std::vector<uint64_t> st(8 * nw);
-  CK(hipMemcpy(st.data(), d_stamps, 64 * nw, hipMemcpyDeviceToHost));
-  uint64_t t0 = ~0ull;
-  for (uint64_t w = 0; w < nw; w++)
-    if (st[8 * w + 1]) t0 = std::min(t0, st[8 * w + 4]);
-  const uint32_t nsm = (uint32_t)counts[4];
-  std::vector<double> entry, search, begin, send, end, s_begin, s_end;
-  std::vector<double> slot_end[kWaves];
-  struct Row {
-    double end, send;
-    uint64_t w, pieces, dyn, sbytes;
-  };
-  std::vector<Row> rows;
-  for (uint64_t w = 0; w < nw; w++) {
-    if (!st[8 * w + 1]) continue;
-    const double e = (st[8 * w + 1] - t0) * 1e-2;
-    if (st[8 * w + 2] == ~0ull) {
-      s_begin.push_back((st[8 * w + 0] - t0) * 1e-2);
-      s_end.push_back(e);
-      continue;
+  // ---- stamped launches
+  auto stamped = [&](const Variant &sv) {
+    set(sv);
+    CK(launch_plan_split(p, 0));
+    CK(hipMemcpy(counts, scratch + 128, 40, hipMemcpyDeviceToHost));
+    CK(hipMemset(d_stamps, 0, 64 * nw));
+    BatchArgs as = a;
+    as.stamps = d_stamps;
+    hipExtLaunchKernelGGL((crc32_batch_kernel<false, kDepth, 0, true, true>), grid, block, 0, 0, k0, k1, 0, as);
+    CK(hipGetLastError());
+    CK(hipDeviceSynchronize());
+    float ms;
+    CK(hipEventElapsedTime(&ms, k0, k1));
+    CK(hipMemcpy(got.data(), d_out, 4 * n, hipMemcpyDeviceToHost));
+    std::vector<uint64_t> st(8 * nw);
+    CK(hipMemcpy(st.data(), d_stamps, 64 * nw, hipMemcpyDeviceToHost));
+    uint64_t t0 = ~0ull;
+    for (uint64_t w = 0; w < nw; w++)
+      if (st[8 * w + 1]) t0 = std::min(t0, st[8 * w + 4]);
+    const uint32_t nsm = (uint32_t)counts[4];
+    std::vector<double> entry, search, begin, send, end, s_begin, s_end;
+    std::vector<double> slot_end[kWaves];
+    struct Row {
+      double end, send;
+      uint64_t w, pieces, dyn, sbytes;
+    };
+    std::vector<Row> rows;
+    for (uint64_t w = 0; w < nw; w++) {
+      if (!st[8 * w + 1]) continue;
+      const double e = (st[8 * w + 1] - t0) * 1e-2;
+      if (st[8 * w + 2] == ~0ull) {
+        s_begin.push_back((st[8 * w + 0] - t0) * 1e-2);
+        s_end.push_back(e);
+        continue;
+      }
+      entry.push_back((st[8 * w + 4] - t0) * 1e-2);
+      search.push_back((st[8 * w + 5] - t0) * 1e-2);
+      begin.push_back((st[8 * w + 0] - t0) * 1e-2);
+      const double se = st[8 * w + 3] ? (st[8 * w + 3] - t0) * 1e-2 : e;
+      send.push_back(se);
+      end.push_back(e);
+      slot_end[w % kWaves].push_back(e);
+      rows.push_back({e, se, w, st[8 * w + 2], st[8 * w + 6], st[8 * w + 7]});
     }
-    entry.push_back((st[8 * w + 4] - t0) * 1e-2);
-    search.push_back((st[8 * w + 5] - t0) * 1e-2);
-    begin.push_back((st[8 * w + 0] - t0) * 1e-2);
-    const double se = st[8 * w + 3] ? (st[8 * w + 3] - t0) * 1e-2 : e;
-    send.push_back(se);
-    end.push_back(e);
-    slot_end[w % kWaves].push_back(e);
-    rows.push_back({e, se, w, st[8 * w + 2], st[8 * w + 6], st[8 * w + 7]});
-  }
-  printf("stamped launch: %.2f us (events), CRCs %s; split %llu: %llu batch buffers, %llu small on %u workgroups "
-         "(%u lanes each)\n",
-         ms * 1e3, got == ref ? "equal" : "DIFFER", (unsigned long long)counts[2], (unsigned long long)counts[0],
-         (unsigned long long)counts[1], nsm, (unsigned)counts[3]);
-  printf("us after first entry      p0      p10     p50     p90     p99    p100\n");
-  auto row = [&](const char *k, const std::vector<double> &v) {
-    printf("  %-20s %7.1f %7.1f %7.1f %7.1f %7.1f %7.1f\n", k, pct(v, 0), pct(v, .1), pct(v, .5), pct(v, .9),
-           pct(v, .99), pct(v, 1));
+    printf("stamped launch (%s): %.2f us (events), CRCs %s; split %llu: %llu batch buffers, %llu small on %u workgroups "
+           "(%u lanes each)\n",
+           sv.name, ms * 1e3, got == ref ? "equal" : "DIFFER", (unsigned long long)counts[2], (unsigned long long)counts[0],
+           (unsigned long long)counts[1], nsm, (unsigned)counts[3]);
+    printf("us after first entry      p0      p10     p50     p90     p99    p100\n");
+    auto row = [&](const char *k, const std::vector<double> &v) {
+      printf("  %-20s %7.1f %7.1f %7.1f %7.1f %7.1f %7.1f\n", k, pct(v, 0), pct(v, .1), pct(v, .5), pct(v, .9),
+             pct(v, .99), pct(v, 1));
+    };
+    row("batch entry", entry);
+    row("batch search", search);
+    row("batch begin", begin);
+    row("batch static end", send);
+    row("batch end", end);
+    row("small begin", s_begin);
+    row("small end", s_end);
+    std::sort(rows.begin(), rows.end(), [](const Row &x, const Row &y) { return x.end > y.end; });
+    printf("last waves: w (cu, slot) end | static end | pieces dyn_units static_KiB\n");
+    for (size_t i = 0; i < rows.size() && i < 24; i++)
+      printf("  %5llu (%3llu,%2llu) %7.1f | %7.1f | %5llu %3llu %8.1f\n", (unsigned long long)rows[i].w,
+             (unsigned long long)(rows[i].w / kWaves), (unsigned long long)(rows[i].w % kWaves), rows[i].end,
+             rows[i].send, (unsigned long long)rows[i].pieces, (unsigned long long)rows[i].dyn, rows[i].sbytes / 1024.0);
+    printf("end p50 by wave slot:");
+    for (int s = 0; s < kWaves; s++) printf(" %.0f", pct(slot_end[s], .5));
+    printf("\n");
   };
-  row("batch entry", entry);
-  row("batch search", search);
-  row("batch begin", begin);
-  row("batch static end", send);
-  row("batch end", end);
-  row("small begin", s_begin);
-  row("small end", s_end);
-  std::sort(rows.begin(), rows.end(), [](const Row &x, const Row &y) { return x.end > y.end; });
-  printf("last waves: w (cu, slot) end | static end | pieces dyn_units static_KiB\n");
-  for (size_t i = 0; i < rows.size() && i < 24; i++)
-    printf("  %5llu (%3llu,%2llu) %7.1f | %7.1f | %5llu %3llu %8.1f\n", (unsigned long long)rows[i].w,
-           (unsigned long long)(rows[i].w / kWaves), (unsigned long long)(rows[i].w % kWaves), rows[i].end,
-           rows[i].send, (unsigned long long)rows[i].pieces, (unsigned long long)rows[i].dyn, rows[i].sbytes / 1024.0);
-  printf("end p50 by wave slot:");
-  for (int s = 0; s < kWaves; s++) printf(" %.0f", pct(slot_end[s], .5));
-  printf("\n");
+  stamped(vs[0]);
+  stamped(vs[2]);
   return 0;
 }

@@ -487,7 +487,7 @@ __device__ void split_accumulate(const BatchArgs &a, uint64_t i, uint64_t n, uin
 // Process every piece of the byte range [S0, S1) of the concatenated batch
 // (S0, S1 snapped; `last_range` also takes the trailing empty buffers).
 // Returns the number of pieces.  Wave-uniform; no barriers.
-template <uint32_t kD, int kAblate, int kAux, bool kStamp, bool kPre = false>
+template <uint32_t kD, int kAblate, int kAux, bool kStamp, bool kPre = false, bool kProg = false>
 __device__ __forceinline__ uint32_t piece_raw(const uint32_t *s_lds, const uint8_t *bptr, uint64_t rel_lo,
                                               uint64_t rel_hi, uint32_t seed, uint32_t lane, uint64_t *t_tail,
                                               const uint4 *pre = nullptr);
@@ -686,7 +686,10 @@ __device__ __forceinline__ void piece_preload(const uint8_t *bptr, uint64_t rel_
 // long), as the raw register at the piece end; the seed is injected when the
 // piece starts the buffer.  kPre: groups 0 and 1 were loaded by
 // piece_preload into pre[0 .. 2 kD).  Wave-uniform; no barriers.
-template <uint32_t kD, int kAblate, int kAux, bool kStamp, bool kPre>
+// kProg (per-buffer mode A/B): the wave's priority falls with its progress
+// through the piece, 3 in the first quarter of its groups .. 0 in the last,
+// so that waves behind issue first and the waves of a CU end together
+template <uint32_t kD, int kAblate, int kAux, bool kStamp, bool kPre, bool kProg>
 __device__ __forceinline__ uint32_t piece_raw(const uint32_t *s_lds, const uint8_t *bptr, uint64_t rel_lo,
                                               uint64_t rel_hi, uint32_t seed, uint32_t lane, uint64_t *t_tail,
                                               const uint4 *pre) {
@@ -759,6 +762,12 @@ __device__ __forceinline__ uint32_t piece_raw(const uint32_t *s_lds, const uint8
       const uint32_t nplain = ngroups - 2;
       uint32_t g = 1;
       for (uint32_t pr = 0; pr < nplain / 2; pr++) {
+        if (kProg) {  // wave-uniform scalar compares: level = floor(4 pr / npairs)
+          const uint32_t q = 4u * pr, np = nplain / 2;
+          if (q >= 3u * np) __builtin_amdgcn_s_setprio(0);
+          else if (q >= 2u * np) __builtin_amdgcn_s_setprio(1);
+          else if (q >= np) __builtin_amdgcn_s_setprio(2);
+        }
         ZCRC_LOADG(ga, g + 1);
         ZCRC_PLAIN(gb);
         ZCRC_LOADG(gb, g + 2);
@@ -810,7 +819,9 @@ __device__ __forceinline__ void small_body(const SmallArgs &a, uint32_t *s_lds, 
 // kPB: the per-buffer mode's form (fused only): 4 = round 4 (tables built in
 // registers, the decision after the work), 5 = the same with the first
 // payload loads issued before the table build, 3 = round 3 (tables and
-// lengths in front of the one barrier); 3 and 5 are A/B forms for tools/)
+// lengths in front of the one barrier); 3 and 5 are A/B forms for tools/.
+// kPB + 10: priority by progress through the buffer instead of by wave slot
+// (piece_raw kProg); kPB + 20: no priorities (A/B forms, tools/c2_probe).
 template <bool kStrided, uint32_t kD = kDepth, int kAblate = 0, bool kRotate = true, bool kStamp = false,
           int kPrio = 1, int kAux = kLoadNt, bool kFused = false, bool kWin = kWindowed, int kPB = 4>
 __global__ __launch_bounds__(kThreads) void crc32_batch_kernel(BatchArgs args) {
@@ -910,7 +921,8 @@ __global__ __launch_bounds__(kThreads) void crc32_batch_kernel(BatchArgs args) {
     // guarded length loads waited for one at a time: the table fill
     // completed 7.7 us after entry, now 3.5 us; tools/c2_probe,
     // profiles/r03/s11, s16.)
-    if (kPB >= 4 && args.n <= (uint64_t)grid * kWaves) {
+    constexpr int kForm = kPB % 10, kPrioMode = kPB / 10;  // kPrioMode: 0 by slot, 1 by progress, 2 none
+    if (kForm >= 4 && args.n <= (uint64_t)grid * kWaves) {
       // Round 4: nothing in front of the payload waits on memory but the
       // wave's own descriptor.  The braid and combine tables are built in
       // registers (braid_gen_lane, comb_gen) and the one barrier in front
@@ -943,7 +955,7 @@ __global__ __launch_bounds__(kThreads) void crc32_batch_kernel(BatchArgs args) {
       uint4 pre[2 * kD];
       // kPB >= 5: the first payload loads go out as soon as the descriptor is
       // in, ahead of the table build (A/B form)
-      if (kPB >= 5) piece_preload<kD, kAux>(bptr, 0, blen, lane, own && blen >= 4, pre);
+      if (kForm >= 5) piece_preload<kD, kAux>(bptr, 0, blen, lane, own && blen >= 4, pre);
       if (wg_busy) {
         const uint32_t e = braid_gen_lane(lane, slot);
         uint4 *dst = reinterpret_cast<uint4 *>(s_lds);
@@ -962,22 +974,27 @@ __global__ __launch_bounds__(kThreads) void crc32_batch_kernel(BatchArgs args) {
       const uint64_t t_lens = kStamp ? __builtin_amdgcn_s_memrealtime() : 0;  // diagnostic: tables written
       __syncthreads();  // the tables are in LDS
       const uint64_t t_fill = kStamp ? __builtin_amdgcn_s_memrealtime() : 0;
-      if (kPB < 5) piece_preload<kD, kAux>(bptr, 0, blen, lane, own && blen >= 4, pre);
+      if (kForm < 5) piece_preload<kD, kAux>(bptr, 0, blen, lane, own && blen >= 4, pre);
       bool big = false;
 #pragma unroll
       for (uint32_t j = 0; j < 8; j++) big |= (tid + 1024u * j < args.n) & (L[j] > kPerBufMax);
       const uint32_t any_big = __ballot(big) ? 1u : 0u;
       if (own) {
         // younger wave slots issue first (the round-3 per-buffer form below)
-        if (slot >= 12) __builtin_amdgcn_s_setprio(3);
-        else if (slot >= 8) __builtin_amdgcn_s_setprio(2);
-        else if (slot >= 4) __builtin_amdgcn_s_setprio(1);
+        if (kPrioMode == 0) {
+          if (slot >= 12) __builtin_amdgcn_s_setprio(3);
+          else if (slot >= 8) __builtin_amdgcn_s_setprio(2);
+          else if (slot >= 4) __builtin_amdgcn_s_setprio(1);
+        } else if (kPrioMode == 1) {
+          __builtin_amdgcn_s_setprio(3);
+        }
         uint32_t r;
         if (blen < 4) {
           r = ~bseed;
           for (uint32_t p = 0; p < (uint32_t)blen; p++) r = (r >> 8) ^ tab->stdtab[(r ^ bptr[p]) & 0xFFu];
         } else {
-          r = piece_raw<kD, kAblate, kAux, false, true>(s_lds, bptr, 0, blen, bseed, lane, nullptr, pre);
+          r = piece_raw<kD, kAblate, kAux, false, true, kPrioMode == 1>(s_lds, bptr, 0, blen, bseed, lane, nullptr,
+                                                                        pre);
         }
         if (lane == 0) args.out[b] = ~r;
         if (kStamp && lane == 0) {  // diagnostic build (tools/c2_probe): this wave's timeline
@@ -988,6 +1005,7 @@ __global__ __launch_bounds__(kThreads) void crc32_batch_kernel(BatchArgs args) {
           args.stamps[8 * w + 5] = t_fill;
           args.stamps[8 * w + 6] = t_lens;
         }
+        if (kPrioMode == 1) __builtin_amdgcn_s_setprio(0);
       }
       __syncthreads();  // every wave is done with the tables: the LDS is free
       if (lane == 0) s_lds[slot] = any_big;
@@ -1139,7 +1157,17 @@ __global__ __launch_bounds__(kThreads) void crc32_batch_kernel(BatchArgs args) {
   uint64_t Td = (args.ctr && shift) ? (total >> shift) : 0;
   if (Td / W < unit) Td = 0;  // fewer units than waves: static only
   const uint64_t Ts = total - Td;
-  const uint64_t units = Td ? (Td + unit - 1) / unit : 0;
+  // dyn_tail (A/B knob): the last min(Td / 2, dyn_tail * W half units) bytes
+  // go out in half units, so that the last claims are shorter
+  const uint64_t half = unit / 2;
+  uint64_t Ut = 0;
+  if (Td && args.dyn_tail) {
+    const uint64_t tb = (uint64_t)args.dyn_tail * W * half;
+    Ut = (tb < Td / 2 ? tb : Td / 2) / half;
+  }
+  const uint64_t Tm = total - Ut * half;  // the main units cover [Ts, Tm)
+  const uint64_t Um = Td ? (Tm - Ts + unit - 1) / unit : 0;
+  const uint64_t units = Um + Ut;
 
   // nominal boundary of wave k: floor(k * Ts / W), without 128-bit math
   const uint64_t q_tot = Ts / W, r_tot = Ts % W;
@@ -1208,10 +1236,11 @@ __global__ __launch_bounds__(kThreads) void crc32_batch_kernel(BatchArgs args) {
     have_next = false;
     u = uni32(nx);
     if (u >= units) break;
-    const uint64_t t0 = Ts + (uint64_t)u * unit;
+    const uint64_t t0 = u < Um ? Ts + (uint64_t)u * unit : Tm + (uint64_t)(u - Um) * half;
+    const uint64_t t1 = u < Um ? (Ut && u + 1 == Um ? Tm : t0 + unit) : t0 + half;
     last = (u + 1 == units);
     if (kStamp) n_dyn++;
-    bv.range(t0, t0 + unit, last, S0, S1, f0, lb1);
+    bv.range(t0, t1, last, S0, S1, f0, lb1);
     salt = u ^ 0x9E3779B9u;
     if (kPrio && band) __builtin_amdgcn_s_setprio(0);
     band = false;

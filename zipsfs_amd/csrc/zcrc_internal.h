@@ -58,6 +58,7 @@ struct BatchArgs {
   uint32_t *ctr;
   uint32_t dyn_shift;
   uint64_t dyn_unit;
+  uint32_t dyn_tail;  // the last min(Td / 2, dyn_tail x waves) half units (0: none; an A/B knob)
   // fused small batches (kFusedMaxN): lengths to scan in-kernel (the scan is
   // written to `prefix`), split-piece accumulators (n words) and the
   // finished-wave counter; acc, *ctr and *done are zero at launch and left
@@ -154,12 +155,23 @@ constexpr uint32_t kSizeClasses = kSmallMax / 256 + 1;  // small list order: 256
 constexpr uint32_t kTileWords = 6;
 constexpr uint64_t kBigMin = 1ull << 20;  // split plan: buffers of at least this go last in the batch kernel's order
 constexpr uint64_t kPlanDirectTiles = 512;  // up to this many tiles each scatter workgroup sums the tile words itself
-// split plan tiles: 1024 * kSplitPerThread buffers per plan_split_count /
-// plan_split_scatter workgroup (the small list is ordered by size class
-// tile by tile)
-constexpr uint32_t kSplitPerThread = 8;
-constexpr uint64_t kSplitTile = 1024u * kSplitPerThread;
-inline uint64_t split_tiles(uint64_t n) { return n == 0 ? 1 : (n + kSplitTile - 1) / kSplitTile; }
+// split plan tiles: 1024 x per buffers per plan_split_count / plan_split_scatter
+// workgroup, per the smallest of 1, 2, 4, 8 that keeps the tiles within
+// kSplitMaxTiles (round 4: config 4's 100k buffers in 98 tiles of 1024 --
+// 11.2 us per plan -- instead of 13 of 8192 -- 24.2 us; 1M buffers 20.9 us
+// at per 4, 44.6 at per 1, whose 977 tiles go through plan_split_tiles;
+// tools/plan_probe, profiles/r04/s6).  The small list is ordered by size
+// class tile by tile.
+constexpr uint64_t kSplitMaxTiles = 256;
+inline uint32_t split_per_thread(uint64_t n) {
+  uint32_t per = 1;
+  while (per < 8 && (n + 1024ull * per - 1) / (1024ull * per) > kSplitMaxTiles) per *= 2;
+  return per;
+}
+inline uint64_t split_tiles(uint64_t n) {
+  const uint64_t t = 1024ull * split_per_thread(n);
+  return n == 0 ? 1 : (n + t - 1) / t;
+}
 constexpr uint32_t kSmallCostDefault = 14;  // 3.5 batch-kernel bytes (zcrc_kernels.hip, plan_split_scatter)
 
 }  // namespace zcrc

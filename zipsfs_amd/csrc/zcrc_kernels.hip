@@ -117,8 +117,9 @@ __global__ __launch_bounds__(1024) void plan_one_tile(const uint64_t *lens, uint
 
 // ------------------------------------------------------------ split plan
 // Two passes like plan_tile_sums/plan_tile_scan, both with plan_one_tile's
-// coalesced layout: wave w of a tile owns its buffers [512w, 512w + 512), lane
-// l takes 512w + 64k + l for k < 8.  Buffers fall into three classes: small
+// coalesced layout at kPer buffers per thread (split_per_thread: tiles of
+// 1024 kPer buffers): wave w of a tile owns its buffers [64 kPer w, 64 kPer
+// (w + 1)), lane l takes 64 kPer w + 64 k + l for k < kPer.  Buffers fall into three classes: small
 // (<= kSmallMax), big (>= kBigMin) and medium (between).  Per tile
 // (kTileWords): medium bytes, big bytes, small bytes, the medium and big
 // counts packed (low / high half), the small count and the small lengths'
@@ -413,8 +414,12 @@ hipError_t launch_plan_split_t(const SplitPlan &p, hipStream_t stream) {
 }
 
 hipError_t launch_plan_split(const SplitPlan &p, hipStream_t stream) {
-  static_assert(kSplitTile == 1024u * kSplitPerThread, "split tile: 16 waves x 64 lanes x kSplitPerThread");
-  return launch_plan_split_t<kSplitPerThread>(p, stream);
+  switch (split_per_thread(p.n)) {
+    case 1: return launch_plan_split_t<1>(p, stream);
+    case 2: return launch_plan_split_t<2>(p, stream);
+    case 4: return launch_plan_split_t<4>(p, stream);
+    default: return launch_plan_split_t<8>(p, stream);
+  }
 }
 
 // ------------------------------------------------------------ launchers

@@ -321,6 +321,14 @@ uint64_t dyn_unit_override() {
   return v;
 }
 
+// Measurement knob: ZCRC_DYN_TAIL = k hands the dynamic part's last
+// min(Td / 2, k x waves) half units out after the full ones (BatchArgs::dyn_tail;
+// read per call)
+uint32_t dyn_tail_setting() {
+  const char *e = getenv("ZCRC_DYN_TAIL");
+  return e ? (uint32_t)strtoul(e, nullptr, 0) : 0u;
+}
+
 // Measurement knob: ZCRC_DYN_SHIFT overrides the dynamic part's share
 // (total >> shift; 0 = none; unset = by mean buffer size, kDynAuto).
 uint32_t dyn_shift_setting() {
@@ -442,6 +450,7 @@ int batch_device_split(const DeviceCtx &dc, const void *const *d_ptrs, const uin
   a.ctr = p.ctr;
   a.dyn_shift = dyn_shift_setting();
   a.dyn_unit = dyn_unit_override();
+  a.dyn_tail = dyn_tail_setting();
   a.fault = reinterpret_cast<uint32_t *>(b + kFaultByte);
   ZCRC_HIP_TRY(launch_plan_split(p, stream));
   ZCRC_HIP_TRY(test_corrupt_prefix(p.prefix_c, n, stream));
@@ -474,6 +483,7 @@ int batch_device_ws(const void *const *d_ptrs, const uint64_t *d_lens, const uin
   a.ctr = d_ctr;
   a.dyn_shift = dyn_shift_setting();
   a.dyn_unit = dyn_unit_override();
+  a.dyn_tail = dyn_tail_setting();
   a.fault = reinterpret_cast<uint32_t *>(static_cast<uint8_t *>(scratch) + kFaultByte);
   a.lens = d_lens;  // the kernel checks every piece's prefix bounds against it
   ZCRC_HIP_TRY(test_corrupt_prefix(d_prefix, n, stream));
