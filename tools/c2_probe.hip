@@ -191,10 +191,10 @@ int main(int argc, char **argv) {
   std::vector<hipEvent_t> ev(2 * kBatches);
   for (auto &e : ev) CHECK(hipEventCreate(&e));
   enum { kProbeWave, kProbeGrid, kCrc, kCrcFused, kCrcFusedR3, kCrcFused5, kProbePb, kProbePbRot, kProbePbNoPrio,
-         kProbePbFat, kCrcFused14, kCrcFused24, kCrcFused15, kNumV };
+         kProbePbFat, kCrcFused14, kCrcFused24, kCrcFused15, kCrcFused104, kCrcFused204, kCrcFused105, kNumV };
   const char *names[kNumV] = {"probe-wave", "probe-grid", "crc", "crc-fused", "crc-fused-r3", "crc-fused-5", "probe-pb",
                               "probe-pb-rot", "probe-pb-np", "probe-pb-fat", "crc-fused-14", "crc-fused-24",
-                              "crc-fused-15"};
+                              "crc-fused-15", "crc-fused-104", "crc-fused-204", "crc-fused-105"};
   auto launch = [&](int v, int b, hipEvent_t e0, hipEvent_t e1) {
     const uint8_t *base = data + b * kBatchBytes;
     switch (v) {
@@ -240,6 +240,18 @@ int main(int argc, char **argv) {
         hipExtLaunchKernelGGL((crc32_batch_kernel<false, kDepth, 0, true, false, 1, kLoadNt, true, kWindowed, 24>),
                               dim3(cus), dim3(kThreads), 0, 0, e0, e1, 0, crc_args(b, true));
         break;
+      case kCrcFused104:
+        hipExtLaunchKernelGGL((crc32_batch_kernel<false, kDepth, 0, true, false, 1, kLoadNt, true, kWindowed, 104>),
+                              dim3(cus), dim3(kThreads), 0, 0, e0, e1, 0, crc_args(b, true));
+        break;
+      case kCrcFused204:
+        hipExtLaunchKernelGGL((crc32_batch_kernel<false, kDepth, 0, true, false, 1, kLoadNt, true, kWindowed, 204>),
+                              dim3(cus), dim3(kThreads), 0, 0, e0, e1, 0, crc_args(b, true));
+        break;
+      case kCrcFused105:
+        hipExtLaunchKernelGGL((crc32_batch_kernel<false, kDepth, 0, true, false, 1, kLoadNt, true, kWindowed, 105>),
+                              dim3(cus), dim3(kThreads), 0, 0, e0, e1, 0, crc_args(b, true));
+        break;
       case kCrcFused15:
         hipExtLaunchKernelGGL((crc32_batch_kernel<false, kDepth, 0, true, false, 1, kLoadNt, true, kWindowed, 15>),
                               dim3(cus), dim3(kThreads), 0, 0, e0, e1, 0, crc_args(b, true));
@@ -272,7 +284,7 @@ int main(int argc, char **argv) {
   launch(kCrcFused5, 0, nullptr, nullptr);
   CHECK(hipMemcpy(o4.data(), out, 4 * kN, hipMemcpyDeviceToHost));
   bool eq = o1 == o2 && o1 == o3 && o1 == o4;
-  for (int v : {kCrcFused14, kCrcFused24, kCrcFused15}) {
+  for (int v : {kCrcFused14, kCrcFused24, kCrcFused15, kCrcFused104, kCrcFused204, kCrcFused105}) {
     launch(v, 0, nullptr, nullptr);
     CHECK(hipMemcpy(o4.data(), out, 4 * kN, hipMemcpyDeviceToHost));
     eq = eq && o1 == o4;
@@ -294,6 +306,9 @@ int main(int argc, char **argv) {
                             dim3(cus), dim3(kThreads), 0, 0, ev[0], ev[1], 0, a);
     else if (fused && pb == 14)
       hipExtLaunchKernelGGL((crc32_batch_kernel<false, kDepth, 0, true, true, 1, kLoadNt, true, kWindowed, 14>),
+                            dim3(cus), dim3(kThreads), 0, 0, ev[0], ev[1], 0, a);
+    else if (fused && pb == 204)
+      hipExtLaunchKernelGGL((crc32_batch_kernel<false, kDepth, 0, true, true, 1, kLoadNt, true, kWindowed, 204>),
                             dim3(cus), dim3(kThreads), 0, 0, ev[0], ev[1], 0, a);
     else if (fused && pb == 24)
       hipExtLaunchKernelGGL((crc32_batch_kernel<false, kDepth, 0, true, true, 1, kLoadNt, true, kWindowed, 24>),
@@ -352,5 +367,6 @@ int main(int argc, char **argv) {
   timeline("crc-fused-5", true, 9, 5);
   timeline("crc-fused-14", true, 11, 14);
   timeline("crc-fused-24", true, 13, 24);
+  timeline("crc-fused-204", true, 15, 204);
   return 0;
 }

@@ -921,7 +921,10 @@ __global__ __launch_bounds__(kThreads) void crc32_batch_kernel(BatchArgs args) {
     // guarded length loads waited for one at a time: the table fill
     // completed 7.7 us after entry, now 3.5 us; tools/c2_probe,
     // profiles/r03/s11, s16.)
-    constexpr int kForm = kPB % 10, kPrioMode = kPB / 10;  // kPrioMode: 0 by slot, 1 by progress, 2 none
+    // kPrioMode: 0 by slot, 1 by progress, 2 none; kDP: blocks per register
+    // group in the per-buffer path (kPB + 100: 6, + 200: 8; two groups in flight)
+    constexpr int kForm = kPB % 10, kPrioMode = (kPB / 10) % 10;
+    constexpr uint32_t kDP = (kPB / 100) == 1 ? 6u : (kPB / 100) == 2 ? 8u : kD;
     if (kForm >= 4 && args.n <= (uint64_t)grid * kWaves) {
       // Round 4: nothing in front of the payload waits on memory but the
       // wave's own descriptor.  The braid and combine tables are built in
@@ -952,10 +955,10 @@ __global__ __launch_bounds__(kThreads) void crc32_batch_kernel(BatchArgs args) {
       }
       const bool own = b < args.n && blen <= kPerBufMax;  // wave-uniform
       const uint8_t *bptr = reinterpret_cast<const uint8_t *>(bp);
-      uint4 pre[2 * kD];
+      uint4 pre[2 * kDP];
       // kPB >= 5: the first payload loads go out as soon as the descriptor is
       // in, ahead of the table build (A/B form)
-      if (kForm >= 5) piece_preload<kD, kAux>(bptr, 0, blen, lane, own && blen >= 4, pre);
+      if (kForm >= 5) piece_preload<kDP, kAux>(bptr, 0, blen, lane, own && blen >= 4, pre);
       if (wg_busy) {
         const uint32_t e = braid_gen_lane(lane, slot);
         uint4 *dst = reinterpret_cast<uint4 *>(s_lds);
@@ -974,7 +977,7 @@ __global__ __launch_bounds__(kThreads) void crc32_batch_kernel(BatchArgs args) {
       const uint64_t t_lens = kStamp ? __builtin_amdgcn_s_memrealtime() : 0;  // diagnostic: tables written
       __syncthreads();  // the tables are in LDS
       const uint64_t t_fill = kStamp ? __builtin_amdgcn_s_memrealtime() : 0;
-      if (kForm < 5) piece_preload<kD, kAux>(bptr, 0, blen, lane, own && blen >= 4, pre);
+      if (kForm < 5) piece_preload<kDP, kAux>(bptr, 0, blen, lane, own && blen >= 4, pre);
       bool big = false;
 #pragma unroll
       for (uint32_t j = 0; j < 8; j++) big |= (tid + 1024u * j < args.n) & (L[j] > kPerBufMax);
@@ -993,7 +996,7 @@ __global__ __launch_bounds__(kThreads) void crc32_batch_kernel(BatchArgs args) {
           r = ~bseed;
           for (uint32_t p = 0; p < (uint32_t)blen; p++) r = (r >> 8) ^ tab->stdtab[(r ^ bptr[p]) & 0xFFu];
         } else {
-          r = piece_raw<kD, kAblate, kAux, false, true, kPrioMode == 1>(s_lds, bptr, 0, blen, bseed, lane, nullptr,
+          r = piece_raw<kDP, kAblate, kAux, false, true, kPrioMode == 1>(s_lds, bptr, 0, blen, bseed, lane, nullptr,
                                                                         pre);
         }
         if (lane == 0) args.out[b] = ~r;
