@@ -146,7 +146,7 @@ def test_config4_sample_zipf(golden):
     np.testing.assert_array_equal(u32(z.crc32_batch_device(ptrs, lens)), cfg["cfg4"])
 
 
-@pytest.mark.parametrize("n_bytes,lead", [(64 << 20, 0), ((64 << 20) + 3, 5), (300_000_007, 11)])
+@pytest.mark.parametrize("n_bytes,lead", [(64 << 20, 0), ((64 << 20) + 3, 5), (300_000_007, 11), (4_500_000_017, 3)])
 def test_single_large_buffer_split_across_waves(n_bytes, lead):
     mem = torch.empty(n_bytes + 64, dtype=torch.uint8, device=DEV)
     ptrs = torch.tensor([mem.data_ptr() + lead], dtype=torch.int64, device=DEV)

@@ -70,6 +70,7 @@ struct Variant {
   uint64_t big_min;
   uint64_t dyn_unit;  // 0: kDynUnit
   uint32_t dyn_tail;  // BatchArgs::dyn_tail
+  uint32_t ab_flags;  // BatchArgs::ab_flags
 };
 
 int main(int argc, char **argv) {
@@ -147,12 +148,12 @@ int main(int argc, char **argv) {
   a.fault = reinterpret_cast<uint32_t *>(scratch + kFaultByte);
 
   const Variant vs[] = {
-      {"default", kSmallCostDefault, kBigMin, 0, 0},
-      {"tail1", kSmallCostDefault, kBigMin, 0, 1},
-      {"tail2", kSmallCostDefault, kBigMin, 0, 2},
-      {"tail4", kSmallCostDefault, kBigMin, 0, 4},
-      {"u256t4", kSmallCostDefault, kBigMin, 256ull << 10, 4},
-      {"u64k", kSmallCostDefault, kBigMin, 64ull << 10, 0},
+      {"default", kSmallCostDefault, kBigMin, 0, 0, 0},
+      {"oldshift", kSmallCostDefault, kBigMin, 0, 0, 1},
+      {"tail1", kSmallCostDefault, kBigMin, 0, 1, 0},
+      {"u96k", kSmallCostDefault, kBigMin, 96ull << 10, 0, 0},
+      {"u64k", kSmallCostDefault, kBigMin, 64ull << 10, 0, 0},
+      {"u64k-old", kSmallCostDefault, kBigMin, 64ull << 10, 0, 1},
   };
   const int nv = (int)(sizeof vs / sizeof vs[0]);
   auto set = [&](const Variant &v) {
@@ -160,6 +161,7 @@ int main(int argc, char **argv) {
     p.big_min = v.big_min;
     a.dyn_unit = v.dyn_unit;
     a.dyn_tail = v.dyn_tail;
+    a.ab_flags = v.ab_flags;
   };
   hipEvent_t e0, e1, k0, k1;
   CK(hipEventCreate(&e0));
@@ -251,9 +253,10 @@ int main(int argc, char **argv) {
     std::vector<double> entry, search, begin, send, end, s_begin, s_end;
     std::vector<double> slot_end[kWaves];
     struct Row {
-      double end, send;
-      uint64_t w, pieces, dyn, sbytes;
+      double end, send, search, claim;
+      uint64_t w, pieces, dyn;
     };
+    std::vector<double> searches, claims;
     std::vector<Row> rows;
     for (uint64_t w = 0; w < nw; w++) {
       if (!st[8 * w + 1]) continue;
@@ -270,7 +273,10 @@ int main(int argc, char **argv) {
       send.push_back(se);
       end.push_back(e);
       slot_end[w % kWaves].push_back(e);
-      rows.push_back({e, se, w, st[8 * w + 2], st[8 * w + 6], st[8 * w + 7]});
+      rows.push_back({e, se, st[8 * w + 6] * 1e-2, st[8 * w + 7] * 1e-2, w, st[8 * w + 2] & 0xFFFFFFFFull,
+                      st[8 * w + 2] >> 32});
+      searches.push_back(st[8 * w + 6] * 1e-2);
+      claims.push_back(st[8 * w + 7] * 1e-2);
     }
     printf("stamped launch (%s): %.2f us (events), CRCs %s; split %llu: %llu batch buffers, %llu small on %u workgroups "
            "(%u lanes each)\n",
@@ -288,17 +294,20 @@ int main(int argc, char **argv) {
     row("batch end", end);
     row("small begin", s_begin);
     row("small end", s_end);
+    row("unit searches (sum)", searches);
+    row("claim waits (sum)", claims);
     std::sort(rows.begin(), rows.end(), [](const Row &x, const Row &y) { return x.end > y.end; });
-    printf("last waves: w (cu, slot) end | static end | pieces dyn_units static_KiB\n");
+    printf("last waves: w (cu, slot) end | static end | pieces dyn_units | unit searches, claim waits (us)\n");
     for (size_t i = 0; i < rows.size() && i < 24; i++)
-      printf("  %5llu (%3llu,%2llu) %7.1f | %7.1f | %5llu %3llu %8.1f\n", (unsigned long long)rows[i].w,
+      printf("  %5llu (%3llu,%2llu) %7.1f | %7.1f | %5llu %3llu | %6.1f %6.1f\n", (unsigned long long)rows[i].w,
              (unsigned long long)(rows[i].w / kWaves), (unsigned long long)(rows[i].w % kWaves), rows[i].end,
-             rows[i].send, (unsigned long long)rows[i].pieces, (unsigned long long)rows[i].dyn, rows[i].sbytes / 1024.0);
+             rows[i].send, (unsigned long long)rows[i].pieces, (unsigned long long)rows[i].dyn, rows[i].search,
+             rows[i].claim);
     printf("end p50 by wave slot:");
     for (int s = 0; s < kWaves; s++) printf(" %.0f", pct(slot_end[s], .5));
     printf("\n");
   };
   stamped(vs[0]);
-  stamped(vs[2]);
+  stamped(vs[1]);
   return 0;
 }

@@ -180,8 +180,41 @@ __device__ __forceinline__ uint32_t mct_apply_global(const uint32_t *t, uint32_t
   return t[r & 0xFFu] ^ t[256 + ((r >> 8) & 0xFFu)] ^ t[512 + ((r >> 16) & 0xFFu)] ^ t[768 + (r >> 24)];
 }
 
-// r * x^(8*nbytes), nbytes arbitrary (split pieces only: once per wave range).
-__device__ uint32_t shift_bytes(const TableBlob *tab, uint32_t r, uint64_t nbytes) {
+// a * b for wave-uniform operands, on the scalar unit (bit-serial: 32 steps of
+// a few SALU instructions, off the VALU the stream needs)
+__device__ __forceinline__ uint32_t gf2_mul_uniform(uint32_t a, uint32_t b) {
+  a = (uint32_t)__builtin_amdgcn_readfirstlane((int)a);
+  b = (uint32_t)__builtin_amdgcn_readfirstlane((int)b);
+  uint32_t p = 0;
+#pragma unroll
+  for (int i = 0; i < 32; i++) {
+    if ((a >> (31 - i)) & 1u) p ^= b;
+    b = (b >> 1) ^ ((b & 1u) ? kPolyReflected : 0u);
+  }
+  return (uint32_t)__builtin_amdgcn_readfirstlane((int)p);
+}
+
+// r * x^(8*nbytes) (split pieces: once per piece, r wave-uniform).  A split
+// piece ends on a whole 64 KiB grain before the buffer end (kSplitGrain), so
+// nbytes = 65536 m and x^(8 nbytes) is at most four products of
+// x8grain[j][byte j of m], whose four scalar loads go out together.  (The
+// round-1..3 form multiplied by x8pow[k] for every set bit k of nbytes: a
+// vector load waited for with vmcnt(0) and ~200 VALU per bit, 4-8 times a
+// piece.)  Other lengths take the per-bit path.
+__device__ __forceinline__ uint32_t shift_bytes(const TableBlob *tab, uint32_t r, uint64_t nbytes,
+                                                bool per_bit = false) {
+  if (!per_bit && (nbytes & (kSplitGrain - 1)) == 0 && (nbytes >> 48) == 0) {
+    typedef const __attribute__((address_space(4))) uint32_t const_u32;  // scalar loads
+    const const_u32 *g = (const const_u32 *)&tab->x8grain[0][0];
+    const uint32_t m = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(nbytes >> 16));  // uniform: s_load
+    const uint32_t f0 = g[m & 255u], f1 = g[256u + ((m >> 8) & 255u)], f2 = g[512u + ((m >> 16) & 255u)],
+                   f3 = g[768u + (m >> 24)];
+    r = gf2_mul_uniform(f0, r);
+    if (m >> 8) r = gf2_mul_uniform(f1, r);
+    if (m >> 16) r = gf2_mul_uniform(f2, r);
+    if (m >> 24) r = gf2_mul_uniform(f3, r);
+    return r;
+  }
   int k = 0;
   while (nbytes) {
     if (nbytes & 1u) r = gf2_mul(tab->x8pow[k], r);
@@ -617,7 +650,7 @@ __device__ __forceinline__ uint64_t process_range(const BatchArgs &args, const B
       if (lane == 0) args.out[oi] = ~r;
     } else {
       const uint64_t d = n - rel_hi;  // bytes after this piece, multiple of kSplitGrain
-      uint32_t contrib = d ? shift_bytes(tab, r, d) : (r ^ 0xFFFFFFFFu);
+      uint32_t contrib = d ? shift_bytes(tab, r, d, args.ab_flags & 1u) : (r ^ 0xFFFFFFFFu);
       if (kFused) {
         if (lane == 0) split_accumulate(args, i, n, rel_lo, rel_hi, contrib);
       } else if (lane == 0) {
@@ -1201,7 +1234,6 @@ __global__ __launch_bounds__(kThreads) void crc32_batch_kernel(BatchArgs args) {
 
   // diagnostic build: wall-clock stamps (s_memrealtime, 100 MHz) per wave
   const uint64_t t_begin = kStamp ? __builtin_amdgcn_s_memrealtime() : 0;
-  const uint64_t static_bytes = S1 - S0;
   uint64_t npieces = 0;
   uint32_t salt = (uint32_t)w;
   // Claims: wave w's first unit is unit w, taken without the counter (all
@@ -1217,7 +1249,8 @@ __global__ __launch_bounds__(kThreads) void crc32_batch_kernel(BatchArgs args) {
   uint32_t u = 0, nx = 0;
   bool have_next = false, first_claim = true;
   uint64_t t_tail = 0;                 // diagnostic build: time in the alignment-padding MCTs (unused)
-  uint64_t t_static_end = 0, n_dyn = 0;  // ... the static range's end, dynamic units taken
+  uint64_t t_static_end = 0, n_dyn = 0;  // ... the static range's end, dynamic units taken,
+  uint64_t t_claim = 0, t_usearch = 0;   // time waiting for unprefetched claims, in unit range searches
   for (;;) {
     if (!band && u + 2 * (uint32_t)W < units) {
       if (lane == 0) nx = (uint32_t)W + atomicAdd(args.ctr, 1u);
@@ -1228,6 +1261,7 @@ __global__ __launch_bounds__(kThreads) void crc32_batch_kernel(BatchArgs args) {
           args, bv, s_lds, tab, S0, S1, last, salt, lane, band, f0, lb1, &t_tail, perbuf_done);
     if (kStamp && first_claim) t_static_end = __builtin_amdgcn_s_memrealtime();
     if (!units) break;
+    const uint64_t tc0 = kStamp ? __builtin_amdgcn_s_memrealtime() : 0;
     if (first_claim) {
       nx = (uint32_t)w;  // units >= W whenever the dynamic part is on
     } else if (units <= W) {
@@ -1238,12 +1272,15 @@ __global__ __launch_bounds__(kThreads) void crc32_batch_kernel(BatchArgs args) {
     first_claim = false;
     have_next = false;
     u = uni32(nx);
+    if (kStamp) t_claim += __builtin_amdgcn_s_memrealtime() - tc0;
     if (u >= units) break;
     const uint64_t t0 = u < Um ? Ts + (uint64_t)u * unit : Tm + (uint64_t)(u - Um) * half;
     const uint64_t t1 = u < Um ? (Ut && u + 1 == Um ? Tm : t0 + unit) : t0 + half;
     last = (u + 1 == units);
     if (kStamp) n_dyn++;
+    const uint64_t ts0 = kStamp ? __builtin_amdgcn_s_memrealtime() : 0;
     bv.range(t0, t1, last, S0, S1, f0, lb1);
+    if (kStamp) t_usearch += __builtin_amdgcn_s_memrealtime() - ts0;
     salt = u ^ 0x9E3779B9u;
     if (kPrio && band) __builtin_amdgcn_s_setprio(0);
     band = false;
@@ -1260,12 +1297,12 @@ __global__ __launch_bounds__(kThreads) void crc32_batch_kernel(BatchArgs args) {
   if (kStamp && lane == 0) {  // (tools/c2_probe, tools/c4_probe)
     args.stamps[8 * w + 0] = t_begin;
     args.stamps[8 * w + 1] = __builtin_amdgcn_s_memrealtime();
-    args.stamps[8 * w + 2] = npieces;
+    args.stamps[8 * w + 2] = npieces | (n_dyn << 32);
     args.stamps[8 * w + 3] = t_static_end;
     args.stamps[8 * w + 4] = t_entry;
     args.stamps[8 * w + 5] = t_search;
-    args.stamps[8 * w + 6] = n_dyn;
-    args.stamps[8 * w + 7] = static_bytes;
+    args.stamps[8 * w + 6] = t_usearch;
+    args.stamps[8 * w + 7] = t_claim;
   }
 }
 

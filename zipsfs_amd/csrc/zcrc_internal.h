@@ -23,6 +23,11 @@ constexpr uint32_t kPlanPerThread = 8;
 constexpr bool kWindowed = true;       // piece descriptors fetched 64 at a time
 constexpr uint64_t kFusedMaxN = 8192;  // one-launch small batches: the kernel scans the lengths itself
 constexpr uint64_t kPerBufMax = kMinRange;  // one-launch batches of buffers up to this: one wave per buffer
+// the per-buffer mode's form in the product (crc32_batch_kernel's kPB): 15 =
+// the first payload loads ahead of the table build, priority by progress
+// (round 4: 45.7-46.3 us against 46.6-47.1 for 4 on config 2, two boxes;
+// tools/c2_probe, profiles/r04/s7, s8)
+constexpr int kPerBufForm = 15;
 constexpr uint64_t kPlanTile = 1024 * kPlanPerThread;
 // one launch covers at most this many bytes (keeps every piece < 2 GiB)
 constexpr uint64_t kMaxLaunchBytes = 1ull << 42;
@@ -36,6 +41,7 @@ struct TableBlob {
   uint32_t x8pow[64];            // x^(8 * 2^k)
   uint32_t braid256[4 * 256];    // MCT(x^(8*256)): the small-buffer kernel's table
   uint32_t xinv8[256];           // r * x^-8 = (r << 8) ^ xinv8[r >> 24] (one zero byte taken off)
+  uint32_t x8grain[4][256];      // x^(8 * 65536 * m * 256^j): a split piece's shift by whole 64 KiB grains
 };
 
 struct BatchArgs {
@@ -59,6 +65,7 @@ struct BatchArgs {
   uint32_t dyn_shift;
   uint64_t dyn_unit;
   uint32_t dyn_tail;  // the last min(Td / 2, dyn_tail x waves) half units (0: none; an A/B knob)
+  uint32_t ab_flags;  // A/B knobs for tools/ (0 in the product): bit 0 = split shifts bit by bit (rounds 1-3)
   // fused small batches (kFusedMaxN): lengths to scan in-kernel (the scan is
   // written to `prefix`), split-piece accumulators (n words) and the
   // finished-wave counter; acc, *ctr and *done are zero at launch and left

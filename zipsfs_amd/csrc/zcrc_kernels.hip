@@ -430,8 +430,8 @@ hipError_t launch_batch(const BatchArgs &args, bool strided, int num_cus, hipStr
   // t0/t1 (profiling): timestamps carried by the dispatch packet itself --
   // event records around the launch add ~11 us of queue bubbles per launch
   if (fused)
-    hipExtLaunchKernelGGL((crc32_batch_kernel<false, kDepth, 0, true, false, 1, kLoadNt, true>), grid, block, 0,
-                          stream, t0, t1, 0, args);
+    hipExtLaunchKernelGGL((crc32_batch_kernel<false, kDepth, 0, true, false, 1, kLoadNt, true, kWindowed, kPerBufForm>),
+                          grid, block, 0, stream, t0, t1, 0, args);
   else if (strided)
     hipExtLaunchKernelGGL((crc32_batch_kernel<true, kDepth, 0>), grid, block, 0, stream, t0, t1, 0, args);
   else
@@ -476,8 +476,8 @@ const char *fused_kernel_name() {
   static char name[160];
   static std::once_flag once;
   std::call_once(once, [] {
-    snprintf(name, sizeof name, "zcrc::crc32_batch_kernel<false, %uu, 0, true, false, 1, %d, true, %s, 4>", kDepth,
-             kLoadNt, kWindowed ? "true" : "false");
+    snprintf(name, sizeof name, "zcrc::crc32_batch_kernel<false, %uu, 0, true, false, 1, %d, true, %s, %d>", kDepth,
+             kLoadNt, kWindowed ? "true" : "false", kPerBufForm);
   });
   return name;
 }

@@ -10,6 +10,8 @@ namespace zcrc {
 // comb   = MCT(x^-32 .. x^-4096)      in-lane and cross-lane combine tree
 // tshift = MCT(x^(-8t)), t < 16       16-B alignment padding at a piece end
 // xinv8  = r * x^-8 byte table         the small-buffer kernel's last 0-3 padding bytes
+// x8grain[j][m] = x^(8 * 65536 * m * 256^j)   split pieces: r * x^(8d), d = whole
+//                                       64 KiB grains, in at most four products
 inline void build_tables(TableBlob &tb) {
   XPowTable xp;
   build_xpow_table(xp);
@@ -21,6 +23,14 @@ inline void build_tables(TableBlob &tb) {
   build_std_table(tb.stdtab);
   build_xinv8_table(tb.xinv8);
   for (int k = 0; k < 64; k++) tb.x8pow[k] = xp.x2k[k + 3];
+  for (int j = 0; j < 4; j++) {
+    const uint32_t base = xp.x2k[19 + 8 * j];  // x^(2^(19 + 8j)) = x^(8 * 65536 * 256^j)
+    uint32_t g = kOne;
+    for (int m = 0; m < 256; m++) {
+      tb.x8grain[j][m] = g;
+      g = gf2_mul(g, base);
+    }
+  }
 }
 
 }  // namespace zcrc
