@@ -74,6 +74,20 @@ __device__ __forceinline__ uint32_t braid_step(const uint32_t *lds, uint32_t x, 
   return lds_u32(lds, a0) ^ lds_u32(lds, a1) ^ lds_u32(lds, a2) ^ lds_u32(lds, a3);
 }
 
+// The same step on a register kept as two words, r = s ^ q (round 4): the
+// index is s ^ q ^ d in one three-input xor, the first three lookups are
+// combined by another and the fourth is kept as the new q -- 2 VALU besides
+// the 4 address builds, against 4 xors.
+__device__ __forceinline__ void braid_step2(const uint32_t *lds, uint32_t &s, uint32_t &q, uint32_t d, uint32_t o0,
+                                            uint32_t o1, uint32_t o2, uint32_t o3) {
+  const uint32_t x = __builtin_amdgcn_bitop3_b32(s, q, d, 0x96);  // s ^ q ^ d
+  const uint32_t t0 = lds_u32(lds, __builtin_amdgcn_perm(x, o0, ZCRC_SEL(0)));
+  const uint32_t t1 = lds_u32(lds, __builtin_amdgcn_perm(x, o1, ZCRC_SEL(1)));
+  const uint32_t t2 = lds_u32(lds, __builtin_amdgcn_perm(x, o2, ZCRC_SEL(2)));
+  q = lds_u32(lds, __builtin_amdgcn_perm(x, o3, ZCRC_SEL(3)));
+  s = __builtin_amdgcn_bitop3_b32(t0, t1, t2, 0x96);
+}
+
 // The braid entry MCT(x^8192)[j][v] this lane builds for wave `w` of the
 // per-buffer mode: j = lane >> 4, v = 4 w + (lane & 3) + 64 ((lane >> 2) & 3),
 // as the xor of the compile-time products q[8j + b] over the set bits b of v
@@ -515,8 +529,9 @@ __device__ void split_accumulate(const BatchArgs &a, uint64_t i, uint64_t n, uin
 
 // ------------------------------------------------------------ the kernel
 
-// kD: 1 KiB blocks per register group (two groups in flight); kAblate != 0
-// replaces the table lookups with one VALU op (measurement builds only).
+// kD: 1 KiB blocks per register group (two groups in flight); kAblate == 1
+// replaces the table lookups with one VALU op (measurement builds only),
+// kAblate == 2 is the round-1..3 step (three xors per dword, A/B builds).
 // Process every piece of the byte range [S0, S1) of the concatenated batch
 // (S0, S1 snapped; `last_range` also takes the trailing empty buffers).
 // Returns the number of pieces.  Wave-uniform; no barriers.
@@ -738,6 +753,11 @@ __device__ __forceinline__ uint32_t piece_raw(const uint32_t *s_lds, const uint8
     const uint32_t inj = uni32((rel_lo == 0) ? ~seed : 0u);
 
     uint32_t s0 = 0, s1 = 0, s2 = 0, s3 = 0;
+    // Round 4: a stream's register is kept as two words, s = s_k ^ q_k
+    // (braid_step2): 2 VALU per step besides the 4 v_perm address builds,
+    // against 4 xors before -- the hot loop's VALU per two 4 KiB groups went
+    // from 264 to 200 instructions.
+    uint32_t q0 = 0, q1 = 0, q2 = 0, q3 = 0;
     // Two register groups of kD blocks: one streams in while the other
     // is consumed (no register rotation, no vmcnt(0) at group boundaries).
     uint4 ga[kD], gb[kD];
@@ -750,13 +770,19 @@ __device__ __forceinline__ uint32_t piece_raw(const uint32_t *s_lds, const uint8
       G[u_] = make_uint4(v_[0], v_[1], v_[2], v_[3]);                                           \
     }                                                                                           \
   }
-#define ZCRC_STEP(x) (kAblate ? __builtin_amdgcn_alignbit((x), (x), 5) : braid_step(s_lds, (x), o0, o1, o2, o3))
-#define ZCRC_CONSUME(d)         \
-  {                             \
-    s0 = ZCRC_STEP(s0 ^ (d).x); \
-    s1 = ZCRC_STEP(s1 ^ (d).y); \
-    s2 = ZCRC_STEP(s2 ^ (d).z); \
-    s3 = ZCRC_STEP(s3 ^ (d).w); \
+#define ZCRC_STEP(x) (kAblate == 1 ? __builtin_amdgcn_alignbit((x), (x), 5) : braid_step(s_lds, (x), o0, o1, o2, o3))
+#define ZCRC_STEP2(S, Q, D) braid_step2(s_lds, (S), (Q), (D), o0, o1, o2, o3)
+#define ZCRC_CONSUME(d)                \
+  if (kAblate == 0) {                  \
+    ZCRC_STEP2(s0, q0, (d).x);         \
+    ZCRC_STEP2(s1, q1, (d).y);         \
+    ZCRC_STEP2(s2, q2, (d).z);         \
+    ZCRC_STEP2(s3, q3, (d).w);         \
+  } else {                             \
+    s0 = ZCRC_STEP(s0 ^ (d).x);        \
+    s1 = ZCRC_STEP(s1 ^ (d).y);        \
+    s2 = ZCRC_STEP(s2 ^ (d).z);        \
+    s3 = ZCRC_STEP(s3 ^ (d).w);        \
   }
   // plain group: every block strictly before block K-1, no fix-up needed
 #define ZCRC_PLAIN(G)                                                   \
@@ -817,12 +843,14 @@ __device__ __forceinline__ uint32_t piece_raw(const uint32_t *s_lds, const uint8
     }
 #undef ZCRC_LOADG
 #undef ZCRC_STEP
+#undef ZCRC_STEP2
 #undef ZCRC_CONSUME
 #undef ZCRC_PLAIN
 #undef ZCRC_EDGE
 
     // ---- fold 256 stream registers into one raw register at `aend` -------
     // stream (lane l, dword q) sits at aend + 16 l + 4 q
+    s0 ^= q0, s1 ^= q1, s2 ^= q2, s3 ^= q3;
     uint32_t r = (s0 ^ comb_apply(s_lds, 0, s1)) ^ comb_apply(s_lds, 1, s2 ^ comb_apply(s_lds, 0, s3));
     // cross-lane levels x^(-128 * 2^j): j < 4 inside 16-lane rows (DPP);
     // the last two on the four row results, read into scalars

@@ -111,9 +111,12 @@ __device__ __forceinline__ void small_body(const SmallArgs &a, uint32_t *s_lds, 
     const uint32_t inj = ~seed;
     const uint32_t kq = (active && !tiny) ? (uint32_t)(span + 255) >> 8 : 0u;
     const uint32_t kmax = uni32(__reduce_max_sync(0xFFFFFFFFFFFFFFFFull, kq));
-    uint32_t s[NS];
+    // stream t's register is s[t] ^ q[t] (q: the last step's fourth lookup,
+    // taken into the next index by a three-input xor; zcrc_batch_kernel.h
+    // piece_raw, ZCRC_STEP2)
+    uint32_t s[NS], q[NS];
 #pragma unroll
-    for (int t = 0; t < NS; t++) s[t] = 0u;
+    for (int t = 0; t < NS; t++) s[t] = 0u, q[t] = 0u;
     int32_t rel0 = kq ? span - 256 * (int32_t)kmax + 16 * C * (int32_t)lg : -(1 << 30);
     for (uint32_t k = 0; k < kmax; k += kD) {
       small_v4u d[kD][C];
@@ -135,15 +138,17 @@ __device__ __forceinline__ void small_body(const SmallArgs &a, uint32_t *s_lds, 
             uint4 w = make_uint4(d[b][c].x, d[b][c].y, d[b][c].z, d[b][c].w);
             if (rel >= 0 && (rel < rs + 4 || rel + 16 > re))
               w = fix_chunk(w, clamp_rel(rs - rel), clamp_rel(re - rel), clamp_rel(rs - rel), inj);
-            s[4 * c + 0] = braid_step(s_lds, s[4 * c + 0] ^ w.x, o0, o1, o2, o3);
-            s[4 * c + 1] = braid_step(s_lds, s[4 * c + 1] ^ w.y, o0, o1, o2, o3);
-            s[4 * c + 2] = braid_step(s_lds, s[4 * c + 2] ^ w.z, o0, o1, o2, o3);
-            s[4 * c + 3] = braid_step(s_lds, s[4 * c + 3] ^ w.w, o0, o1, o2, o3);
+            braid_step2(s_lds, s[4 * c + 0], q[4 * c + 0], w.x, o0, o1, o2, o3);
+            braid_step2(s_lds, s[4 * c + 1], q[4 * c + 1], w.y, o0, o1, o2, o3);
+            braid_step2(s_lds, s[4 * c + 2], q[4 * c + 2], w.z, o0, o1, o2, o3);
+            braid_step2(s_lds, s[4 * c + 3], q[4 * c + 3], w.w, o0, o1, o2, o3);
           }
         }
       }
       rel0 += 256 * kD;
     }
+#pragma unroll
+    for (int t = 0; t < NS; t++) s[t] ^= q[t];
     // fold: the lane's dwords sit 4 B apart, lanes 16 C B apart
 #pragma unroll
     for (int t = 0; t < LOG_NS; t++)
