@@ -1274,6 +1274,26 @@ __global__ __launch_bounds__(kThreads) void crc32_batch_kernel(BatchArgs args) {
   // current unit is processed, so the atomic's latency hides behind the
   // unit) while more than 2W units remain -- near the end a
   // held-but-unstarted unit would become a straggler.
+  // A/B (args.ctr_parts, tools/c4_probe): claims spread over kClaimParts
+  // counters 256 B apart; partition p holds units W + p + kClaimParts c, and
+  // a wave claims from partition (workgroup % kClaimParts) until it runs dry,
+  // then from the next one not known to be dry.
+  uint32_t *const cparts = args.ctr_parts;
+  uint32_t home = blockIdx.x & (kClaimParts - 1u), dry = 0;
+  auto issue = [&]() -> uint32_t { return cparts ? atomicAdd(cparts + 64u * home, 1u) : atomicAdd(args.ctr, 1u); };
+  auto resolve = [&](uint32_t c) -> uint32_t {  // raw claim -> unit (>= units: nothing left)
+    if (!cparts) return (uint32_t)W + c;
+    uint32_t uu = (uint32_t)W + home + kClaimParts * c;
+    while (uu >= units) {
+      dry |= 1u << home;
+      if (dry == (1u << kClaimParts) - 1u) return (uint32_t)units;
+      do home = (home + 1u) & (kClaimParts - 1u); while ((dry >> home) & 1u);
+      uint32_t c2 = 0;
+      if (lane == 0) c2 = atomicAdd(cparts + 64u * home, 1u);
+      uu = (uint32_t)W + home + kClaimParts * uni32(c2);
+    }
+    return uu;
+  };
   uint32_t u = 0, nx = 0;
   bool have_next = false, first_claim = true;
   uint64_t t_tail = 0;                 // diagnostic build: time in the alignment-padding MCTs (unused)
@@ -1281,7 +1301,7 @@ __global__ __launch_bounds__(kThreads) void crc32_batch_kernel(BatchArgs args) {
   uint64_t t_claim = 0, t_usearch = 0;   // time waiting for unprefetched claims, in unit range searches
   for (;;) {
     if (!band && u + 2 * (uint32_t)W < units) {
-      if (lane == 0) nx = (uint32_t)W + atomicAdd(args.ctr, 1u);
+      if (lane == 0) nx = issue();
       have_next = true;
     }
     if (S0 < S1 || last)
@@ -1291,15 +1311,15 @@ __global__ __launch_bounds__(kThreads) void crc32_batch_kernel(BatchArgs args) {
     if (!units) break;
     const uint64_t tc0 = kStamp ? __builtin_amdgcn_s_memrealtime() : 0;
     if (first_claim) {
-      nx = (uint32_t)w;  // units >= W whenever the dynamic part is on
+      u = (uint32_t)w;  // units >= W whenever the dynamic part is on
     } else if (units <= W) {
       break;  // every unit was pre-assigned: no claim (and no atomic) at all
-    } else if (!have_next && lane == 0) {
-      nx = (uint32_t)W + atomicAdd(args.ctr, 1u);
+    } else {
+      if (!have_next && lane == 0) nx = issue();
+      u = resolve(uni32(nx));
     }
     first_claim = false;
     have_next = false;
-    u = uni32(nx);
     if (kStamp) t_claim += __builtin_amdgcn_s_memrealtime() - tc0;
     if (u >= units) break;
     const uint64_t t0 = u < Um ? Ts + (uint64_t)u * unit : Tm + (uint64_t)(u - Um) * half;
