@@ -60,6 +60,36 @@ def xpow8(nbytes: int) -> int:
     return acc
 
 
+def x8grain_table() -> list:
+    """zcrc_tables.h x8grain[j][m] = x^(8 * 65536 * m * 256^j): base
+    x^(2^(19 + 8j)) raised to m (TableBlob; the split-piece shift)."""
+    x2k, v = [], ONE >> 1
+    for _ in range(51):
+        x2k.append(v)
+        v = gf2_mul(v, v)
+    out = []
+    for j in range(4):
+        g, row = ONE, []
+        for _ in range(256):
+            row.append(g)
+            g = gf2_mul(g, x2k[19 + 8 * j])
+        out.append(row)
+    return out
+
+
+def grain_shift(r: int, nbytes: int, grain=None) -> int:
+    """zcrc_batch_kernel.h shift_bytes for nbytes = 65536 m: r times at most
+    four x8grain products (byte j of m picks row j)."""
+    assert nbytes % 65536 == 0 and nbytes < 1 << 48
+    g = grain or x8grain_table()
+    m = nbytes >> 16
+    r = gf2_mul(g[0][m & 255], r)
+    for j in (1, 2, 3):
+        if m >> (8 * j):
+            r = gf2_mul(g[j][(m >> (8 * j)) & 255], r)
+    return r
+
+
 def xinvpow8(nbytes: int) -> int:
     r = ONE
     for _ in range(8 * nbytes):

@@ -343,3 +343,17 @@ def test_model_constants_mirror_the_header():
              "kSplitMaxTiles": km.K_SPLIT_MAX_TILES}
     for name, model in pairs.items():
         assert vals.get(name) == model, (name, vals.get(name), model)
+
+
+def test_grain_table_shift_equals_x_power():
+    """The split-piece shift by whole 64 KiB grains (x8grain, at most four
+    products) equals multiplying by x^(8d) bit by bit, for d across the four
+    table rows (d up to 2^42 bytes, kMaxLaunchBytes)."""
+    rnd = random.Random(8)
+    g = km.x8grain_table()
+    ds = [65536 * m for m in (1, 2, 255, 256, 257, 4577, 65535, 65536, 68664, (1 << 24) - 1, 1 << 24,
+                              (1 << 26) - 1)]
+    ds += [65536 * rnd.randrange(1, 1 << 26) for _ in range(20)]
+    for d in ds:
+        r = rnd.getrandbits(32)
+        assert km.grain_shift(r, d, g) == km.gf2_mul(km.xpow8(d), r), d
