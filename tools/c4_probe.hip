@@ -71,7 +71,6 @@ struct Variant {
   uint64_t dyn_unit;  // 0: kDynUnit
   uint32_t dyn_tail;  // BatchArgs::dyn_tail
   uint32_t ab_flags;  // BatchArgs::ab_flags
-  bool parts;         // partitioned claim counters (BatchArgs::ctr_parts)
 };
 
 int main(int argc, char **argv) {
@@ -110,9 +109,6 @@ int main(int argc, char **argv) {
   CK(hipMalloc(&scratch, sbytes));
   CK(hipMalloc(&d_out, 4 * n));
   CK(hipMalloc(&d_stamps, 64 * nw));
-  uint32_t *d_parts;
-  CK(hipMalloc(&d_parts, 256 * kClaimParts));
-  CK(hipMemset(d_parts, 0, 256 * kClaimParts));
   CK(hipMemset(scratch, 0, sbytes));
   CK(hipMemcpy(d_lens, lens.data(), 8 * n, hipMemcpyHostToDevice));
   CK(hipMemcpy(d_ptrs, ptrs.data(), 8 * n, hipMemcpyHostToDevice));
@@ -152,12 +148,10 @@ int main(int argc, char **argv) {
   a.fault = reinterpret_cast<uint32_t *>(scratch + kFaultByte);
 
   const Variant vs[] = {
-      {"default", kSmallCostDefault, kBigMin, 0, 0, 0, false},
-      {"parts8", kSmallCostDefault, kBigMin, 0, 0, 0, true},
-      {"oldshift", kSmallCostDefault, kBigMin, 0, 0, 1, false},
-      {"u64k", kSmallCostDefault, kBigMin, 64ull << 10, 0, 0, false},
-      {"u64k-p8", kSmallCostDefault, kBigMin, 64ull << 10, 0, 0, true},
-      {"tail1-p8", kSmallCostDefault, kBigMin, 0, 1, 0, true},
+      {"default", kSmallCostDefault, kBigMin, 0, 0, 0},
+      {"oldshift", kSmallCostDefault, kBigMin, 0, 0, 1},
+      {"tail1", kSmallCostDefault, kBigMin, 0, 1, 0},
+      {"u192k", kSmallCostDefault, kBigMin, 192ull << 10, 0, 0},
   };
   const int nv = (int)(sizeof vs / sizeof vs[0]);
   auto set = [&](const Variant &v) {
@@ -166,8 +160,6 @@ int main(int argc, char **argv) {
     a.dyn_unit = v.dyn_unit;
     a.dyn_tail = v.dyn_tail;
     a.ab_flags = v.ab_flags;
-    a.ctr_parts = v.parts ? d_parts : nullptr;
-    p.ctr_parts = a.ctr_parts;
   };
   hipEvent_t e0, e1, k0, k1;
   CK(hipEventCreate(&e0));

@@ -1274,26 +1274,8 @@ __global__ __launch_bounds__(kThreads) void crc32_batch_kernel(BatchArgs args) {
   // current unit is processed, so the atomic's latency hides behind the
   // unit) while more than 2W units remain -- near the end a
   // held-but-unstarted unit would become a straggler.
-  // A/B (args.ctr_parts, tools/c4_probe): claims spread over kClaimParts
-  // counters 256 B apart; partition p holds units W + p + kClaimParts c, and
-  // a wave claims from partition (workgroup % kClaimParts) until it runs dry,
-  // then from the next one not known to be dry.
-  uint32_t *const cparts = args.ctr_parts;
-  uint32_t home = blockIdx.x & (kClaimParts - 1u), dry = 0;
-  auto issue = [&]() -> uint32_t { return cparts ? atomicAdd(cparts + 64u * home, 1u) : atomicAdd(args.ctr, 1u); };
-  auto resolve = [&](uint32_t c) -> uint32_t {  // raw claim -> unit (>= units: nothing left)
-    if (!cparts) return (uint32_t)W + c;
-    uint32_t uu = (uint32_t)W + home + kClaimParts * c;
-    while (uu >= units) {
-      dry |= 1u << home;
-      if (dry == (1u << kClaimParts) - 1u) return (uint32_t)units;
-      do home = (home + 1u) & (kClaimParts - 1u); while ((dry >> home) & 1u);
-      uint32_t c2 = 0;
-      if (lane == 0) c2 = atomicAdd(cparts + 64u * home, 1u);
-      uu = (uint32_t)W + home + kClaimParts * uni32(c2);
-    }
-    return uu;
-  };
+  // (Round 4: claims spread over 8 counters 256 B apart, a wave's home
+  // counter chosen by workgroup, ran 3% slower on config 4: DESIGN.md 7d.)
   uint32_t u = 0, nx = 0;
   bool have_next = false, first_claim = true;
   uint64_t t_tail = 0;                 // diagnostic build: time in the alignment-padding MCTs (unused)
@@ -1301,7 +1283,7 @@ __global__ __launch_bounds__(kThreads) void crc32_batch_kernel(BatchArgs args) {
   uint64_t t_claim = 0, t_usearch = 0;   // time waiting for unprefetched claims, in unit range searches
   for (;;) {
     if (!band && u + 2 * (uint32_t)W < units) {
-      if (lane == 0) nx = issue();
+      if (lane == 0) nx = atomicAdd(args.ctr, 1u);
       have_next = true;
     }
     if (S0 < S1 || last)
@@ -1315,8 +1297,8 @@ __global__ __launch_bounds__(kThreads) void crc32_batch_kernel(BatchArgs args) {
     } else if (units <= W) {
       break;  // every unit was pre-assigned: no claim (and no atomic) at all
     } else {
-      if (!have_next && lane == 0) nx = issue();
-      u = resolve(uni32(nx));
+      if (!have_next && lane == 0) nx = atomicAdd(args.ctr, 1u);
+      u = (uint32_t)W + uni32(nx);
     }
     first_claim = false;
     have_next = false;

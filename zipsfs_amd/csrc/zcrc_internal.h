@@ -66,7 +66,6 @@ struct BatchArgs {
   uint64_t dyn_unit;
   uint32_t dyn_tail;  // the last min(Td / 2, dyn_tail x waves) half units (0: none; an A/B knob)
   uint32_t ab_flags;  // A/B knobs for tools/ (0 in the product): bit 0 = split shifts bit by bit (rounds 1-3)
-  uint32_t *ctr_parts;  // A/B (tools/c4_probe): kClaimParts claim counters 256 B apart, zero at launch; null: ctr
   // fused small batches (kFusedMaxN): lengths to scan in-kernel (the scan is
   // written to `prefix`), split-piece accumulators (n words) and the
   // finished-wave counter; acc, *ctr and *done are zero at launch and left
@@ -157,7 +156,6 @@ struct SplitPlan {
   uint64_t big_min;       // on a split, buffers of at least this go after the others (kBigMin)
   uint32_t direct_ok;     // a batch of about equal small buffers may skip the lists (mode 2)
   uint64_t *stamps;       // diagnostics (tools/plan_probe): 8 s_memrealtime stamps per scatter workgroup, or null
-  uint32_t *ctr_parts;    // A/B (tools/c4_probe): the batch kernel's partitioned claim counters (zeroed), or null
 };
 hipError_t launch_plan_split(const SplitPlan &p, hipStream_t stream);
 constexpr uint32_t kSizeClasses = kSmallMax / 256 + 1;  // small list order: 256-B block count
@@ -181,7 +179,6 @@ inline uint64_t split_tiles(uint64_t n) {
   const uint64_t t = 1024ull * split_per_thread(n);
   return n == 0 ? 1 : (n + t - 1) / t;
 }
-constexpr uint32_t kClaimParts = 8;  // BatchArgs::ctr_parts (A/B): a wave claims from partition (workgroup % 8) first
 constexpr uint32_t kSmallCostDefault = 14;  // 3.5 batch-kernel bytes (zcrc_kernels.hip, plan_split_scatter)
 
 }  // namespace zcrc

@@ -216,7 +216,6 @@ __global__ __launch_bounds__(1024) void plan_split_scatter(SplitPlan p) {
   uint64_t st[6] = {0, 0, 0, 0, 0, 0};  // diagnostics: phase stamps (p.stamps)
   if (p.stamps) st[0] = __builtin_amdgcn_s_memrealtime();
   if (blockIdx.x == 0 && tid == 0) p.ctr[0] = 0u, p.ctr[kFaultByte / 4] = 0u;  // work counter, fault word
-  if (p.ctr_parts && blockIdx.x == 0 && tid < kClaimParts) p.ctr_parts[64u * tid] = 0u;
   const uint64_t base = (uint64_t)blockIdx.x * (1024u * kPer) + 64u * kPer * wv + lane;
   // this thread's lengths first (coalesced); pointers and seeds are loaded
   // for the stores at the end (holding them from here spilled 61 VGPRs)
