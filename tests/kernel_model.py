@@ -219,13 +219,12 @@ def device_snap(batch: "Batch", t: int):
     return b0 + q, i, (i - 1 if q < m else i)
 
 
-def wave_ranges(batch: Batch, num_cus: int, dyn_shift: int = K_DYN_SHIFT, unit: int = K_DYN_UNIT, tail: int = 0):
+def wave_ranges(batch: Batch, num_cus: int, dyn_shift: int = K_DYN_SHIFT, unit: int = K_DYN_UNIT):
     """Every (s0, s1, last) range the kernel processes: W static wave ranges
     over the first Ts bytes, then the dynamic units of `unit` nominal bytes
     over the last Td = total >> dyn_shift bytes (zcrc_batch_kernel.h,
-    crc32_batch_kernel) -- with `tail` (BatchArgs::dyn_tail), the last
-    min(Td / 2, tail x W half units) bytes in half units.  Which wave claims
-    a unit does not matter for the result, so the model lists them in order."""
+    crc32_batch_kernel).  Which wave claims a unit does not matter for the
+    result, so the model lists them in order."""
     total = batch.total
     want = max(1, (total + K_MIN_RANGE - 1) // K_MIN_RANGE, batch.n)
     W = min(want, num_cus * K_WAVES)
@@ -244,21 +243,12 @@ def wave_ranges(batch: Batch, num_cus: int, dyn_shift: int = K_DYN_SHIFT, unit: 
         else:
             s1 = batch.snap(q * (w + 1) + (r * (w + 1)) // W)
         out.append((s0, s1, w + 1 == W and not Td))
-    half = unit // 2
-    Ut = min(tail * W * half, Td // 2) // half if Td and tail else 0
-    Tm = total - Ut * half
-    Um = (Tm - Ts + unit - 1) // unit if Td else 0
-    units = Um + Ut
+    units = (Td + unit - 1) // unit if Td else 0
     for u in range(units):
-        if u < Um:
-            t0 = Ts + u * unit
-            t1 = Tm if Ut and u + 1 == Um else t0 + unit
-        else:
-            t0 = Tm + (u - Um) * half
-            t1 = t0 + half
+        t0 = Ts + u * unit
         last = u + 1 == units
         s0 = batch.snap(min(t0, total))
-        s1 = total if last else batch.snap(min(t1, total))
+        s1 = total if last else batch.snap(min(t0 + unit, total))
         out.append((s0, s1, last))
     return out
 
@@ -343,12 +333,11 @@ def crc_piece(mem: np.ndarray, pstart: int, pend: int, inj: int, T: Tables) -> i
     return r0
 
 
-def run_batch(batch: Batch, num_cus: int = 256, dyn_shift: int = K_DYN_SHIFT, unit: int = K_DYN_UNIT,
-              tail: int = 0) -> np.ndarray:
+def run_batch(batch: Batch, num_cus: int = 256, dyn_shift: int = K_DYN_SHIFT, unit: int = K_DYN_UNIT) -> np.ndarray:
     """CRCs of every buffer, computed the way the kernel computes them."""
     T = tables()
     out = np.zeros(batch.n, dtype=np.uint32)
-    for (s0, s1, last) in wave_ranges(batch, num_cus, dyn_shift, unit, tail):
+    for (s0, s1, last) in wave_ranges(batch, num_cus, dyn_shift, unit):
         for (i, rel_lo, rel_hi) in wave_pieces(batch, s0, s1, last):
             n = batch.lens[i]
             seed = batch.seeds[i]

@@ -196,18 +196,14 @@ def test_random_mixed_batches_vs_oracle():
         np.testing.assert_array_equal(got, exp, err_msg=f"trial {trial}")
 
 
-@pytest.mark.parametrize("dyn_tail", [None, "2"])
 @pytest.mark.parametrize("shape", ["large_mean", "small_mean"])
-def test_dynamic_part_mixed_batches(shape, dyn_tail, monkeypatch):
+def test_dynamic_part_mixed_batches(shape):
     """Batches big enough that the kernel's dynamic part engages: claimed
     128 KiB units cut buffers at arbitrary places, next to empty, tiny and
     unaligned buffers with random seeds, in shuffled address order.  Mean
     buffer >= 512 KiB -> a quarter of the bytes dynamic, below -> half
     (zcrc_internal.h kDynSmallAvg; tests/kernel_model.py mirrors the rule).
-    Every CRC vs the oracle; also with the last units halved (ZCRC_DYN_TAIL,
-    BatchArgs::dyn_tail)."""
-    if dyn_tail:
-        monkeypatch.setenv("ZCRC_DYN_TAIL", dyn_tail)
+    Every CRC vs the oracle."""
     rnd = random.Random(2024 if shape == "large_mean" else 99)
     if shape == "large_mean":
         kinds = [lambda: 0, lambda: rnd.randint(1, 3), lambda: rnd.randint(4, 5000),

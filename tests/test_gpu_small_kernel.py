@@ -178,13 +178,14 @@ def test_device_split_plan_direct_mode(lens_kind, direct, monkeypatch):
                                   _oracle(host, offs, lens, np.zeros(n, np.uint32)))
 
 
-@pytest.mark.parametrize("dyn_tail", [None, "2"])
-def test_config4_golden_replicated_through_split_plan(golden, dyn_tail, monkeypatch):
+@pytest.mark.parametrize("join", [True, False])
+def test_config4_golden_replicated_through_split_plan(golden, join, monkeypatch):
     """The config-4 golden sample repeated 9 times (> kFusedMaxN buffers, so
-    the device split plan runs): every CRC equals the reference's -- also with
-    the dynamic part's last units halved (ZCRC_DYN_TAIL, BatchArgs::dyn_tail)."""
-    if dyn_tail:
-        monkeypatch.setenv("ZCRC_DYN_TAIL", dyn_tail)
+    the device split plan runs): every CRC equals the reference's -- with the
+    small-list workgroups joining the dynamic part when done (the product)
+    and without (ZCRC_AB_FLAGS=4, an A/B knob)."""
+    if not join:
+        monkeypatch.setenv("ZCRC_AB_FLAGS", "4")
     cfg = golden["cfg"]
     idx = cfg["cfg4_idx"].astype(np.int64)
     L = cfg["cfg4_len"].astype(np.int64)

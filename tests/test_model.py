@@ -105,37 +105,6 @@ def test_dynamic_units_chain():
     assert len(km.wave_ranges(b, 256)) == 4096 + -(-(sum(lens) >> 1) // (128 << 10))
 
 
-@pytest.mark.parametrize("tail", [1, 2, 4, 1000])
-def test_dynamic_tail_half_units_chain(tail):
-    """BatchArgs::dyn_tail: the last min(Td / 2, tail x W) half units still
-    tile [0, total) with the static ranges and the full units, for totals that
-    are not multiples of the unit (config 4's and a single buffer's)."""
-    lens4 = [int(x) for x in o.zipf_lens(100000)]
-    for lens in ([2**34 + 12345], lens4):
-        b = km.Batch(np.zeros(1, dtype=np.uint8), [0] * len(lens), lens)
-        rs = km.wave_ranges(b, 256, tail=tail)
-        base = km.wave_ranges(b, 256)
-        assert len(rs) > len(base)  # the half units are there
-        assert sum(1 for *_, last in rs if last) == 1
-        ends = sorted((s0, s1) for s0, s1, _ in rs if s1 > s0)
-        assert ends[0][0] == 0 and ends[-1][1] == b.total
-        for (a0, a1), (c0, c1) in zip(ends, ends[1:]):
-            assert a1 == c0
-
-
-def test_model_dynamic_tail_half_units_match_oracle():
-    rnd = random.Random(11)
-    mem = np.random.default_rng(11).integers(0, 256, size=21_000_000, dtype=np.uint8)
-    lens = [0, 3, 4000, 70000, 200_001, 1 << 20, 3_000_017, 3_000_017, 5_000_011, 65536, 2, 131072,
-            4_000_003] + [rnd.randint(0, 300_000) for _ in range(4)]
-    addrs, seeds = _mk_batch(rnd, mem.size, lens)
-    b = km.Batch(mem, addrs, lens, seeds)
-    assert len(km.wave_ranges(b, 1, 1, 128 << 10, 2)) > len(km.wave_ranges(b, 1, 1, 128 << 10))
-    got = km.run_batch(b, num_cus=1, dyn_shift=1, tail=2)
-    exp = [o.cg_crc32(mem[a:a + L], s) for a, L, s in zip(addrs, lens, seeds)]
-    assert list(got) == exp
-
-
 @pytest.mark.parametrize("dyn_shift,unit", [(1, 128 << 10), (2, 128 << 10), (1, 200_000)])
 def test_model_dynamic_tail_matches_oracle(dyn_shift, unit):
     rnd = random.Random(7 + dyn_shift)

@@ -7,7 +7,7 @@
 // launch, events around `steps` back-to-back steps), the plan alone, and the
 // CRC launch alone (its dispatch packet's timestamps).  Variants move the
 // split's knobs: the small-list workgroups' cost weight (small_cost), the big
-// class edge (big_min), the dynamic unit and the tail half units (dyn_tail).  Then one stamped launch
+// class edge (big_min), the dynamic unit and A/B flags (ab_flags).  Then one stamped launch
 // (kStamp build, s_memrealtime at 100 MHz): batch waves' entry, static
 // range end and end, small-list waves' end, percentiles; the last 24 waves
 // to finish with their pieces, dynamic units and static bytes; end p50 per
@@ -69,7 +69,6 @@ struct Variant {
   uint32_t small_cost;
   uint64_t big_min;
   uint64_t dyn_unit;  // 0: kDynUnit
-  uint32_t dyn_tail;  // BatchArgs::dyn_tail
   uint32_t ab_flags;  // BatchArgs::ab_flags
 };
 
@@ -148,17 +147,16 @@ int main(int argc, char **argv) {
   a.fault = reinterpret_cast<uint32_t *>(scratch + kFaultByte);
 
   const Variant vs[] = {
-      {"default", kSmallCostDefault, kBigMin, 0, 0, 0},
-      {"oldshift", kSmallCostDefault, kBigMin, 0, 0, 1},
-      {"tail1", kSmallCostDefault, kBigMin, 0, 1, 0},
-      {"u192k", kSmallCostDefault, kBigMin, 192ull << 10, 0, 0},
+      {"default", kSmallCostDefault, kBigMin, 0, 0},
+      {"nojoin", kSmallCostDefault, kBigMin, 0, 4},
+      {"cost28", 28, kBigMin, 0, 0},
+      {"cost7", 7, kBigMin, 0, 0},
   };
   const int nv = (int)(sizeof vs / sizeof vs[0]);
   auto set = [&](const Variant &v) {
     p.small_cost = v.small_cost;
     p.big_min = v.big_min;
     a.dyn_unit = v.dyn_unit;
-    a.dyn_tail = v.dyn_tail;
     a.ab_flags = v.ab_flags;
   };
   hipEvent_t e0, e1, k0, k1;
@@ -248,7 +246,7 @@ int main(int argc, char **argv) {
     for (uint64_t w = 0; w < nw; w++)
       if (st[8 * w + 1]) t0 = std::min(t0, st[8 * w + 4]);
     const uint32_t nsm = (uint32_t)counts[4];
-    std::vector<double> entry, search, begin, send, end, s_begin, s_end;
+    std::vector<double> entry, search, begin, send, end, s_begin, s_end, j_start, j_end, j_units;
     std::vector<double> slot_end[kWaves];
     struct Row {
       double end, send, search, claim;
@@ -262,6 +260,13 @@ int main(int argc, char **argv) {
       if (st[8 * w + 2] == ~0ull) {
         s_begin.push_back((st[8 * w + 0] - t0) * 1e-2);
         s_end.push_back(e);
+        continue;
+      }
+      if (st[8 * w + 2] >> 63) {  // a small-list wave that joined the dynamic part
+        s_begin.push_back((st[8 * w + 4] - t0) * 1e-2);
+        j_start.push_back((st[8 * w + 3] - t0) * 1e-2);
+        j_end.push_back(e);
+        j_units.push_back((double)((st[8 * w + 2] >> 32) & 0x7FFFFFFFull));
         continue;
       }
       entry.push_back((st[8 * w + 4] - t0) * 1e-2);
@@ -292,6 +297,9 @@ int main(int argc, char **argv) {
     row("batch end", end);
     row("small begin", s_begin);
     row("small end", s_end);
+    row("joined at", j_start);
+    row("joined: end", j_end);
+    row("joined: units", j_units);
     row("unit searches (sum)", searches);
     row("claim waits (sum)", claims);
     std::sort(rows.begin(), rows.end(), [](const Row &x, const Row &y) { return x.end > y.end; });

@@ -888,6 +888,8 @@ template <bool kStrided, uint32_t kD = kDepth, int kAblate = 0, bool kRotate = t
 __global__ __launch_bounds__(kThreads) void crc32_batch_kernel(BatchArgs args) {
   __shared__ __attribute__((aligned(16))) uint32_t s_lds[kLdsBytes / 4];
   uint32_t grid = gridDim.x;  // the batch's workgroups
+  // a small-list workgroup that, its list done, joins the batch's dynamic part
+  bool join = false;
   if (!kStrided && !kFused && args.n_dev) {
     // split plan: its counts; when it split, the top n_dev[4] workgroups take
     // the small list (zcrc_small_kernel.h, own LDS table) and the rest the
@@ -913,7 +915,14 @@ __global__ __launch_bounds__(kThreads) void crc32_batch_kernel(BatchArgs args) {
           args.stamps[8 * w + 1] = __builtin_amdgcn_s_memrealtime();
           args.stamps[8 * w + 2] = ~0ull;
         }
-        return;  // uniform per workgroup: no barrier is skipped
+        // Round 4: with its list done, the workgroup joins the batch's
+        // dynamic part -- it loads the batch tables like the others and claims
+        // units from the same counter (config 4: the 13 small-list CUs were
+        // done at ~1.1 of ~2.0 ms and idled).  ab_flags bit 2
+        // (A/B) keeps them out.
+        if ((args.ab_flags & 4u) || uni64(args.n_dev[0]) == 0) return;  // uniform per workgroup
+        join = true;
+        __syncthreads();  // every wave is done with the small body's LDS tables
       }
       grid -= nsm;
       args.ptrs = args.ptrs_split;
@@ -1200,7 +1209,7 @@ __global__ __launch_bounds__(kThreads) void crc32_batch_kernel(BatchArgs args) {
   if (want < args.n) want = args.n;
   if (want < 1) want = 1;
   const uint64_t W = want < max_waves ? want : max_waves;
-  if ((uint64_t)blockIdx.x * kWaves >= W) return;  // whole workgroup idle (uniform: no barrier is skipped)
+  if ((uint64_t)blockIdx.x * kWaves >= W && !join) return;  // whole workgroup idle (uniform: no barrier is skipped)
 
   const uint32_t lane = threadIdx.x & 63u;
   const uint64_t w = (uint64_t)blockIdx.x * kWaves + (threadIdx.x >> 6);
@@ -1221,17 +1230,10 @@ __global__ __launch_bounds__(kThreads) void crc32_batch_kernel(BatchArgs args) {
   uint64_t Td = (args.ctr && shift) ? (total >> shift) : 0;
   if (Td / W < unit) Td = 0;  // fewer units than waves: static only
   const uint64_t Ts = total - Td;
-  // dyn_tail (A/B knob): the last min(Td / 2, dyn_tail * W half units) bytes
-  // go out in half units, so that the last claims are shorter
-  const uint64_t half = unit / 2;
-  uint64_t Ut = 0;
-  if (Td && args.dyn_tail) {
-    const uint64_t tb = (uint64_t)args.dyn_tail * W * half;
-    Ut = (tb < Td / 2 ? tb : Td / 2) / half;
-  }
-  const uint64_t Tm = total - Ut * half;  // the main units cover [Ts, Tm)
-  const uint64_t Um = Td ? (Tm - Ts + unit - 1) / unit : 0;
-  const uint64_t units = Um + Ut;
+  // (Round 4: the last units halved -- ZCRC_DYN_TAIL, an A/B knob -- ran
+  // 0.4-1.5% slower on config 4 and was dropped: DESIGN.md 7d.)
+  const uint64_t units = Td ? (Td + unit - 1) / unit : 0;
+  if (join && units <= W) return;  // no claims to join: every unit is pre-assigned (uniform per workgroup)
 
   // nominal boundary of wave k: floor(k * Ts / W), without 128-bit math
   const uint64_t q_tot = Ts / W, r_tot = Ts % W;
@@ -1256,7 +1258,7 @@ __global__ __launch_bounds__(kThreads) void crc32_batch_kernel(BatchArgs args) {
     cdst[tid + 1024u] = comb1;
   }
   __syncthreads();
-  if (w >= W) return;  // no barrier after this point
+  if (w >= W && !join) return;  // no barrier after this point
   bool band = true;
 
 
@@ -1292,7 +1294,7 @@ __global__ __launch_bounds__(kThreads) void crc32_batch_kernel(BatchArgs args) {
     if (kStamp && first_claim) t_static_end = __builtin_amdgcn_s_memrealtime();
     if (!units) break;
     const uint64_t tc0 = kStamp ? __builtin_amdgcn_s_memrealtime() : 0;
-    if (first_claim) {
+    if (first_claim && !join) {
       u = (uint32_t)w;  // units >= W whenever the dynamic part is on
     } else if (units <= W) {
       break;  // every unit was pre-assigned: no claim (and no atomic) at all
@@ -1304,12 +1306,11 @@ __global__ __launch_bounds__(kThreads) void crc32_batch_kernel(BatchArgs args) {
     have_next = false;
     if (kStamp) t_claim += __builtin_amdgcn_s_memrealtime() - tc0;
     if (u >= units) break;
-    const uint64_t t0 = u < Um ? Ts + (uint64_t)u * unit : Tm + (uint64_t)(u - Um) * half;
-    const uint64_t t1 = u < Um ? (Ut && u + 1 == Um ? Tm : t0 + unit) : t0 + half;
+    const uint64_t t0 = Ts + (uint64_t)u * unit;
     last = (u + 1 == units);
     if (kStamp) n_dyn++;
     const uint64_t ts0 = kStamp ? __builtin_amdgcn_s_memrealtime() : 0;
-    bv.range(t0, t1, last, S0, S1, f0, lb1);
+    bv.range(t0, t0 + unit, last, S0, S1, f0, lb1);
     if (kStamp) t_usearch += __builtin_amdgcn_s_memrealtime() - ts0;
     salt = u ^ 0x9E3779B9u;
     if (kPrio && band) __builtin_amdgcn_s_setprio(0);
@@ -1327,7 +1328,7 @@ __global__ __launch_bounds__(kThreads) void crc32_batch_kernel(BatchArgs args) {
   if (kStamp && lane == 0) {  // (tools/c2_probe, tools/c4_probe)
     args.stamps[8 * w + 0] = t_begin;
     args.stamps[8 * w + 1] = __builtin_amdgcn_s_memrealtime();
-    args.stamps[8 * w + 2] = npieces | (n_dyn << 32);
+    args.stamps[8 * w + 2] = npieces | (n_dyn << 32) | ((uint64_t)join << 63);
     args.stamps[8 * w + 3] = t_static_end;
     args.stamps[8 * w + 4] = t_entry;
     args.stamps[8 * w + 5] = t_search;

@@ -64,8 +64,8 @@ struct BatchArgs {
   uint32_t *ctr;
   uint32_t dyn_shift;
   uint64_t dyn_unit;
-  uint32_t dyn_tail;  // the last min(Td / 2, dyn_tail x waves) half units (0: none; an A/B knob)
-  uint32_t ab_flags;  // A/B knobs for tools/ (0 in the product): bit 0 = split shifts bit by bit (rounds 1-3)
+  uint32_t ab_flags;  // A/B knobs (0 in the product; ZCRC_AB_FLAGS): bit 0 = split shifts bit by bit (rounds
+                      // 1-3), bit 2 = the split plan's small-list workgroups do not join the dynamic part
   // fused small batches (kFusedMaxN): lengths to scan in-kernel (the scan is
   // written to `prefix`), split-piece accumulators (n words) and the
   // finished-wave counter; acc, *ctr and *done are zero at launch and left

@@ -321,11 +321,11 @@ uint64_t dyn_unit_override() {
   return v;
 }
 
-// Measurement knob: ZCRC_DYN_TAIL = k hands the dynamic part's last
-// min(Td / 2, k x waves) half units out after the full ones (BatchArgs::dyn_tail;
-// read per call)
-uint32_t dyn_tail_setting() {
-  const char *e = getenv("ZCRC_DYN_TAIL");
+// Measurement knob: ZCRC_AB_FLAGS (read per call) = BatchArgs::ab_flags for
+// device batches: bit 0 split shifts bit by bit, bit 2 the split plan's
+// small-list workgroups stay out of the dynamic part (rounds 1-3 forms)
+uint32_t ab_flags_setting() {
+  const char *e = getenv("ZCRC_AB_FLAGS");
   return e ? (uint32_t)strtoul(e, nullptr, 0) : 0u;
 }
 
@@ -450,7 +450,7 @@ int batch_device_split(const DeviceCtx &dc, const void *const *d_ptrs, const uin
   a.ctr = p.ctr;
   a.dyn_shift = dyn_shift_setting();
   a.dyn_unit = dyn_unit_override();
-  a.dyn_tail = dyn_tail_setting();
+  a.ab_flags = ab_flags_setting();
   a.fault = reinterpret_cast<uint32_t *>(b + kFaultByte);
   ZCRC_HIP_TRY(launch_plan_split(p, stream));
   ZCRC_HIP_TRY(test_corrupt_prefix(p.prefix_c, n, stream));
@@ -483,7 +483,7 @@ int batch_device_ws(const void *const *d_ptrs, const uint64_t *d_lens, const uin
   a.ctr = d_ctr;
   a.dyn_shift = dyn_shift_setting();
   a.dyn_unit = dyn_unit_override();
-  a.dyn_tail = dyn_tail_setting();
+  a.ab_flags = ab_flags_setting();
   a.fault = reinterpret_cast<uint32_t *>(static_cast<uint8_t *>(scratch) + kFaultByte);
   a.lens = d_lens;  // the kernel checks every piece's prefix bounds against it
   ZCRC_HIP_TRY(test_corrupt_prefix(d_prefix, n, stream));
