@@ -82,9 +82,10 @@ int zcrc32_batch(const void *const *ptrs, const size_t *lens, const uint32_t *se
  * d_lens: device array of n byte counts; d_seeds_or_null: device array or
  * NULL; d_out: device array of n results.  Asynchronous on `stream`; its
  * scratch (work counter, length prefix, plan tile sums: 256 + 8*(n+1) +
- * 8*ceil(n/8192) bytes; above 8192 buffers also the split lists, 32*n +
- * 72*ceil(n/8192) + 56 more) is a grow-only buffer cached per stream (stream-
- * ordered allocations under graph capture).  Above 8192 buffers the plan may
+ * 8*ceil(n/8192) bytes; above 8192 buffers the split plan's layout instead,
+ * 16*n + (312 + 24*n + 96*T rounded up to 16) bytes with T = ceil(n/(1024*p))
+ * tiles, p the smallest of 1, 2, 4, 8 for which T <= 256) is a grow-only
+ * buffer cached per stream (stream-ordered allocations under graph capture).  Above 8192 buffers the plan may
  * split the batch on the device: when buffers of at most 8 KiB are worth at
  * least two of the CRC kernel's workgroups, some workgroups of the same
  * launch run the small-buffer body on them (ZCRC_SMALL=0 in the environment:
