@@ -14,7 +14,7 @@
 // wave slot.  Parity: every variant's CRCs equal, and 64 sampled buffers
 // equal a bitwise host CRC.
 //
-//   make -C tools c4_probe && tools/c4_probe [rounds] [steps]
+//   make -C tools c4_probe && tools/c4_probe [rounds] [steps] [all|big|medium|nosmall]
 #include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -75,7 +75,19 @@ struct Variant {
 int main(int argc, char **argv) {
   const int rounds = argc > 1 ? atoi(argv[1]) : 3;
   const int steps = argc > 2 ? atoi(argv[2]) : 20;
-  const uint64_t n = 100000;
+  // argv[3]: which of config 4's buffers (all / big: >= 1 MiB / medium: 8 KiB <
+  // len < 1 MiB / nosmall: > 8 KiB), or uniform1m (config 3's 1 MiB buffers,
+  // ~13 GB), to see which class streams below config 3
+  const std::string cls = argc > 3 ? argv[3] : "all";
+  std::vector<uint64_t> law;
+  for (uint64_t i = 0; i < 100000; i++) {
+    const uint64_t L = zipf_len(i);
+    const bool keep = cls == "all" || (cls == "big" && L >= (1u << 20)) ||
+                      (cls == "medium" && L > 8192 && L < (1u << 20)) || (cls == "nosmall" && L > 8192);
+    if (keep) law.push_back(L);
+  }
+  if (cls == "uniform1m") law.assign(12516, 1ull << 20);  // config 3's buffers, config 4's byte count
+  const uint64_t n = law.size();
   int cus = 0;
   CK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));
   static TableBlob tb;
@@ -87,7 +99,7 @@ int main(int argc, char **argv) {
   std::vector<uint64_t> lens(n), offs(n), ptrs(n);
   uint64_t off = 0, total = 0;
   for (uint64_t i = 0; i < n; i++) {
-    lens[i] = zipf_len(i);
+    lens[i] = law[i];
     offs[i] = off;
     off += (lens[i] + 15) & ~15ull;
     total += lens[i];
@@ -214,8 +226,9 @@ int main(int argc, char **argv) {
   }
   uint64_t counts[5];
   CK(hipMemcpy(counts, scratch + 128, 40, hipMemcpyDeviceToHost));
-  printf("c4_probe: %d CUs, n %llu, %.3f GB, rounds %d x %d steps; variants agree: %s; host CRC 64 sampled: %d/64\n",
-         cus, (unsigned long long)n, total / 1e9, rounds, steps, parity ? "yes" : "NO", host_ok);
+  printf("c4_probe (%s): %d CUs, n %llu, %.3f GB, rounds %d x %d steps; variants agree: %s; host CRC 64 sampled: "
+         "%d/64\n",
+         cls.c_str(), cus, (unsigned long long)n, total / 1e9, rounds, steps, parity ? "yes" : "NO", host_ok);
   for (int vi = 0; vi < nv; vi++) {
     std::string sm, pm, km;
     char b[32];
