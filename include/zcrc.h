@@ -160,7 +160,11 @@ int zcrc_inflate_device(const void *d_src, uint64_t src_len, void *d_dst, uint64
  * deflated entry (raw stream via libzip ZIP_FL_COMPRESSED) inflated and
  * checksummed in one call.  Streams are packed into pinned staging, inflated
  * and checksummed on the GPU and copied back; synchronous.  out_len[i] = 0 and
- * crc_or_null[i] = 0 unless status[i] == ZCRC_INFLATE_OK.  flags: pass 0. */
+ * crc_or_null[i] = 0 unless status[i] == ZCRC_INFLATE_OK.  flags: pass 0.
+ * The calling thread keeps its device buffer (inputs | outputs | descriptors)
+ * for its next call when it is at most 1 GiB, as zcrc_zip_verify_host keeps
+ * its image and arena buffers (at most 1 GiB each); larger ones are freed on
+ * return. */
 int zcrc_inflate_batch(const void *const *src, const size_t *src_len, void *const *dst, const size_t *cap,
                        size_t *out_len, int32_t *status, uint32_t *crc_or_null, size_t n, unsigned flags);
 

@@ -2137,7 +2137,9 @@ int inflate_host_group(const void *const *src, const size_t *src_len, void *cons
     ZCRC_HIP_TRY(hipMemcpyAsync(crcv.data(), d_crc, 4 * m, hipMemcpyDeviceToHost, st));
   }
   ZCRC_HIP_TRY(hipStreamSynchronize(st));
-  tl_device_trim(kTlInflateHost, 4ull << 30);  // keep up to 4 GiB for the thread's next call
+  // keep up to 1 GiB for the thread's next call: ZIPsFS runs up to 32 preload
+  // threads, and 4 GiB each (the round-4 first form) could hold 128 GiB of HBM
+  tl_device_trim(kTlInflateHost, 1ull << 30);
   if (rc) return rc;
   po = 0;
   jobs.clear();
