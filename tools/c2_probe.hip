@@ -12,12 +12,16 @@
 //   probe-pb     pure read in the per-buffer mode's mapping and 2 x 4 KiB
 //                ping-pong, slot priorities as the product; -rot: each wave
 //                starts at a hashed block of its buffer and wraps; -np:
-//                no slot priorities
+//                no slot priorities; -fat: ~600 VALU before the first load
 //   crc          the product kernel (prefix precomputed: the plan's output)
-//   crc-fused    the one-launch kernel (per-buffer mode, round-4 form: tables
-//                built in registers, the batch decided after the work)
-//   crc-fused-r3 the same kernel with the round-3 per-buffer form (tables and
-//                lengths in front of its one barrier), for A/B
+//   crc-fused    the one-launch kernel, per-buffer form 4 (tables built in
+//                registers, the batch decided after the work)
+//   crc-fused-r3 the round-3 per-buffer form (tables and lengths in front of
+//                its one barrier)
+//   crc-fused-N  per-buffer form N (crc32_batch_kernel's kPB): 5 = first
+//                payload loads ahead of the table build; +10 priority by
+//                progress, +20 none (instead of by wave slot); +100 / +200
+//                6- / 8-block register groups.  15 is the product's form.
 // and one stamped launch of each CRC form (s_memrealtime, 100 MHz) printed
 // as a timeline: kernel entry, range search done, LDS fill + barrier done,
 // wave end -- percentiles over all waves, relative to the first entry.  The
