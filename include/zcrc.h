@@ -85,7 +85,11 @@ int zcrc32_batch(const void *const *ptrs, const size_t *lens, const uint32_t *se
  * 8*ceil(n/8192) bytes; above 8192 buffers the split plan's layout instead,
  * 16*n + (312 + 24*n + 96*T rounded up to 16) bytes with T = ceil(n/(1024*p))
  * tiles, p the smallest of 1, 2, 4, 8 for which T <= 256) is a grow-only
- * buffer cached per stream (stream-ordered allocations under graph capture).  Above 8192 buffers the plan may
+ * buffer from a per-device cache, leased per call: an entry another stream
+ * used last is taken only after that stream's launches on it (an event wait),
+ * so streams may be created and destroyed freely; idle entries above
+ * ZCRC_SCRATCH_CACHE_MIB (default 2048) per device are freed (stream-ordered
+ * allocations under graph capture).  Above 8192 buffers the plan may
  * split the batch on the device: when buffers of at most 8 KiB are worth at
  * least two of the CRC kernel's workgroups, some workgroups of the same
  * launch run the small-buffer body on them (ZCRC_SMALL=0 in the environment:
@@ -102,7 +106,8 @@ int zcrc32_batch_device_ws(const void *const *d_ptrs, const uint64_t *d_lens,
                            void *d_scratch, size_t scratch_bytes, void *stream);
 
 /* Integrity check of the last zcrc32_batch_device / _ws launch on a scratch
- * (d_scratch, or NULL for the stream's own cached one): synchronizes `stream`
+ * (d_scratch, or NULL for the cached one the stream's last call used, while
+ * no other stream has taken it since): synchronizes `stream`
  * and sets *faults nonzero when the CRC kernel found inconsistent length-
  * prefix bounds in the scratch (a corrupted scratch -- e.g. written by
  * another stream -- makes the kernel skip those buffers, with result 0,
@@ -280,6 +285,25 @@ uint32_t zcrc32_combine(uint32_t crc_a, uint32_t crc_b, uint64_t len_b);
  *   word j = splitmix64(seed ^ (index << 32 | j)), little-endian. */
 int zcrc_fill_synthetic(const uint64_t *d_ptrs, const uint64_t *d_lens, size_t n, uint64_t index0,
                         uint64_t index_step, uint64_t seed, void *stream);
+
+/* Memory the library keeps between calls: the calling thread's device
+ * buffers of zcrc_inflate_batch and the ZIP entry points (kept up to 1 GiB
+ * each per purpose, at most ZCRC_TL_CACHE_MIB -- default 8192 -- per device
+ * over all threads), and every device's idle cached scratch of the
+ * device-pointer calls.  zcrc_release_cached frees them (the pinned staging
+ * pool stays); *freed_bytes (may be NULL) = device bytes freed.
+ * zcrc_cache_info reports device `dev`'s cached scratch entries and bytes and
+ * the thread-local bytes kept there by all threads. */
+int zcrc_release_cached(uint64_t *freed_bytes);
+int zcrc_cache_info(int dev, uint64_t *scratch_entries, uint64_t *scratch_bytes, uint64_t *thread_local_bytes);
+
+/* Measurement only: the same launches as zcrc32_batch_device (same plan,
+ * same workgroups, same loads, same fold) with every table lookup of the
+ * hot loop replaced by one VALU rotate -- the same-shape read ceiling the
+ * CRC rate is judged against (bench.py roofline.read_ceiling).  d_out does
+ * NOT receive CRCs. */
+int zcrc32_batch_device_read_ceiling(const void *const *d_ptrs, const uint64_t *d_lens, uint32_t *d_out, size_t n,
+                                     void *stream);
 
 /* Diagnostics / measurement. */
 /* Host staging pool: pinned bytes allocated (all devices), slots leased now,

@@ -53,6 +53,23 @@ def test_config5_shard_through_rccl_at_world_size_1():
 
 
 @pytest.mark.timeout(300)
+def test_config5_full_per_gpu_shard_through_rccl():
+    """The exact per-rank workload of the driver's 8-GPU run: 131,072 x 1 MiB
+    = 128 GiB in HBM (bench.py's default at N > 1), RCCL all_gather at world
+    size 1, and every config-5 fixture inside [0, 2^17) in global order
+    (reference: one core per entry,
+    src/ZIPsFS_preloadfileram.c:243)."""
+    d = _bench_line(["--config", "5", "--collective", "--dist-backend", "nccl",
+                     "--steps", "3", "--warmup", "1", "--no-cpu-baseline"], timeout=280)
+    assert d["config"]["buffers_per_gpu"] == 131072
+    assert d["config"]["bytes_per_gpu_per_step"] == 131072 << 20
+    assert d["collective"]["backend"] == "RCCL"
+    assert d["parity"].startswith("768/768"), d["parity"]
+    assert d["value"] > 3000.0, d["value"]
+    print("CONFIG5_FULL_LINE " + json.dumps(d))
+
+
+@pytest.mark.timeout(300)
 def test_two_ranks_spawned_over_gloo_on_one_gpu():
     d = _bench_line(["--gpus", "2", "--dist-backend", "gloo", "--buffers-per-gpu", "32768",
                      "--steps", "3", "--warmup", "1"])

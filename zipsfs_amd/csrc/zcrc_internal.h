@@ -115,8 +115,9 @@ hipError_t launch_small(const SmallArgs &args, bool strided, int lanes, int num_
 const char *small_kernel_name(int lanes);
 
 // t0/t1: optional events stamped with the kernel's own start and end
+// ablate: the read-ceiling variant (table lookups replaced by one VALU op; no CRCs)
 hipError_t launch_batch(const BatchArgs &args, bool strided, int num_cus, hipStream_t stream,
-                        hipEvent_t t0 = nullptr, hipEvent_t t1 = nullptr, bool fused = false);
+                        hipEvent_t t0 = nullptr, hipEvent_t t1 = nullptr, bool fused = false, bool ablate = false);
 inline uint64_t plan_tiles(uint64_t n) { return n == 0 ? 1 : (n + kPlanTile - 1) / kPlanTile; }
 const char *product_kernel_name();
 const char *fused_kernel_name();

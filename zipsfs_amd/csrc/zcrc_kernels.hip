@@ -425,10 +425,19 @@ hipError_t launch_plan_split(const SplitPlan &p, hipStream_t stream) {
 // ------------------------------------------------------------ launchers
 
 hipError_t launch_batch(const BatchArgs &args, bool strided, int num_cus, hipStream_t stream, hipEvent_t t0,
-                        hipEvent_t t1, bool fused) {
+                        hipEvent_t t1, bool fused, bool ablate) {
   const dim3 grid((unsigned)num_cus), block(kThreads);
   // t0/t1 (profiling): timestamps carried by the dispatch packet itself --
   // event records around the launch add ~11 us of queue bubbles per launch
+  if (ablate) {  // the read ceiling (zcrc32_batch_device_read_ceiling): lookups replaced by one VALU op
+    if (strided) return hipErrorInvalidValue;
+    if (fused)
+      hipExtLaunchKernelGGL((crc32_batch_kernel<false, kDepth, 1, true, false, 1, kLoadNt, true, kWindowed, kPerBufForm>),
+                            grid, block, 0, stream, t0, t1, 0, args);
+    else
+      hipExtLaunchKernelGGL((crc32_batch_kernel<false, kDepth, 1>), grid, block, 0, stream, t0, t1, 0, args);
+    return hipGetLastError();
+  }
   if (fused)
     hipExtLaunchKernelGGL((crc32_batch_kernel<false, kDepth, 0, true, false, 1, kLoadNt, true, kWindowed, kPerBufForm>),
                           grid, block, 0, stream, t0, t1, 0, args);

@@ -23,16 +23,40 @@ size_t host_shards(uint64_t bytes);
 int run_sharded(size_t shards, const std::function<int(size_t)> &job);
 
 // Per-thread, per-device, grow-only device buffers for the synchronous
-// host-memory calls (zcrc_inflate_batch, the ZIP verifier): hipMalloc'd
-// once and reused by the thread's later calls, each of which synchronizes
-// before it returns.  (Round 4: a stream-ordered hipMallocAsync/hipFreeAsync
-// pair per call gave the split inflate's finder stale input on the second
-// call of a C process -- ROCm 7.2's runtime; torch's bundled 7.0 did not
-// show it -- and one illegal-address fault: DESIGN.md section 7d.)
+// calls (zcrc_inflate_batch, the ZIP verifier and extractor): hipMalloc'd once
+// and reused by the thread's later calls, each of which synchronizes its
+// stream before it returns -- on every exit once work is queued (SyncOnExit
+// below).  Kept bytes per device are bounded (ZCRC_TL_CACHE_MIB, default
+// 8 GiB); zcrc_release_cached() frees the calling thread's.  Round 4 replaced
+// a per-call hipMallocAsync/hipFreeAsync pair with these after the split
+// inflate's finder and probe read other bytes than its decoder on the second
+// call of a C process, and one illegal-address fault followed (DESIGN.md 7e
+// states what that trace does and does not show).  ZCRC_TL_EXACT=1 (tests)
+// allocates exactly the size asked behind a canary that the trim checks.
 enum TlBuffer { kTlInflateHost = 0, kTlZipImage, kTlZipDesc, kTlZipArena, kTlZipCopy, kTlCount };
 int tl_device_buffer(int purpose, size_t bytes, void **out);
-// free the buffer when it holds more than keep_max bytes (large one-off arenas)
-void tl_device_trim(int purpose, size_t keep_max);
+// After the call's synchronize: checks the canary (ZCRC_TL_EXACT: an error
+// when an out-of-bounds write changed it), then frees the buffer when it
+// holds more than keep_max bytes, when the device's kept bytes exceed the
+// budget, or in exact mode.
+int tl_device_trim(int purpose, size_t keep_max);
+// after a failed synchronize: free the buffer (hipFree waits for the device)
+void tl_device_drop(int purpose);
+uint64_t tl_kept_bytes(int dev);
+
+// Synchronizes `st` on scope exit unless disarmed: a call that returns early
+// after queueing work must not leave it running on a buffer its thread's
+// next call reuses.  When that synchronize fails, the thread-local
+// buffer `purpose` (if >= 0) is dropped.
+struct SyncOnExit {
+  hipStream_t st;
+  int purpose;
+  bool armed = true;
+  SyncOnExit(hipStream_t s, int p) : st(s), purpose(p) {}
+  ~SyncOnExit() {
+    if (armed && hipStreamSynchronize(st) != hipSuccess && purpose >= 0) tl_device_drop(purpose);
+  }
+};
 
 // Runs fn(stream) on the HIP stream of a staging slot leased on the current
 // device (waiting while none is free), returned afterwards: a persistent

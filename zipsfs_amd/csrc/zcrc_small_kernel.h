@@ -39,7 +39,9 @@ typedef unsigned int small_v4u __attribute__((ext_vector_type(4)));
 // chunk of the combine area where the x^-8 byte table goes (table 7's)
 constexpr uint32_t kXinv8Chunk = 7u * 256u;
 
-template <bool kStrided, int G, int kD>
+// kAblate == 1 (measurement builds, zcrc32_batch_device_read_ceiling): the
+// braid steps become one VALU rotate each -- the same loads, no lookups.
+template <bool kStrided, int G, int kD, int kAblate>
 __device__ __forceinline__ void small_body(const SmallArgs &a, uint32_t *s_lds, uint64_t n, uint32_t blk,
                                            uint32_t nblk) {
   static_assert(G == 8 || G == 16, "lanes per buffer");
@@ -138,10 +140,17 @@ __device__ __forceinline__ void small_body(const SmallArgs &a, uint32_t *s_lds, 
             uint4 w = make_uint4(d[b][c].x, d[b][c].y, d[b][c].z, d[b][c].w);
             if (rel >= 0 && (rel < rs + 4 || rel + 16 > re))
               w = fix_chunk(w, clamp_rel(rs - rel), clamp_rel(re - rel), clamp_rel(rs - rel), inj);
-            braid_step2(s_lds, s[4 * c + 0], q[4 * c + 0], w.x, o0, o1, o2, o3);
-            braid_step2(s_lds, s[4 * c + 1], q[4 * c + 1], w.y, o0, o1, o2, o3);
-            braid_step2(s_lds, s[4 * c + 2], q[4 * c + 2], w.z, o0, o1, o2, o3);
-            braid_step2(s_lds, s[4 * c + 3], q[4 * c + 3], w.w, o0, o1, o2, o3);
+            if (kAblate == 1) {
+              s[4 * c + 0] = __builtin_amdgcn_alignbit(s[4 * c + 0] ^ w.x, s[4 * c + 0] ^ w.x, 5);
+              s[4 * c + 1] = __builtin_amdgcn_alignbit(s[4 * c + 1] ^ w.y, s[4 * c + 1] ^ w.y, 5);
+              s[4 * c + 2] = __builtin_amdgcn_alignbit(s[4 * c + 2] ^ w.z, s[4 * c + 2] ^ w.z, 5);
+              s[4 * c + 3] = __builtin_amdgcn_alignbit(s[4 * c + 3] ^ w.w, s[4 * c + 3] ^ w.w, 5);
+            } else {
+              braid_step2(s_lds, s[4 * c + 0], q[4 * c + 0], w.x, o0, o1, o2, o3);
+              braid_step2(s_lds, s[4 * c + 1], q[4 * c + 1], w.y, o0, o1, o2, o3);
+              braid_step2(s_lds, s[4 * c + 2], q[4 * c + 2], w.z, o0, o1, o2, o3);
+              braid_step2(s_lds, s[4 * c + 3], q[4 * c + 3], w.w, o0, o1, o2, o3);
+            }
           }
         }
       }
@@ -182,7 +191,7 @@ __device__ __forceinline__ void small_body(const SmallArgs &a, uint32_t *s_lds, 
 template <bool kStrided, int G, int kD>
 __global__ __launch_bounds__(1024) void crc32_small_kernel(SmallArgs a) {
   __shared__ __attribute__((aligned(16))) uint32_t s_lds[kLdsBytes / 4];
-  small_body<kStrided, G, kD>(a, s_lds, a.n, blockIdx.x, gridDim.x);
+  small_body<kStrided, G, kD, 0>(a, s_lds, a.n, blockIdx.x, gridDim.x);
 }
 
 }  // namespace zcrc

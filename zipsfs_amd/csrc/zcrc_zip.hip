@@ -177,6 +177,7 @@ int verify_deflated_chunk(const uint8_t *d_archive, zcrc_zip_entry *entries, con
   void *d_arena = nullptr, *d_desc = nullptr;
   if (zcrc::tl_device_buffer(zcrc::kTlZipArena, arena_bytes + 16, &d_arena)) return zfail("inflate arena allocation failed");
   if (zcrc::tl_device_buffer(zcrc::kTlZipDesc, 8 * 5 * m + 8 * m, &d_desc)) return zfail("inflate descriptor allocation failed");
+  zcrc::SyncOnExit guard(st, zcrc::kTlZipArena);  // (disarmed after the synchronize below)
   for (size_t j = 0; j < m; j++) h[2 * m + j] += reinterpret_cast<uint64_t>(d_arena);
   uint64_t *dd = static_cast<uint64_t *>(d_desc);
   uint64_t *d_src = dd, *d_srclen = dd + m, *d_dst = dd + 2 * m, *d_cap = dd + 3 * m, *d_olen = dd + 4 * m;
@@ -197,9 +198,17 @@ int verify_deflated_chunk(const uint8_t *d_archive, zcrc_zip_entry *entries, con
               hipMemcpyAsync(status.data(), d_status, 4 * m, hipMemcpyDeviceToHost, st) != hipSuccess ||
               hipMemcpyAsync(crc.data(), d_crc, 4 * m, hipMemcpyDeviceToHost, st) != hipSuccess))
     rc = zfail("result download failed");
-  if (hipStreamSynchronize(st) != hipSuccess && !rc) rc = zfail("stream synchronize failed");
-  zcrc::tl_device_trim(zcrc::kTlZipArena, 1ull << 30);  // arenas above 1 GiB are not kept
+  if (hipStreamSynchronize(st) != hipSuccess) {
+    if (!rc) rc = zfail("stream synchronize failed");
+    zcrc::tl_device_drop(zcrc::kTlZipArena);
+    zcrc::tl_device_drop(zcrc::kTlZipDesc);
+  }
+  guard.armed = false;
+  int trc = zcrc::tl_device_trim(zcrc::kTlZipArena, 1ull << 30);  // arenas above 1 GiB are not kept
+  const int trd = zcrc::tl_device_trim(zcrc::kTlZipDesc, 1ull << 30);
+  if (!trc) trc = trd;
   if (rc) return rc;
+  if (trc) return trc;
   for (size_t j = 0; j < m; j++) {
     zcrc_zip_entry &E = entries[idx[a + j]];
     E.inflate_status = status[j];
@@ -323,8 +332,13 @@ extern "C" int zcrc_zip_extract_stored_device(const void *d_archive, size_t arch
   if (!rc) rc = zcrc32_batch_device(reinterpret_cast<const void *const *>(d_dstp), d_len, nullptr, d_crc, m, stream);
   if (!rc && hipMemcpyAsync(crc.data(), d_crc, 4 * m, hipMemcpyDeviceToHost, st) != hipSuccess)
     rc = zfail("result download failed");
-  if (hipStreamSynchronize(st) != hipSuccess && !rc) rc = zfail("stream synchronize failed");
+  if (hipStreamSynchronize(st) != hipSuccess) {
+    if (!rc) rc = zfail("stream synchronize failed");
+    zcrc::tl_device_drop(zcrc::kTlZipCopy);
+  }
+  const int trc = zcrc::tl_device_trim(zcrc::kTlZipCopy, 1ull << 30);
   if (rc) return rc;
+  if (trc) return trc;
   finish(entries, idx, crc);
   return ZCRC_OK;
 }
@@ -388,8 +402,13 @@ extern "C" int zcrc_zip_verify_device(const void *d_archive, size_t archive_len,
     if (!rc) rc = zcrc32_batch_device(reinterpret_cast<const void *const *>(dp), dl, nullptr, dout, m, stream);
     if (!rc && hipMemcpyAsync(crc.data(), dout, 4 * m, hipMemcpyDeviceToHost, st) != hipSuccess)
       rc = zfail("result download failed");
-    if (hipStreamSynchronize(st) != hipSuccess && !rc) rc = zfail("stream synchronize failed");
+    if (hipStreamSynchronize(st) != hipSuccess) {
+      if (!rc) rc = zfail("stream synchronize failed");
+      zcrc::tl_device_drop(zcrc::kTlZipDesc);
+    }
+    const int trc = zcrc::tl_device_trim(zcrc::kTlZipDesc, 1ull << 30);
     if (rc) return rc;
+    if (trc) return trc;
   }
   finish(entries, idx, crc);
   // deflated entries in chunks of <= kArenaBytes of output
@@ -428,12 +447,17 @@ int verify_host_run(const uint8_t *archive, zcrc_zip_entry *entries, const std::
   const int rc = zcrc::with_lease_stream([&](hipStream_t st) {
     void *d = nullptr;
     if (zcrc::tl_device_buffer(zcrc::kTlZipImage, len ? len : 1, &d)) return zfail("archive allocation failed");
+    zcrc::SyncOnExit guard(st, zcrc::kTlZipImage);
     if (len && hipMemcpyAsync(d, archive + lo, len, hipMemcpyHostToDevice, st) != hipSuccess)
       return zfail("archive upload failed");
-    const int r = zcrc_zip_verify_device(d, len, local.data(), local.size(), st);
-    (void)hipStreamSynchronize(st);
-    zcrc::tl_device_trim(zcrc::kTlZipImage, 1ull << 30);
-    return r;
+    int r = zcrc_zip_verify_device(d, len, local.data(), local.size(), st);
+    if (hipStreamSynchronize(st) != hipSuccess) {
+      if (!r) r = zfail("stream synchronize failed");
+      zcrc::tl_device_drop(zcrc::kTlZipImage);
+    }
+    guard.armed = false;
+    const int trc = zcrc::tl_device_trim(zcrc::kTlZipImage, 1ull << 30);
+    return r ? r : trc;
   });
   if (rc) return rc;
   for (size_t k = a; k < b; k++) {
