@@ -389,6 +389,9 @@ def main() -> None:
     ap.add_argument("--cpu-budget-s", type=float, default=12.0)
     ap.add_argument("--cpu-sample-gib", type=float, default=4.0,
                     help="host-resident CPU-baseline sample (>= 2x the host L3)")
+    ap.add_argument("--host-resident-gib", type=float, default=4.0,
+                    help="configs 3/5: host-resident zcrc32_batch over this many GiB of the workload's buffers "
+                         "(0: skip); at N > 1 rank 0 runs it over every visible GPU")
     ap.add_argument("--pmc-traffic-bytes", type=float, default=None,
                     help="HBM bytes per launch from a separate rocprofv3 --pmc pass (corrected)")
     args = ap.parse_args()
@@ -433,9 +436,10 @@ def main() -> None:
             else:
                 dist.barrier()
 
-    def measure(cfg: int, steps: int, warmup: int, n_override=None) -> dict:
+    def measure(cfg: int, steps: int, warmup: int, n_override=None, extra=None) -> dict:
         """Warmup, then exactly `steps` timed steps between barriers and
-        synchronizes (max over ranks), then a parity spot-check."""
+        synchronizes (max over ranks), then a parity spot-check, then (outside
+        the timed region) the same-shape read ceiling and `extra(wl, crcs)`."""
         wl = Workload(cfg, rank, world, dev, n_override)
         out = torch.empty(wl.n_local, dtype=torch.int32, device=dev)
         result = {"global": out}
@@ -496,15 +500,98 @@ def main() -> None:
         gathered_on = str(result["global"].device)
         glob = result["global"].cpu().numpy().view(np.uint32)
         parity = golden_check(cfg, glob) if rank == 0 else None
+        ceiling = read_ceiling(wl, out, steps)
+        extra_res = extra(wl, out.cpu().numpy().view(np.uint32)) if extra else None
         # the device path runs in one batch-kernel launch per step (the split
         # plan's small list, when it splits, runs inside it: zcrc_kernels.hip)
         res = {"wl_desc": wl.desc, "n_local": wl.n_local, "kernel": z.kernel_name_for(wl.n_local),
                "bytes_local": wl.bytes_local, "elapsed": elapsed, "bytes_all": bytes_all,
                "avg_kernel_ms": avg_kernel_ms, "kernel_timing": timing, "launches": launches, "parity": parity,
-               "gathered_on": gathered_on, "bytes_main": wl.bytes_local, "small": None}
+               "gathered_on": gathered_on, "bytes_main": wl.bytes_local, "small": None, "ceiling": ceiling,
+               "extra": extra_res}
         del wl, out, result
         torch.cuda.empty_cache()
         return res
+
+    def read_ceiling(wl, out, steps: int) -> dict:
+        """The same-shape read ceiling: interleaved pairs
+        of `k` CRC launches and `k` launches of the ablated kernel
+        (zcrc32_batch_device_read_ceiling: the same plan, workgroups, loads and
+        fold, one VALU op per dword instead of the table lookups) over the same
+        batches, each block timed by one HIP event pair on the launch stream.
+        Judging the CRC by its ratio to the ceiling measured minutes apart in
+        the same process makes an A/B independent of the box's HBM rate."""
+        k = max(5, steps // 2)
+        sink = torch.empty_like(out)
+
+        def block(fn) -> float:
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for s in range(k):
+                ptrs, lens = wl.batches[s % len(wl.batches)]
+                fn(ptrs, lens)
+            e1.record()
+            torch.cuda.synchronize()
+            return e0.elapsed_time(e1) / k
+
+        crc = lambda p, l: z.crc32_batch_device(p, l, out=sink)
+        ceil = lambda p, l: z.batch_device_read_ceiling(p, l, out=sink)
+        block(ceil)  # warm the ablated kernel's code object
+        pairs = [(block(crc), block(ceil)) for _ in range(3)]
+        crc_ms = float(np.median([a for a, _ in pairs]))
+        ceil_ms = float(np.median([b for _, b in pairs]))
+        gbs = wl.bytes_local / (ceil_ms * 1e-3) / 1e9
+        return {"read_ceiling_gbs": round(gbs, 1), "ceiling_ms": round(ceil_ms, 4),
+                "crc_ms_interleaved": round(crc_ms, 4), "frac_of_ceiling_interleaved": round(ceil_ms / crc_ms, 4),
+                "pairs_ms": [[round(a, 4), round(b, 4)] for a, b in pairs], "launches_per_block": k,
+                "method": "3 interleaved pairs of k CRC launches and k read-ceiling launches "
+                          "(zcrc32_batch_device_read_ceiling: same plan, loads and fold, table lookups "
+                          "replaced by one VALU op), HIP events per block, medians"}
+
+    def host_resident(wl, crcs, n_host: int, reps: int) -> dict:
+        """SURVEY 8(d)/north_star: the path starts and ends in host memory.
+        zcrc32_batch over n_host x 1 MiB config-3 buffers in pageable host
+        memory (copied out of the workload), i.e. the library's pinned staging
+        and PCIe transfer included, over the device set (ZCRC_DEVICES, default
+        every visible GPU); results checked against the device path's CRCs of
+        the same buffers (themselves checked against the golden vectors)."""
+        import ctypes
+        try:
+            L = 1 << 20
+            n_host = min(n_host, wl.n_local)
+            host = wl.mem[0][: n_host * L].cpu()  # pageable, like ZIPsFS's preload buffers
+            ptrs = np.arange(n_host, dtype=np.uint64) * np.uint64(L) + np.uint64(host.data_ptr())
+            lens = np.full(n_host, L, dtype=np.uint64)
+            res = np.zeros(n_host, dtype=np.uint32)
+            lib = z.lib()
+
+            def run() -> None:
+                rc = lib.zcrc32_batch(ptrs.ctypes.data, lens.ctypes.data, None, res.ctypes.data, n_host, 0)
+                if rc:
+                    raise RuntimeError(f"zcrc32_batch failed ({rc}): {lib.zcrc_last_error().decode()}")
+
+            run()  # warm: staging slots, device set
+            t = []
+            for _ in range(reps):
+                res[:] = 0
+                t0 = time.perf_counter()
+                run()
+                t.append(time.perf_counter() - t0)
+            bad = int((res != crcs[:n_host]).sum())
+            devs = z.device_set()
+            st = z.staging_info()
+            out = {"value": round(n_host * L / float(np.median(t)) / GiB, 2), "unit": "GiB/s",
+                   "bytes_per_call": n_host * L, "reps": reps, "seconds": [round(x, 4) for x in t],
+                   "devices": devs, "bytes_per_device": n_host * L // max(1, len(devs)),
+                   "parity": (f"{n_host - bad}/{n_host} equal the device path's CRCs of the same buffers"),
+                   "staging": st,
+                   "api": "zcrc32_batch (host pointers; pinned staging + PCIe inside, zero-copy kernel reads)"}
+            if bad:
+                out["error"] = f"{bad} CRCs differ from the device path"
+            del host
+            return out
+        except Exception as e:  # reported in the line, never failing the run
+            return {"error": f"{type(e).__name__}: {e}"}
 
     def pmc_traffic(cfg: int, bytes_local: int):
         """PMC traffic per launch recorded for this workload AND these kernel
@@ -518,7 +605,20 @@ def main() -> None:
             return pm["traffic_bytes_per_launch"], pm["source"]
         return None, None
 
-    m = measure(args.config, args.steps, args.warmup, args.buffers_per_gpu)
+    host_extra = None
+    if args.config in (3, 5) and args.host_resident_gib > 0:
+        n_host = int(args.host_resident_gib * 1024)
+        if world == 1:
+            host_extra = lambda wl, crcs: host_resident(wl, crcs, n_host, 3)
+        else:
+            # N > 1: after the timed steps, rank 0 alone runs a host batch over
+            # every visible GPU (the in-process device set, ZIPsFS's one
+            # process) while the other ranks wait
+            def host_extra(wl, crcs):
+                r = host_resident(wl, crcs, n_host, 3) if rank == 0 else None
+                barrier()
+                return r
+    m = measure(args.config, args.steps, args.warmup, args.buffers_per_gpu, extra=host_extra)
     elapsed, bytes_all = m["elapsed"], m["bytes_all"]
 
     class _WL:  # the headline workload's figures, for the line below
@@ -538,13 +638,20 @@ def main() -> None:
             r = measure(c, ks, max(args.warmup, 3))
             ach = r["bytes_main"] / (r["avg_kernel_ms"] * 1e-3) / 1e9
             tr, _ = pmc_traffic(c, r["bytes_local"])
+            ce = r["ceiling"]
             secondary[f"config{c}"] = {
                 "workload": r["wl_desc"], "value": round(r["bytes_all"] * ks / r["elapsed"] / GiB, 2),
+                "read_ceiling_gbs": ce["read_ceiling_gbs"],
+                "frac_of_ceiling": round(ach / ce["read_ceiling_gbs"], 4), "read_ceiling": ce,
                 "unit": "GiB/s", "steps": ks, "ms_per_step": round(r["elapsed"] / ks * 1e3, 4),
                 "avg_kernel_ms": round(r["avg_kernel_ms"], 4), "achieved": round(ach, 1),
                 "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None if tr is None else int(tr),
                 "algorithmic_bytes_per_launch": r["bytes_main"], "kernel": r["kernel"], "small_kernel": r["small"],
                 "parity": r["parity"]}
+
+    if m["extra"] is not None:  # host-resident rate (N = 1) / host batch over the device set (N > 1)
+        secondary = secondary or {}
+        secondary["host_resident" if world == 1 else "host_multi_device"] = m["extra"]
 
     ms_per_step = elapsed / args.steps * 1e3
     value = bytes_all * args.steps / elapsed / GiB
@@ -600,6 +707,9 @@ def main() -> None:
                 "launches_timed": m["launches"],
                 "kernel_timing": m["kernel_timing"],
                 "small_kernel": m["small"],
+                "read_ceiling_gbs": m["ceiling"]["read_ceiling_gbs"],
+                "frac_of_ceiling": round(achieved / m["ceiling"]["read_ceiling_gbs"], 4),
+                "read_ceiling": m["ceiling"],
             },
             "cpu_baseline": cpu,
             "parity": parity,

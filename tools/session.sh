@@ -16,6 +16,8 @@
 #   small                  uniform small device batches (tools/small_batches.py)
 #   probe:<tool>:<args>    a built tools/<tool> binary (commas for spaces)
 #   py:<script>:<args>     python3 <script> <args> (commas for spaces)
+#   export:<VAR>=<value>   set an environment variable for the steps after it
+#   unset:<VAR>            remove it again
 set -o pipefail
 export TMPDIR=/tmp
 NAME=${1:?usage: session.sh <name> <step>...}
@@ -56,6 +58,10 @@ for step in "$@"; do
       script=${arg%%:*}; pargs=${arg#*:}; [ "$pargs" = "$arg" ] && pargs=""
       # shellcheck disable=SC2086
       timeout -k 10 600 python3 -u "$script" ${pargs//,/ } > "$log" 2>&1 ;;
+    export)
+      export "${arg?}"; echo "    $arg" >> "$O/steps.txt"; continue ;;
+    unset)
+      unset "${arg?}"; continue ;;
     *)
       echo "unknown step $step" | tee -a "$O/steps.txt"; exit 90 ;;
   esac

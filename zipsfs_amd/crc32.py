@@ -28,7 +28,7 @@ __all__ = [
     "crc32_batch_strided", "crc32_tensors", "crc32_combine", "fhandle_check_crc32",
     "verify_entries", "fill_synthetic", "profile", "device_info", "version",
     "inflate_batch_device", "inflate_to_device", "inflate_batch", "inflate_device", "INFLATE_STATUS",
-    "device_set", "shard_plan",
+    "device_set", "shard_plan", "batch_device_read_ceiling", "release_cached", "cache_info",
 ]
 
 
@@ -231,6 +231,39 @@ def crc32_batch_device(ptrs, lens, seeds=None, out=None, stream=None):
     check(lib().zcrc32_batch_device(ptrs.data_ptr(), lens.data_ptr(), sp, out.data_ptr(), n, _stream_ptr(stream)),
           "zcrc32_batch_device")
     return out
+
+
+def batch_device_read_ceiling(ptrs, lens, out=None, stream=None):
+    """Measurement only (zcrc32_batch_device_read_ceiling): the launches of
+    ``crc32_batch_device`` on the same batch with the hot loop's table lookups
+    replaced by one VALU op -- the same-shape read ceiling.  ``out`` receives
+    no CRCs."""
+    torch = _torch()
+    _check_dev(ptrs, "ptrs", torch.int64)
+    _check_dev(lens, "lens", torch.int64)
+    n = ptrs.numel()
+    if lens.numel() != n:
+        raise ValueError("ptrs/lens length mismatch")
+    if out is None:
+        out = torch.empty(n, dtype=torch.int32, device=ptrs.device)
+    _check_results(out, n)
+    check(lib().zcrc32_batch_device_read_ceiling(ptrs.data_ptr(), lens.data_ptr(), out.data_ptr(), n,
+                                                 _stream_ptr(stream)), "zcrc32_batch_device_read_ceiling")
+    return out
+
+
+def release_cached() -> int:
+    """zcrc_release_cached: free this thread's device buffers and every idle
+    cached scratch; returns the device bytes freed."""
+    v = ctypes.c_uint64(0)
+    check(lib().zcrc_release_cached(ctypes.byref(v)), "zcrc_release_cached")
+    return int(v.value)
+
+
+def cache_info(dev: int = 0) -> dict:
+    v = [ctypes.c_uint64() for _ in range(3)]
+    check(lib().zcrc_cache_info(dev, *[ctypes.byref(x) for x in v]), "zcrc_cache_info")
+    return dict(zip(["scratch_entries", "scratch_bytes", "thread_local_bytes"], [x.value for x in v]))
 
 
 def crc32_batch_device_ws(ptrs, lens, scratch, seeds=None, out=None, stream=None):
