@@ -72,7 +72,20 @@ def test_text_entry_preload_twice_exact_allocations(tmp_path):
     path.write_bytes(S.deflate(data, 6))
     exp = zlib.crc32(data)
     rc, rows, stats, err = du.run_preload(exe, path, exp, 3, ["gpu_inflate"],
-                                          {"ZCRC_PRELOAD_DEFLATED": str(len(data)), "ZCRC_TL_EXACT": "1"})
+                                          {"ZCRC_PRELOAD_DEFLATED": str(len(data)), "ZCRC_TL_EXACT": "1",
+                                           "ZCRC_SPLIT_TRACE": "1"})
     assert rc == 0, err
     r = rows["gpu_inflate"]
     assert r["ok"] and int(r["crc"], 16) == exp, r
+    # The finder, the probes and the speculative decode are functions of the
+    # input bytes alone: every call on the same entry must lay the stream out
+    # identically.  Round 4's second call did not (its finder and probes saw
+    # other bytes than its decoder: DESIGN.md 7e).
+    blocks = []
+    for line in err.splitlines():
+        if line.startswith("[split] src"):
+            blocks.append([line])
+        elif line.startswith("[split]") and blocks:
+            blocks[-1].append(line)
+    assert len(blocks) == 3, err[-3000:]
+    assert blocks[1] == blocks[0] and blocks[2] == blocks[0], (blocks[0][:3], blocks[1][:3], blocks[2][:3])
