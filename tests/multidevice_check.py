@@ -11,6 +11,7 @@ import json
 import os
 import sys
 import threading
+import time
 import zipfile
 import zlib
 
@@ -85,6 +86,28 @@ def main() -> int:
     for t in th:
         t.join()
     res["streams"] = all(v == want for v in outs)
+
+    # concurrent sharded callers: 8 host threads, each batch cut
+    # across the logical devices; every result checked, every caller finishes
+    bufs = [o.payload(4 << 20, 1000 + i) for i in range(8)]
+    want_c = np.array([o.payload_crc(4 << 20, 1000 + i) for i in range(8)], dtype=np.uint32)
+    conc = [None] * 8
+
+    def caller(k):
+        t0 = time.perf_counter()
+        ok = 0
+        for _ in range(3):
+            ok += int((z.crc32_batch(bufs) == want_c).all())
+        conc[k] = (ok, time.perf_counter() - t0)
+
+    th = [threading.Thread(target=caller, args=(k,)) for k in range(8)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=300)
+    res["concurrent"] = [sum(c[0] for c in conc if c), 24]
+    res["concurrent_s"] = [round(c[1], 4) for c in conc if c]
+    del bufs
 
     # ZIP verification from host memory (runs of entries per device) and host inflate batches
     buf = io.BytesIO()

@@ -39,7 +39,7 @@ def test_host_entry_points_over_logical_devices(env):
     r = _child(env)
     n = len(env["ZCRC_DEVICES"].split(","))
     assert r["device_set"] == [0] * n
-    for k in ("config2", "config4", "chains", "zip", "inflate"):
+    for k in ("config2", "config4", "chains", "zip", "inflate", "concurrent"):
         assert r[k][0] == r[k][1], (k, r[k])
     assert r["checked"] and r["dropin"] and r["streams"], r
     assert r["dropin_stats"]["gpu"] == 3 and r["dropin_stats"]["fallback"] == 0, r["dropin_stats"]

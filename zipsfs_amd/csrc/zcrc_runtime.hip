@@ -1453,13 +1453,22 @@ void plan_shards(const size_t *lens, size_t n, size_t g_count, ShardPlan *p) {
   }
 }
 
-// One persistent worker thread per shard index >= 1 (shard 0 runs on the
-// calling thread).  Jobs of concurrent callers queue per worker; a job never
-// waits on another worker.
+// Shards >= 1 of a call run on a process-wide pool of worker threads (shard
+// 0 runs on the calling thread).  Any idle worker takes any queued shard,
+// and the pool grows (up to kMaxShardWorkers) whenever the queued shards
+// outnumber the idle workers, so concurrent callers -- ZIPsFS's up to 32
+// preload threads (src/ZIPsFS_async.c:468, src/ZIPsFS_configuration.h:110)
+// -- run their shards side by side.  (Round 4 had one worker per shard index,
+// shared by every caller: the shards k of concurrent calls queued behind
+// each other on one thread, each blocking on a staging lease and a
+// synchronize)  Workers are never destroyed: threads outlive
+// static destructors.
+constexpr size_t kMaxShardWorkers = 256;
+
 class ShardWorkers {
  public:
   static ShardWorkers &get() {
-    static ShardWorkers *w = new ShardWorkers();  // never destroyed: threads outlive static destructors
+    static ShardWorkers *w = new ShardWorkers();
     return *w;
   }
   void run(size_t m, const std::function<void(size_t)> &fn) {
@@ -1470,51 +1479,48 @@ class ShardWorkers {
       size_t left = 0;
     } latch;
     latch.left = m - 1;
-    for (size_t k = 1; k < m; k++) {
-      Worker &w = worker(k);
-      {
-        std::lock_guard<std::mutex> lk(w.mu);
-        w.q.push_back([&fn, &latch, k] {
+    if (m > 1) {
+      std::lock_guard<std::mutex> lk(mu_);
+      for (size_t k = 1; k < m; k++)
+        q_.push_back([&fn, &latch, k] {
           fn(k);
           std::lock_guard<std::mutex> l2(latch.mu);
           if (--latch.left == 0) latch.cv.notify_one();
         });
+      while (idle_ < q_.size() && threads_ < kMaxShardWorkers) {
+        threads_++;
+        idle_++;
+        std::thread([this] { loop(); }).detach();
       }
-      w.cv.notify_one();
     }
+    cv_.notify_all();
     fn(0);
     std::unique_lock<std::mutex> lk(latch.mu);
     latch.cv.wait(lk, [&] { return latch.left == 0; });
   }
+  size_t threads() {
+    std::lock_guard<std::mutex> lk(mu_);
+    return threads_;
+  }
 
  private:
-  struct Worker {
-    std::mutex mu;
-    std::condition_variable cv;
-    std::deque<std::function<void()>> q;
-  };
-  Worker &worker(size_t k) {
-    std::lock_guard<std::mutex> lk(mu_);
-    while (workers_.size() <= k) {
-      workers_.emplace_back(new Worker());
-      Worker *w = workers_.back().get();
-      std::thread([w] {
-        for (;;) {
-          std::function<void()> job;
-          {
-            std::unique_lock<std::mutex> l(w->mu);
-            w->cv.wait(l, [&] { return !w->q.empty(); });
-            job = std::move(w->q.front());
-            w->q.pop_front();
-          }
-          job();
-        }
-      }).detach();
+  void loop() {
+    std::unique_lock<std::mutex> lk(mu_);
+    for (;;) {
+      cv_.wait(lk, [&] { return !q_.empty(); });
+      std::function<void()> job = std::move(q_.front());
+      q_.pop_front();
+      idle_--;
+      lk.unlock();
+      job();
+      lk.lock();
+      idle_++;
     }
-    return *workers_[k];
   }
   std::mutex mu_;
-  std::vector<std::unique_ptr<Worker>> workers_;
+  std::condition_variable cv_;
+  std::deque<std::function<void()>> q_;
+  size_t idle_ = 0, threads_ = 0;
 };
 
 int run_sharded_impl(size_t shards, const std::function<int(size_t)> &job) {
