@@ -25,6 +25,8 @@
 //   read-G*-strided  the same with addresses computed (no descriptor loads)
 //   crc              the product's small kernel (the split plan's direct mode
 //                    runs the same body inside the batch kernel)
+//   read-G*-pipe     pure reads with the next step's loads issued before the
+//                    current step's bytes are used (two steps in flight)
 // Every launch is timed by its own dispatch packet (hipExtLaunchKernelGGL
 // events); the figures are averages over the launches, in GB/s of payload.
 //
@@ -147,6 +149,10 @@ __global__ __launch_bounds__(1024) void k_wgc(const uint8_t *base, uint32_t *out
   if (acc == 0x12345678u) out[g * 16 + wv] = acc;
 }
 
+// tails are claimed from 16 counters 256 B apart (counter c owns the tails of
+// buffers c, c + 16, ...; a wave starts at the counter of its slot and moves
+// on when it runs dry), so that 4096 claims do not serialise on one address
+// (~11 ns each there: 4096 of them would take ~47 us)
 __global__ __launch_bounds__(1024) void k_pb_tail(const uint8_t *base, uint32_t *ctr, uint32_t *out) {
   const uint32_t lane = threadIdx.x & 63u, slot = threadIdx.x >> 6;
   const uint64_t w = (uint64_t)slot * gridDim.x + blockIdx.x;
@@ -158,11 +164,15 @@ __global__ __launch_bounds__(1024) void k_pb_tail(const uint8_t *base, uint32_t 
     acc ^= read_blocks(r, 0, 48, lane);
   }
   __builtin_amdgcn_s_setprio(0);
-  for (;;) {
+  for (uint32_t c = 0; c < 16;) {
+    const uint32_t home = (slot + c) & 15u;
     uint32_t t = 0;
-    if (lane == 0) t = atomicAdd(ctr, 1u);
-    t = (uint32_t)__builtin_amdgcn_readfirstlane((int)t);
-    if (t >= kN) break;
+    if (lane == 0) t = atomicAdd(ctr + 64 * home, 1u);
+    t = home + 16u * (uint32_t)__builtin_amdgcn_readfirstlane((int)t);
+    if (t >= kN) {
+      c++;
+      continue;
+    }
     const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc((void *)(base + (uint64_t)t * kLen), (short)0,
                                                                         (int)kLen, 0x00020000);
     acc ^= read_blocks(r, 48, 64, lane);
@@ -221,6 +231,82 @@ __global__ __launch_bounds__(1024) void k_small_read(const uint64_t *ptrs, const
         for (int c = 0; c < C; c++) acc ^= xr(d[b][c]);
       rel0 += 256 * kD;
     }
+  }
+  if (acc == 0x12345678u) out[tid] = acc;
+}
+
+// The same mapping with the payload software-pipelined: the loads of the
+// next step (the next round of this group, or the first round of the wave's
+// next group, whose descriptor is kept one group further ahead) are issued
+// before the current step's bytes are used -- the batch kernel's two groups
+// in flight, which the small body does not have.
+template <int G, int kD>
+__global__ __launch_bounds__(1024) void k_small_read_pipe(const uint64_t *ptrs, const uint64_t *lens, uint64_t n,
+                                                          uint32_t *out) {
+  constexpr int C = 16 / G;
+  constexpr uint32_t BPW = 64 / G;
+  const uint32_t tid = threadIdx.x, lane = tid & 63u, g = lane / G, lg = lane % G;
+  const uint64_t waves = (uint64_t)gridDim.x * 16;
+  const uint64_t nq = (n + BPW - 1) / BPW;
+  struct Grp {
+    uint64_t astart;
+    int32_t rel0;
+    uint32_t kmax;
+  };
+  auto group = [&](uint64_t q) {
+    Grp r{0, -(1 << 30), 0};
+    const uint64_t bi = BPW * q + g;
+    uint32_t kq = 0;
+    if (q < nq && bi < n) {
+      const uint64_t p = ptrs[bi];
+      const uint32_t l = (uint32_t)lens[bi];
+      r.astart = p & ~(uint64_t)15;
+      const int32_t rs = (int32_t)(p & 15u), re = rs + (int32_t)l, span = (re + 15) & ~15;
+      kq = l ? (uint32_t)(span + 255) >> 8 : 0u;
+      r.rel0 = span;  // finished below
+    }
+    r.kmax = q < nq ? (uint32_t)__builtin_amdgcn_readfirstlane(__reduce_max_sync(0xFFFFFFFFFFFFFFFFull, kq)) : 0u;
+    r.rel0 = kq ? r.rel0 - 256 * (int32_t)r.kmax + 16 * C * (int32_t)lg : -(1 << 30);
+    return r;
+  };
+  auto load = [&](const Grp &x, uint32_t k, v4u (*d)[C]) {
+#pragma unroll
+    for (int b = 0; b < kD; b++)
+#pragma unroll
+      for (int c = 0; c < C; c++) {
+        const int32_t rel = x.rel0 + 256 * (int32_t)(k + b) + 16 * c;
+        d[b][c] = (v4u)(0u);
+        if (k + b < x.kmax && rel >= 0) d[b][c] = __builtin_nontemporal_load(reinterpret_cast<const v4u *>(x.astart + (uint32_t)rel));
+      }
+  };
+  uint64_t q = (uint64_t)blockIdx.x * 16 + (tid >> 6);
+  Grp cur = group(q), nxt = group(q + waves);
+  uint32_t k = 0;
+  v4u da[kD][C], db[kD][C];
+  uint32_t acc = 0;
+  load(cur, 0, da);
+  bool flip = false;
+  while (q < nq) {
+    // the step after (q, k)
+    uint64_t q2 = q;
+    uint32_t k2 = k + kD;
+    Grp g2 = cur;
+    if (k2 >= cur.kmax) q2 = q + waves, k2 = 0, g2 = nxt;
+    if (q2 < nq) {
+      if (flip) load(g2, k2, da);
+      else load(g2, k2, db);
+    }
+#pragma unroll
+    for (int b = 0; b < kD; b++)
+#pragma unroll
+      for (int c = 0; c < C; c++) acc ^= xr(flip ? db[b][c] : da[b][c]);
+    flip = !flip;
+    if (q2 != q) {
+      cur = nxt;
+      nxt = group(q2 + waves);
+    }
+    q = q2;
+    k = k2;
   }
   if (acc == 0x12345678u) out[tid] = acc;
 }
@@ -285,7 +371,7 @@ int main(int argc, char **argv) {
               case 2: hipExtLaunchKernelGGL(k_grid16, dim3(cus), dim3(1024), 0, 0, a, z, 0, base, out); break;
               case 3: hipExtLaunchKernelGGL(k_wgc, dim3(cus), dim3(1024), 0, 0, a, z, 0, base, out); break;
               case 4:
-                CHECK(hipMemsetAsync(scratch, 0, 4, 0));
+                CHECK(hipMemsetAsync(scratch, 0, 16 * 256, 0));
                 hipExtLaunchKernelGGL(k_pb_tail, dim3(cus), dim3(1024), 0, 0, a, z, 0, base, scratch, out);
                 break;
               default: {
@@ -296,9 +382,9 @@ int main(int argc, char **argv) {
                 x.out = out;
                 x.n = kN;
                 x.tab = d_tab;
-                x.ctr = scratch + 64;
-                x.done = scratch + 65;
-                x.acc = reinterpret_cast<uint64_t *>(scratch + 128);
+                x.ctr = scratch + 2048;
+                x.done = scratch + 2049;
+                x.acc = reinterpret_cast<uint64_t *>(scratch + 4096);
                 x.dyn_shift = kDynAuto;
                 hipExtLaunchKernelGGL(
                     (crc32_batch_kernel<false, kDepth, 0, true, false, 1, kLoadNt, true, kWindowed, kPerBufForm>),
@@ -332,8 +418,11 @@ int main(int argc, char **argv) {
     uint8_t *data;
     CHECK(hipMalloc(&data, 2 * n * stride + 256));
     uint64_t *dp, *dl;
+    uint32_t *o1, *o2;  // results of "crc" and "crc-pipe" (compared below)
     CHECK(hipMalloc(&dp, 16 * n));
     CHECK(hipMalloc(&dl, 16 * n));
+    CHECK(hipMalloc(&o1, 4 * n));
+    CHECK(hipMalloc(&o2, 4 * n));
     std::vector<uint64_t> hp(2 * n), hl(2 * n, L);
     for (uint64_t i = 0; i < 2 * n; i++) hp[i] = (uint64_t)(data + i * stride);
     CHECK(hipMemcpy(dp, hp.data(), 16 * n, hipMemcpyHostToDevice));
@@ -341,8 +430,8 @@ int main(int argc, char **argv) {
     CHECK(launch_fill_synthetic(dp, dl, 2 * n, 0, 1, 0xC0FFEE, 0));
     CHECK(hipDeviceSynchronize());
     const char *names[] = {"read-G4", "read-G8", "read-G16", "read-G4-strided", "read-G8-strided", "read-G16-strided",
-                           "crc"};
-    constexpr int kV = 7;
+                           "crc", "read-G8-pipe", "read-G16-pipe", "crc-pipe-G8", "crc-pipe-G16", "crc-pipe-G16h"};
+    constexpr int kV = 12;
     std::vector<std::vector<double>> t(kV);
     const int lanes = L <= 2048 ? 8 : 16;  // the product's choice (small_lanes)
     for (int r = 0; r < reps; r++)
@@ -358,11 +447,28 @@ int main(int argc, char **argv) {
               case 3: hipExtLaunchKernelGGL((k_small_read<4, 2, false>), dim3(cus), dim3(1024), 0, 0, a, z, 0, p, l, base, stride, L, n, out); break;
               case 4: hipExtLaunchKernelGGL((k_small_read<8, 4, false>), dim3(cus), dim3(1024), 0, 0, a, z, 0, p, l, base, stride, L, n, out); break;
               case 5: hipExtLaunchKernelGGL((k_small_read<16, 8, false>), dim3(cus), dim3(1024), 0, 0, a, z, 0, p, l, base, stride, L, n, out); break;
+              case 7: hipExtLaunchKernelGGL((k_small_read_pipe<8, 4>), dim3(cus), dim3(1024), 0, 0, a, z, 0, p, l, n, out); break;
+              case 8: hipExtLaunchKernelGGL((k_small_read_pipe<16, 8>), dim3(cus), dim3(1024), 0, 0, a, z, 0, p, l, n, out); break;
+              case 9: case 10: case 11: {
+                SmallArgs s{};
+                s.ptrs = reinterpret_cast<const uint8_t *const *>(p);
+                s.lens = l;
+                s.out = o2;
+                s.n = n;
+                s.tab = d_tab;
+                if (v == 9)
+                  hipExtLaunchKernelGGL((crc32_small_kernel_pipe<false, 8, 2>), dim3(cus), dim3(1024), 0, 0, a, z, 0, s);
+                else if (v == 10)
+                  hipExtLaunchKernelGGL((crc32_small_kernel_pipe<false, 16, 8>), dim3(cus), dim3(1024), 0, 0, a, z, 0, s);
+                else
+                  hipExtLaunchKernelGGL((crc32_small_kernel_pipe<false, 16, 4>), dim3(cus), dim3(1024), 0, 0, a, z, 0, s);
+                break;
+              }
               default: {
                 SmallArgs s{};
                 s.ptrs = reinterpret_cast<const uint8_t *const *>(p);
                 s.lens = l;
-                s.out = out;
+                s.out = o1;
                 s.n = n;
                 s.tab = d_tab;
                 if (lanes == 8)
@@ -381,10 +487,34 @@ int main(int argc, char **argv) {
       printf("    %-17s avg %8.2f us  %7.1f GB/s (avg)  %7.1f GB/s (best)\n", names[v], avg * 1e3,
              n * L / (avg * 1e-3) / 1e9, n * L / (pct(t[v], 0) * 1e-3) / 1e9);
     }
+    {  // every crc-pipe form against "crc" (whose last launch ran batch 1), on batch 1
+      std::vector<uint32_t> h1(n), h2(n);
+      CHECK(hipMemcpy(h1.data(), o1, 4 * n, hipMemcpyDeviceToHost));
+      for (int v = 9; v < 12; v++) {
+        CHECK(hipMemset(o2, 0, 4 * n));
+        SmallArgs s{};
+        s.ptrs = reinterpret_cast<const uint8_t *const *>(dp + n);
+        s.lens = dl + n;
+        s.out = o2;
+        s.n = n;
+        s.tab = d_tab;
+        if (v == 9) hipLaunchKernelGGL((crc32_small_kernel_pipe<false, 8, 2>), dim3(cus), dim3(1024), 0, 0, s);
+        else if (v == 10) hipLaunchKernelGGL((crc32_small_kernel_pipe<false, 16, 8>), dim3(cus), dim3(1024), 0, 0, s);
+        else hipLaunchKernelGGL((crc32_small_kernel_pipe<false, 16, 4>), dim3(cus), dim3(1024), 0, 0, s);
+        CHECK(hipDeviceSynchronize());
+        CHECK(hipMemcpy(h2.data(), o2, 4 * n, hipMemcpyDeviceToHost));
+        uint64_t bad = 0;
+        for (uint64_t i = 0; i < n; i++) bad += h1[i] != h2[i];
+        printf("    %s results: %s (%llu of %llu differ from crc)\n", names[v], bad ? "DIFFER" : "equal",
+               (unsigned long long)bad, (unsigned long long)n);
+      }
+    }
     fflush(stdout);
     CHECK(hipFree(data));
     CHECK(hipFree(dp));
     CHECK(hipFree(dl));
+    CHECK(hipFree(o1));
+    CHECK(hipFree(o2));
   }
   return 0;
 }
