@@ -16,6 +16,9 @@
 //             all buffers claimed from one counter by the waves that finish
 //             first
 //   crc       the product's one-launch per-buffer CRC form (kPerBufForm)
+//   pb-lds4/8 per-CU queue: the workgroup's 16 buffers cut into 4 (8)
+//             pieces; wave s reads piece 0 of its own buffer, then claims
+//             pieces from an LDS counter
 // Part 2, uniform small buffers (1024, 2048, 3000, 4096, 8192 B; >= 1 GiB
 // per batch, two batches rotated), whole buffers in the small body's lane
 // mapping (zcrc_small_kernel.h: G lanes per buffer, 256-B blocks, lane l of
@@ -178,6 +181,37 @@ __global__ __launch_bounds__(1024) void k_pb_tail(const uint8_t *base, uint32_t 
     acc ^= read_blocks(r, 48, 64, lane);
   }
   if (acc == 0x12345678u) out[w] = acc;
+}
+
+// Per-CU queue: workgroup g owns buffers g + grid k (k < 16), cut into
+// quarters of 16 KiB; wave s reads quarter 0 of its own buffer, then claims
+// the other 48 quarters (quarter-major) from an LDS counter -- the waves of a
+// CU that the SIMDs serve first take more pieces (within-CU balance, no
+// global atomics)
+template <uint32_t kParts>
+__global__ __launch_bounds__(1024) void k_pb_lds(const uint8_t *base, uint32_t *out) {
+  __shared__ uint32_t next;
+  const uint32_t lane = threadIdx.x & 63u, slot = threadIdx.x >> 6, g = blockIdx.x, grid = gridDim.x;
+  constexpr uint32_t kPart = 64u / kParts;  // blocks per piece
+  if (threadIdx.x == 0) next = 16u;
+  __syncthreads();
+  slot_prio(slot);
+  uint32_t acc = 0;
+  uint32_t piece = slot;  // piece p: buffer p % 16 of the workgroup, part p / 16
+  for (;;) {
+    const uint64_t buf = g + (uint64_t)grid * (piece & 15u);
+    const uint32_t part = piece >> 4;
+    if (buf < kN) {
+      const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc((void *)(base + buf * kLen), (short)0,
+                                                                          (int)kLen, 0x00020000);
+      acc ^= read_blocks(r, kPart * part, kPart * (part + 1), lane);
+    }
+    uint32_t t = 0;
+    if (lane == 0) t = atomicAdd(&next, 1u);
+    piece = (uint32_t)__builtin_amdgcn_readfirstlane((int)t);
+    if (piece >= 16u * kParts) break;
+  }
+  if (acc == 0x12345678u) out[g * 16 + slot] = acc;
 }
 
 // ---------------------------------------------------------------- part 2
@@ -357,8 +391,8 @@ int main(int argc, char **argv) {
     CHECK(hipMemcpy(dl, hl.data(), 8 * kN * kBatches, hipMemcpyHostToDevice));
     CHECK(launch_fill_synthetic(dp, dl, kN * kBatches, 0, 1, 0xC0FFEE, 0));
     CHECK(hipDeviceSynchronize());
-    const char *names[] = {"pb", "grid8", "grid16", "wgc", "pb-tail", "crc"};
-    constexpr int kV = 6;
+    const char *names[] = {"pb", "grid8", "grid16", "wgc", "pb-tail", "crc", "pb-lds4", "pb-lds8"};
+    constexpr int kV = 8;
     std::vector<std::vector<double>> t(kV);
     for (int r = 0; r < reps; r++)
       for (int v = 0; v < kV; v++)
@@ -374,6 +408,8 @@ int main(int argc, char **argv) {
                 CHECK(hipMemsetAsync(scratch, 0, 16 * 256, 0));
                 hipExtLaunchKernelGGL(k_pb_tail, dim3(cus), dim3(1024), 0, 0, a, z, 0, base, scratch, out);
                 break;
+              case 6: hipExtLaunchKernelGGL(k_pb_lds<4>, dim3(cus), dim3(1024), 0, 0, a, z, 0, base, out); break;
+              case 7: hipExtLaunchKernelGGL(k_pb_lds<8>, dim3(cus), dim3(1024), 0, 0, a, z, 0, base, out); break;
               default: {
                 BatchArgs x{};
                 x.ptrs = reinterpret_cast<const uint8_t *const *>(dp + (uint64_t)b * kN);
