@@ -391,8 +391,11 @@ int main(int argc, char **argv) {
     CHECK(hipMemcpy(dl, hl.data(), 8 * kN * kBatches, hipMemcpyHostToDevice));
     CHECK(launch_fill_synthetic(dp, dl, kN * kBatches, 0, 1, 0xC0FFEE, 0));
     CHECK(hipDeviceSynchronize());
-    const char *names[] = {"pb", "grid8", "grid16", "wgc", "pb-tail", "crc", "pb-lds4", "pb-lds8"};
-    constexpr int kV = 8;
+    const char *names[] = {"pb", "grid8", "grid16", "wgc", "pb-tail", "crc", "pb-lds4", "pb-lds8", "crc-q6",
+                           "crc-q16", "crc-q26"};
+    constexpr int kV = 11;
+    uint32_t *qout;  // results of the queue forms (compared with crc's below)
+    CHECK(hipMalloc(&qout, 4 * kN * 4));
     std::vector<std::vector<double>> t(kV);
     for (int r = 0; r < reps; r++)
       for (int v = 0; v < kV; v++)
@@ -410,12 +413,36 @@ int main(int argc, char **argv) {
                 break;
               case 6: hipExtLaunchKernelGGL(k_pb_lds<4>, dim3(cus), dim3(1024), 0, 0, a, z, 0, base, out); break;
               case 7: hipExtLaunchKernelGGL(k_pb_lds<8>, dim3(cus), dim3(1024), 0, 0, a, z, 0, base, out); break;
+              case 8: case 9: case 10: {
+                BatchArgs x{};
+                x.ptrs = reinterpret_cast<const uint8_t *const *>(dp + (uint64_t)b * kN);
+                x.lens = dl + (uint64_t)b * kN;
+                x.prefix = dpre;
+                x.out = qout + kN * (uint64_t)(v - 7);
+                x.n = kN;
+                x.tab = d_tab;
+                x.ctr = scratch + 2048;
+                x.done = scratch + 2049;
+                x.acc = reinterpret_cast<uint64_t *>(scratch + 4096);
+                x.wg_ctr = scratch + 65536;
+                x.dyn_shift = kDynAuto;
+                if (v == 8)
+                  hipExtLaunchKernelGGL((crc32_batch_kernel<false, kDepth, 0, true, false, 1, kLoadNt, true, kWindowed, 6>),
+                                        dim3(cus), dim3(kThreads), 0, 0, a, z, 0, x);
+                else if (v == 9)
+                  hipExtLaunchKernelGGL((crc32_batch_kernel<false, kDepth, 0, true, false, 1, kLoadNt, true, kWindowed, 16>),
+                                        dim3(cus), dim3(kThreads), 0, 0, a, z, 0, x);
+                else
+                  hipExtLaunchKernelGGL((crc32_batch_kernel<false, kDepth, 0, true, false, 1, kLoadNt, true, kWindowed, 26>),
+                                        dim3(cus), dim3(kThreads), 0, 0, a, z, 0, x);
+                break;
+              }
               default: {
                 BatchArgs x{};
                 x.ptrs = reinterpret_cast<const uint8_t *const *>(dp + (uint64_t)b * kN);
                 x.lens = dl + (uint64_t)b * kN;
                 x.prefix = dpre;
-                x.out = out;
+                x.out = qout;
                 x.n = kN;
                 x.tab = d_tab;
                 x.ctr = scratch + 2048;
@@ -438,7 +465,23 @@ int main(int argc, char **argv) {
       printf("  %-8s avg %7.2f us  p10 %7.2f  p50 %7.2f  %7.1f GB/s (avg)\n", names[v], avg * 1e3, pct(t[v], 0.1) * 1e3,
              pct(t[v], 0.5) * 1e3, kBatchBytes / (avg * 1e-3) / 1e9);
     }
+    {  // the queue forms' CRCs against the product form's (all ran batch 15 last)
+      std::vector<uint32_t> h(4 * kN);
+      CHECK(hipMemcpy(h.data(), qout, 16 * kN, hipMemcpyDeviceToHost));
+      for (int q = 1; q < 4; q++) {
+        uint64_t bad = 0;
+        for (uint64_t i = 0; i < kN; i++) bad += h[q * kN + i] != h[i];
+        printf("  %s results: %s (%llu of %llu differ from crc)\n", names[7 + q], bad ? "DIFFER" : "equal",
+               (unsigned long long)bad, (unsigned long long)kN);
+      }
+      uint32_t z[16];
+      CHECK(hipMemcpy(z, scratch + 65536, sizeof z, hipMemcpyDeviceToHost));
+      uint32_t nz = 0;
+      for (uint32_t x : z) nz |= x;
+      printf("  queue counters after the launches: %s\n", nz ? "NOT ZERO" : "zero");
+    }
     fflush(stdout);
+    CHECK(hipFree(qout));
     CHECK(hipFree(data));
     CHECK(hipFree(dp));
     CHECK(hipFree(dl));

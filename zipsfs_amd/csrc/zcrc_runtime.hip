@@ -691,10 +691,13 @@ bool fused_enabled(size_t n, int num_cus) {
   return n <= (size_t)num_cus * kWaves && n <= kFusedMaxN;
 }
 
-// Fixed layout, whatever n: counters | acc[kFusedMaxN] | prefix[kFusedMaxN+1].
-// The accumulators must never overlap a prefix an earlier, smaller batch left
-// in the same slot (the kernel zeroes only the accumulators it used).
-size_t fused_scratch_bytes() { return kCtrBytes + 8 * kFusedMaxN + 8 * (kFusedMaxN + 1); }
+// Fixed layout, whatever n: counters | acc[kFusedMaxN] | prefix[kFusedMaxN+1]
+// | per-workgroup queue counters (2 x kMaxQueueWgs words, the per-buffer
+// queue form).  The accumulators must never overlap a prefix an earlier,
+// smaller batch left in the same slot (the kernel zeroes only the
+// accumulators it used).
+size_t fused_queue_offset() { return kCtrBytes + 8 * kFusedMaxN + 8 * (kFusedMaxN + 1); }
+size_t fused_scratch_bytes() { return fused_queue_offset() + 8 * kMaxQueueWgs; }
 
 int batch_device_fused(const void *const *d_ptrs, const uint64_t *d_lens, const uint32_t *d_seeds, uint32_t *d_out,
                        size_t n, void *scratch, hipStream_t stream) {
@@ -714,6 +717,8 @@ int batch_device_fused(const void *const *d_ptrs, const uint64_t *d_lens, const 
   a.dyn_shift = dyn_shift_setting();
   a.acc = reinterpret_cast<uint64_t *>(sc + kCtrBytes);
   a.prefix = a.acc + kFusedMaxN;
+  a.wg_ctr = reinterpret_cast<uint32_t *>(sc + fused_queue_offset());
+  if (dc->num_cus > (int)kMaxQueueWgs) return fail(ZCRC_ERR_HIP, "more CUs than the queue counters cover");
   return launch_main(a, false, *dc, stream, true);
 }
 
