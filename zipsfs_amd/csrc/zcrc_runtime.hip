@@ -318,13 +318,15 @@ class ScratchCache {
     ScratchEntry *e = nullptr;
     {
       std::lock_guard<std::mutex> lk(mu_);
+      // this stream's own entry, else the least recently used idle one (the
+      // most likely to have no launch left pending on its last stream)
       for (ScratchEntry *x : entries_) {
         if (x->busy || x->dev != dev || x->use != use) continue;
         if (x->last_st == st) {
           e = x;
           break;
         }
-        if (!e || x->tick > e->tick) e = x;
+        if (!e || x->tick < e->tick) e = x;
       }
       if (!e) {
         e = new (std::nothrow) ScratchEntry();
