@@ -500,7 +500,10 @@ def main() -> None:
         gathered_on = str(result["global"].device)
         glob = result["global"].cpu().numpy().view(np.uint32)
         parity = golden_check(cfg, glob) if rank == 0 else None
-        ceiling = read_ceiling(wl, out, steps)
+        try:  # measurement beside the line's numbers: never fails the run
+            ceiling = read_ceiling(wl, out, steps)
+        except Exception as e:
+            ceiling = {"error": f"{type(e).__name__}: {e}", "read_ceiling_gbs": None}
         extra_res = extra(wl, out.cpu().numpy().view(np.uint32)) if extra else None
         # the device path runs in one batch-kernel launch per step (the split
         # plan's small list, when it splits, runs inside it: zcrc_kernels.hip)
@@ -642,7 +645,8 @@ def main() -> None:
             secondary[f"config{c}"] = {
                 "workload": r["wl_desc"], "value": round(r["bytes_all"] * ks / r["elapsed"] / GiB, 2),
                 "read_ceiling_gbs": ce["read_ceiling_gbs"],
-                "frac_of_ceiling": round(ach / ce["read_ceiling_gbs"], 4), "read_ceiling": ce,
+                "frac_of_ceiling": round(ach / ce["read_ceiling_gbs"], 4) if ce["read_ceiling_gbs"] else None,
+                "read_ceiling": ce,
                 "unit": "GiB/s", "steps": ks, "ms_per_step": round(r["elapsed"] / ks * 1e3, 4),
                 "avg_kernel_ms": round(r["avg_kernel_ms"], 4), "achieved": round(ach, 1),
                 "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None if tr is None else int(tr),
@@ -708,7 +712,8 @@ def main() -> None:
                 "kernel_timing": m["kernel_timing"],
                 "small_kernel": m["small"],
                 "read_ceiling_gbs": m["ceiling"]["read_ceiling_gbs"],
-                "frac_of_ceiling": round(achieved / m["ceiling"]["read_ceiling_gbs"], 4),
+                "frac_of_ceiling": (round(achieved / m["ceiling"]["read_ceiling_gbs"], 4)
+                                    if m["ceiling"]["read_ceiling_gbs"] else None),
                 "read_ceiling": m["ceiling"],
             },
             "cpu_baseline": cpu,
