@@ -167,7 +167,7 @@ __global__ __launch_bounds__(1024) void k_pb_tail(const uint8_t *base, uint32_t 
     acc ^= read_blocks(r, 0, 48, lane);
   }
   __builtin_amdgcn_s_setprio(0);
-  for (uint32_t c = 0; c < 16;) {
+  for (uint32_t c = 0, guard = 0; c < 16 && guard < 4u * kN; guard++) {
     const uint32_t home = (slot + c) & 15u;
     uint32_t t = 0;
     if (lane == 0) t = atomicAdd(ctr + 64 * home, 1u);
@@ -198,7 +198,7 @@ __global__ __launch_bounds__(1024) void k_pb_lds(const uint8_t *base, uint32_t *
   slot_prio(slot);
   uint32_t acc = 0;
   uint32_t piece = slot;  // piece p: buffer p % 16 of the workgroup, part p / 16
-  for (;;) {
+  for (uint32_t guard = 0; guard < 1024; guard++) {
     const uint64_t buf = g + (uint64_t)grid * (piece & 15u);
     const uint32_t part = piece >> 4;
     if (buf < kN) {
@@ -365,16 +365,25 @@ int main(int argc, char **argv) {
   CHECK(hipMalloc(&out, 4u << 20));
   CHECK(hipMalloc(&scratch, 1 << 20));
   CHECK(hipMemset(scratch, 0, 1 << 20));
-  hipEvent_t e0, e1;
-  CHECK(hipEventCreate(&e0));
-  CHECK(hipEventCreate(&e1));
-  auto timed = [&](auto launch) -> double {  // one launch, its own dispatch-packet time (ms)
-    launch(e0, e1);
+  std::vector<hipEvent_t> ev(2 * kBatches);  // one pair per batch: a variant's launches go back to back
+  for (auto &e : ev) CHECK(hipEventCreate(&e));
+  // progress on stderr (unbuffered): the first launch of every variant is
+  // announced before it starts, so that a launch that never ends names itself
+  const char *cur_name = "";
+  int cur_first = 0;
+  // launch(b, e0, e1) for b < nb back to back on the null stream (each timed by
+  // its own dispatch packet, as c2_probe), one synchronize, then the times
+  auto timed = [&](int nb, auto launch, std::vector<double> &into) {
+    if (cur_first) fprintf(stderr, "  %s ...", cur_name);
+    for (int b = 0; b < nb; b++) launch(b, ev[2 * b], ev[2 * b + 1]);
     CHECK(hipGetLastError());
-    CHECK(hipEventSynchronize(e1));
-    float ms = 0;
-    CHECK(hipEventElapsedTime(&ms, e0, e1));
-    return ms;
+    CHECK(hipDeviceSynchronize());
+    for (int b = 0; b < nb; b++) {
+      float ms = 0;
+      CHECK(hipEventElapsedTime(&ms, ev[2 * b], ev[2 * b + 1]));
+      into.push_back(ms);
+      if (cur_first && b == 0) fprintf(stderr, " %.1f us\n", ms * 1e3);
+    }
   };
 
   // ---------------------------------------------------------------- part 1
@@ -398,10 +407,11 @@ int main(int argc, char **argv) {
     CHECK(hipMalloc(&qout, 4 * kN * 4));
     std::vector<std::vector<double>> t(kV);
     for (int r = 0; r < reps; r++)
-      for (int v = 0; v < kV; v++)
-        for (int b = 0; b < kBatches; b++) {
+      for (int v = 0; v < kV; v++) {
+          cur_name = names[v];
+          cur_first = r == 0;
+          timed(kBatches, [&](int b, hipEvent_t a, hipEvent_t z) {
           const uint8_t *base = data + (uint64_t)b * kBatchBytes;
-          t[v].push_back(timed([&](hipEvent_t a, hipEvent_t z) {
             switch (v) {
               case 0: hipExtLaunchKernelGGL(k_pb, dim3(cus), dim3(1024), 0, 0, a, z, 0, base, out); break;
               case 1: hipExtLaunchKernelGGL(k_grid8, dim3(cus * 8), dim3(256), 0, 0, a, z, 0, base, out); break;
@@ -454,8 +464,8 @@ int main(int argc, char **argv) {
                     dim3(cus), dim3(kThreads), 0, 0, a, z, 0, x);
               }
             }
-          }));
-        }
+          }, t[v]);
+      }
     printf("ceiling_probe part 1: config 2 (4096 x 64 KiB), %d CUs, %d batches rotated, %d reps\n", cus, kBatches,
            reps);
     for (int v = 0; v < kV; v++) {
@@ -490,6 +500,7 @@ int main(int argc, char **argv) {
 
   // ---------------------------------------------------------------- part 2
   const uint64_t sizes[] = {1024, 2048, 3000, 4096, 8192};
+  fprintf(stderr, "part 2\n");
   printf("ceiling_probe part 2: uniform small buffers, 2 batches of >= 1 GiB rotated, %d reps\n", reps);
   for (uint64_t L : sizes) {
     const uint64_t stride = (L + 15) & ~15ull;
@@ -514,11 +525,12 @@ int main(int argc, char **argv) {
     std::vector<std::vector<double>> t(kV);
     const int lanes = L <= 2048 ? 8 : 16;  // the product's choice (small_lanes)
     for (int r = 0; r < reps; r++)
-      for (int v = 0; v < kV; v++)
-        for (int b = 0; b < 2; b++) {
+      for (int v = 0; v < kV; v++) {
+          cur_name = names[v];
+          cur_first = r == 0;
+          timed(2, [&](int b, hipEvent_t a, hipEvent_t z) {
           const uint64_t *p = dp + (uint64_t)b * n, *l = dl + (uint64_t)b * n;
           const uint8_t *base = data + (uint64_t)b * n * stride;
-          t[v].push_back(timed([&](hipEvent_t a, hipEvent_t z) {
             switch (v) {
               case 0: hipExtLaunchKernelGGL((k_small_read<4, 2, true>), dim3(cus), dim3(1024), 0, 0, a, z, 0, p, l, base, stride, L, n, out); break;
               case 1: hipExtLaunchKernelGGL((k_small_read<8, 4, true>), dim3(cus), dim3(1024), 0, 0, a, z, 0, p, l, base, stride, L, n, out); break;
@@ -556,8 +568,8 @@ int main(int argc, char **argv) {
                   hipExtLaunchKernelGGL((crc32_small_kernel<false, 16, 8>), dim3(cus), dim3(1024), 0, 0, a, z, 0, s);
               }
             }
-          }));
-        }
+          }, t[v]);
+      }
     printf("  L %5llu  n %8llu per batch\n", (unsigned long long)L, (unsigned long long)n);
     for (int v = 0; v < kV; v++) {
       double s = 0;
