@@ -386,6 +386,118 @@ int main(int argc, char **argv) {
     }
   };
 
+  auto part2 = [&]() {
+  // ---------------------------------------------------------------- part 2
+    const uint64_t sizes[] = {1024, 2048, 3000, 4096, 8192};
+    fprintf(stderr, "part 2\n");
+    printf("ceiling_probe part 2: uniform small buffers, 2 batches of >= 1 GiB rotated, %d reps\n", reps);
+    for (uint64_t L : sizes) {
+      const uint64_t stride = (L + 15) & ~15ull;
+      const uint64_t n = (1ull << 30) / L;
+      uint8_t *data;
+      CHECK(hipMalloc(&data, 2 * n * stride + 256));
+      uint64_t *dp, *dl;
+      uint32_t *o1, *o2;  // results of "crc" and "crc-pipe" (compared below)
+      CHECK(hipMalloc(&dp, 16 * n));
+      CHECK(hipMalloc(&dl, 16 * n));
+      CHECK(hipMalloc(&o1, 4 * n));
+      CHECK(hipMalloc(&o2, 4 * n));
+      std::vector<uint64_t> hp(2 * n), hl(2 * n, L);
+      for (uint64_t i = 0; i < 2 * n; i++) hp[i] = (uint64_t)(data + i * stride);
+      CHECK(hipMemcpy(dp, hp.data(), 16 * n, hipMemcpyHostToDevice));
+      CHECK(hipMemcpy(dl, hl.data(), 16 * n, hipMemcpyHostToDevice));
+      CHECK(launch_fill_synthetic(dp, dl, 2 * n, 0, 1, 0xC0FFEE, 0));
+      CHECK(hipDeviceSynchronize());
+      const char *names[] = {"read-G4", "read-G8", "read-G16", "read-G4-strided", "read-G8-strided", "read-G16-strided",
+                             "crc", "read-G8-pipe", "read-G16-pipe", "crc-pipe-G8", "crc-pipe-G16", "crc-pipe-G16h"};
+      constexpr int kV = 12;
+      std::vector<std::vector<double>> t(kV);
+      const int lanes = L <= 2048 ? 8 : 16;  // the product's choice (small_lanes)
+      for (int r = 0; r < reps; r++)
+        for (int v = 0; v < kV; v++) {
+            cur_name = names[v];
+            cur_first = r == 0;
+            timed(2, [&](int b, hipEvent_t a, hipEvent_t z) {
+            const uint64_t *p = dp + (uint64_t)b * n, *l = dl + (uint64_t)b * n;
+            const uint8_t *base = data + (uint64_t)b * n * stride;
+              switch (v) {
+                case 0: hipExtLaunchKernelGGL((k_small_read<4, 2, true>), dim3(cus), dim3(1024), 0, 0, a, z, 0, p, l, base, stride, L, n, out); break;
+                case 1: hipExtLaunchKernelGGL((k_small_read<8, 4, true>), dim3(cus), dim3(1024), 0, 0, a, z, 0, p, l, base, stride, L, n, out); break;
+                case 2: hipExtLaunchKernelGGL((k_small_read<16, 8, true>), dim3(cus), dim3(1024), 0, 0, a, z, 0, p, l, base, stride, L, n, out); break;
+                case 3: hipExtLaunchKernelGGL((k_small_read<4, 2, false>), dim3(cus), dim3(1024), 0, 0, a, z, 0, p, l, base, stride, L, n, out); break;
+                case 4: hipExtLaunchKernelGGL((k_small_read<8, 4, false>), dim3(cus), dim3(1024), 0, 0, a, z, 0, p, l, base, stride, L, n, out); break;
+                case 5: hipExtLaunchKernelGGL((k_small_read<16, 8, false>), dim3(cus), dim3(1024), 0, 0, a, z, 0, p, l, base, stride, L, n, out); break;
+                case 7: hipExtLaunchKernelGGL((k_small_read_pipe<8, 4>), dim3(cus), dim3(1024), 0, 0, a, z, 0, p, l, n, out); break;
+                case 8: hipExtLaunchKernelGGL((k_small_read_pipe<16, 8>), dim3(cus), dim3(1024), 0, 0, a, z, 0, p, l, n, out); break;
+                case 9: case 10: case 11: {
+                  SmallArgs s{};
+                  s.ptrs = reinterpret_cast<const uint8_t *const *>(p);
+                  s.lens = l;
+                  s.out = o2;
+                  s.n = n;
+                  s.tab = d_tab;
+                  if (v == 9)
+                    hipExtLaunchKernelGGL((crc32_small_kernel_pipe<false, 8, 2>), dim3(cus), dim3(1024), 0, 0, a, z, 0, s);
+                  else if (v == 10)
+                    hipExtLaunchKernelGGL((crc32_small_kernel_pipe<false, 16, 8>), dim3(cus), dim3(1024), 0, 0, a, z, 0, s);
+                  else
+                    hipExtLaunchKernelGGL((crc32_small_kernel_pipe<false, 16, 4>), dim3(cus), dim3(1024), 0, 0, a, z, 0, s);
+                  break;
+                }
+                default: {
+                  SmallArgs s{};
+                  s.ptrs = reinterpret_cast<const uint8_t *const *>(p);
+                  s.lens = l;
+                  s.out = o1;
+                  s.n = n;
+                  s.tab = d_tab;
+                  if (lanes == 8)
+                    hipExtLaunchKernelGGL((crc32_small_kernel<false, 8, 4>), dim3(cus), dim3(1024), 0, 0, a, z, 0, s);
+                  else
+                    hipExtLaunchKernelGGL((crc32_small_kernel<false, 16, 8>), dim3(cus), dim3(1024), 0, 0, a, z, 0, s);
+                }
+              }
+            }, t[v]);
+        }
+      printf("  L %5llu  n %8llu per batch\n", (unsigned long long)L, (unsigned long long)n);
+      for (int v = 0; v < kV; v++) {
+        double s = 0;
+        for (double x : t[v]) s += x;
+        const double avg = s / t[v].size();
+        printf("    %-17s avg %8.2f us  %7.1f GB/s (avg)  %7.1f GB/s (best)\n", names[v], avg * 1e3,
+               n * L / (avg * 1e-3) / 1e9, n * L / (pct(t[v], 0) * 1e-3) / 1e9);
+      }
+      {  // every crc-pipe form against "crc" (whose last launch ran batch 1), on batch 1
+        std::vector<uint32_t> h1(n), h2(n);
+        CHECK(hipMemcpy(h1.data(), o1, 4 * n, hipMemcpyDeviceToHost));
+        for (int v = 9; v < 12; v++) {
+          CHECK(hipMemset(o2, 0, 4 * n));
+          SmallArgs s{};
+          s.ptrs = reinterpret_cast<const uint8_t *const *>(dp + n);
+          s.lens = dl + n;
+          s.out = o2;
+          s.n = n;
+          s.tab = d_tab;
+          if (v == 9) hipLaunchKernelGGL((crc32_small_kernel_pipe<false, 8, 2>), dim3(cus), dim3(1024), 0, 0, s);
+          else if (v == 10) hipLaunchKernelGGL((crc32_small_kernel_pipe<false, 16, 8>), dim3(cus), dim3(1024), 0, 0, s);
+          else hipLaunchKernelGGL((crc32_small_kernel_pipe<false, 16, 4>), dim3(cus), dim3(1024), 0, 0, s);
+          CHECK(hipDeviceSynchronize());
+          CHECK(hipMemcpy(h2.data(), o2, 4 * n, hipMemcpyDeviceToHost));
+          uint64_t bad = 0;
+          for (uint64_t i = 0; i < n; i++) bad += h1[i] != h2[i];
+          printf("    %s results: %s (%llu of %llu differ from crc)\n", names[v], bad ? "DIFFER" : "equal",
+                 (unsigned long long)bad, (unsigned long long)n);
+        }
+      }
+      fflush(stdout);
+      CHECK(hipFree(data));
+      CHECK(hipFree(dp));
+      CHECK(hipFree(dl));
+      CHECK(hipFree(o1));
+      CHECK(hipFree(o2));
+    }
+  };
+
   // ---------------------------------------------------------------- part 1
   {
     uint8_t *data;
@@ -406,8 +518,15 @@ int main(int argc, char **argv) {
     uint32_t *qout;  // results of the queue forms (compared with crc's below)
     CHECK(hipMalloc(&qout, 4 * kN * 4));
     std::vector<std::vector<double>> t(kV);
+    // the queue forms (v >= 8) run last, in their own pass (part 3 below):
+    // a form that never ends must not cost the other figures
+    for (int pass = 0; pass < 2; pass++) {
+    if (pass == 1) {
+      printf("ceiling_probe part 1 (queue forms, run last)\n");
+      fflush(stdout);
+    }
     for (int r = 0; r < reps; r++)
-      for (int v = 0; v < kV; v++) {
+      for (int v = pass ? 8 : 0; v < (pass ? kV : 8); v++) {
           cur_name = names[v];
           cur_first = r == 0;
           timed(kBatches, [&](int b, hipEvent_t a, hipEvent_t z) {
@@ -435,6 +554,7 @@ int main(int argc, char **argv) {
                 x.done = scratch + 2049;
                 x.acc = reinterpret_cast<uint64_t *>(scratch + 4096);
                 x.wg_ctr = scratch + 65536;
+                x.fault = scratch + 70000;
                 x.dyn_shift = kDynAuto;
                 if (v == 8)
                   hipExtLaunchKernelGGL((crc32_batch_kernel<false, kDepth, 0, true, false, 1, kLoadNt, true, kWindowed, 6>),
@@ -466,16 +586,17 @@ int main(int argc, char **argv) {
             }
           }, t[v]);
       }
-    printf("ceiling_probe part 1: config 2 (4096 x 64 KiB), %d CUs, %d batches rotated, %d reps\n", cus, kBatches,
-           reps);
-    for (int v = 0; v < kV; v++) {
+    if (pass == 0)
+      printf("ceiling_probe part 1: config 2 (4096 x 64 KiB), %d CUs, %d batches rotated, %d reps\n", cus, kBatches,
+             reps);
+    for (int v = pass ? 8 : 0; v < (pass ? kV : 8); v++) {
       double s = 0;
       for (double x : t[v]) s += x;
       const double avg = s / t[v].size();
       printf("  %-8s avg %7.2f us  p10 %7.2f  p50 %7.2f  %7.1f GB/s (avg)\n", names[v], avg * 1e3, pct(t[v], 0.1) * 1e3,
              pct(t[v], 0.5) * 1e3, kBatchBytes / (avg * 1e-3) / 1e9);
     }
-    {  // the queue forms' CRCs against the product form's (all ran batch 15 last)
+    if (pass == 1) {  // the queue forms' CRCs against the product form's (all ran batch 15 last)
       std::vector<uint32_t> h(4 * kN);
       CHECK(hipMemcpy(h.data(), qout, 16 * kN, hipMemcpyDeviceToHost));
       for (int q = 1; q < 4; q++) {
@@ -484,13 +605,20 @@ int main(int argc, char **argv) {
         printf("  %s results: %s (%llu of %llu differ from crc)\n", names[7 + q], bad ? "DIFFER" : "equal",
                (unsigned long long)bad, (unsigned long long)kN);
       }
-      uint32_t z[16];
+      uint32_t z[16], fl = 0;
+      CHECK(hipMemcpy(&fl, scratch + 70000, 4, hipMemcpyDeviceToHost));
+      printf("  queue fault word: %u\n", fl);
       CHECK(hipMemcpy(z, scratch + 65536, sizeof z, hipMemcpyDeviceToHost));
       uint32_t nz = 0;
       for (uint32_t x : z) nz |= x;
       printf("  queue counters after the launches: %s\n", nz ? "NOT ZERO" : "zero");
     }
     fflush(stdout);
+    if (pass == 0) {  // part 2 first; then back here for the queue forms
+      part2();
+      fflush(stdout);
+    }
+    }
     CHECK(hipFree(qout));
     CHECK(hipFree(data));
     CHECK(hipFree(dp));
@@ -498,114 +626,5 @@ int main(int argc, char **argv) {
     CHECK(hipFree(dpre));
   }
 
-  // ---------------------------------------------------------------- part 2
-  const uint64_t sizes[] = {1024, 2048, 3000, 4096, 8192};
-  fprintf(stderr, "part 2\n");
-  printf("ceiling_probe part 2: uniform small buffers, 2 batches of >= 1 GiB rotated, %d reps\n", reps);
-  for (uint64_t L : sizes) {
-    const uint64_t stride = (L + 15) & ~15ull;
-    const uint64_t n = (1ull << 30) / L;
-    uint8_t *data;
-    CHECK(hipMalloc(&data, 2 * n * stride + 256));
-    uint64_t *dp, *dl;
-    uint32_t *o1, *o2;  // results of "crc" and "crc-pipe" (compared below)
-    CHECK(hipMalloc(&dp, 16 * n));
-    CHECK(hipMalloc(&dl, 16 * n));
-    CHECK(hipMalloc(&o1, 4 * n));
-    CHECK(hipMalloc(&o2, 4 * n));
-    std::vector<uint64_t> hp(2 * n), hl(2 * n, L);
-    for (uint64_t i = 0; i < 2 * n; i++) hp[i] = (uint64_t)(data + i * stride);
-    CHECK(hipMemcpy(dp, hp.data(), 16 * n, hipMemcpyHostToDevice));
-    CHECK(hipMemcpy(dl, hl.data(), 16 * n, hipMemcpyHostToDevice));
-    CHECK(launch_fill_synthetic(dp, dl, 2 * n, 0, 1, 0xC0FFEE, 0));
-    CHECK(hipDeviceSynchronize());
-    const char *names[] = {"read-G4", "read-G8", "read-G16", "read-G4-strided", "read-G8-strided", "read-G16-strided",
-                           "crc", "read-G8-pipe", "read-G16-pipe", "crc-pipe-G8", "crc-pipe-G16", "crc-pipe-G16h"};
-    constexpr int kV = 12;
-    std::vector<std::vector<double>> t(kV);
-    const int lanes = L <= 2048 ? 8 : 16;  // the product's choice (small_lanes)
-    for (int r = 0; r < reps; r++)
-      for (int v = 0; v < kV; v++) {
-          cur_name = names[v];
-          cur_first = r == 0;
-          timed(2, [&](int b, hipEvent_t a, hipEvent_t z) {
-          const uint64_t *p = dp + (uint64_t)b * n, *l = dl + (uint64_t)b * n;
-          const uint8_t *base = data + (uint64_t)b * n * stride;
-            switch (v) {
-              case 0: hipExtLaunchKernelGGL((k_small_read<4, 2, true>), dim3(cus), dim3(1024), 0, 0, a, z, 0, p, l, base, stride, L, n, out); break;
-              case 1: hipExtLaunchKernelGGL((k_small_read<8, 4, true>), dim3(cus), dim3(1024), 0, 0, a, z, 0, p, l, base, stride, L, n, out); break;
-              case 2: hipExtLaunchKernelGGL((k_small_read<16, 8, true>), dim3(cus), dim3(1024), 0, 0, a, z, 0, p, l, base, stride, L, n, out); break;
-              case 3: hipExtLaunchKernelGGL((k_small_read<4, 2, false>), dim3(cus), dim3(1024), 0, 0, a, z, 0, p, l, base, stride, L, n, out); break;
-              case 4: hipExtLaunchKernelGGL((k_small_read<8, 4, false>), dim3(cus), dim3(1024), 0, 0, a, z, 0, p, l, base, stride, L, n, out); break;
-              case 5: hipExtLaunchKernelGGL((k_small_read<16, 8, false>), dim3(cus), dim3(1024), 0, 0, a, z, 0, p, l, base, stride, L, n, out); break;
-              case 7: hipExtLaunchKernelGGL((k_small_read_pipe<8, 4>), dim3(cus), dim3(1024), 0, 0, a, z, 0, p, l, n, out); break;
-              case 8: hipExtLaunchKernelGGL((k_small_read_pipe<16, 8>), dim3(cus), dim3(1024), 0, 0, a, z, 0, p, l, n, out); break;
-              case 9: case 10: case 11: {
-                SmallArgs s{};
-                s.ptrs = reinterpret_cast<const uint8_t *const *>(p);
-                s.lens = l;
-                s.out = o2;
-                s.n = n;
-                s.tab = d_tab;
-                if (v == 9)
-                  hipExtLaunchKernelGGL((crc32_small_kernel_pipe<false, 8, 2>), dim3(cus), dim3(1024), 0, 0, a, z, 0, s);
-                else if (v == 10)
-                  hipExtLaunchKernelGGL((crc32_small_kernel_pipe<false, 16, 8>), dim3(cus), dim3(1024), 0, 0, a, z, 0, s);
-                else
-                  hipExtLaunchKernelGGL((crc32_small_kernel_pipe<false, 16, 4>), dim3(cus), dim3(1024), 0, 0, a, z, 0, s);
-                break;
-              }
-              default: {
-                SmallArgs s{};
-                s.ptrs = reinterpret_cast<const uint8_t *const *>(p);
-                s.lens = l;
-                s.out = o1;
-                s.n = n;
-                s.tab = d_tab;
-                if (lanes == 8)
-                  hipExtLaunchKernelGGL((crc32_small_kernel<false, 8, 4>), dim3(cus), dim3(1024), 0, 0, a, z, 0, s);
-                else
-                  hipExtLaunchKernelGGL((crc32_small_kernel<false, 16, 8>), dim3(cus), dim3(1024), 0, 0, a, z, 0, s);
-              }
-            }
-          }, t[v]);
-      }
-    printf("  L %5llu  n %8llu per batch\n", (unsigned long long)L, (unsigned long long)n);
-    for (int v = 0; v < kV; v++) {
-      double s = 0;
-      for (double x : t[v]) s += x;
-      const double avg = s / t[v].size();
-      printf("    %-17s avg %8.2f us  %7.1f GB/s (avg)  %7.1f GB/s (best)\n", names[v], avg * 1e3,
-             n * L / (avg * 1e-3) / 1e9, n * L / (pct(t[v], 0) * 1e-3) / 1e9);
-    }
-    {  // every crc-pipe form against "crc" (whose last launch ran batch 1), on batch 1
-      std::vector<uint32_t> h1(n), h2(n);
-      CHECK(hipMemcpy(h1.data(), o1, 4 * n, hipMemcpyDeviceToHost));
-      for (int v = 9; v < 12; v++) {
-        CHECK(hipMemset(o2, 0, 4 * n));
-        SmallArgs s{};
-        s.ptrs = reinterpret_cast<const uint8_t *const *>(dp + n);
-        s.lens = dl + n;
-        s.out = o2;
-        s.n = n;
-        s.tab = d_tab;
-        if (v == 9) hipLaunchKernelGGL((crc32_small_kernel_pipe<false, 8, 2>), dim3(cus), dim3(1024), 0, 0, s);
-        else if (v == 10) hipLaunchKernelGGL((crc32_small_kernel_pipe<false, 16, 8>), dim3(cus), dim3(1024), 0, 0, s);
-        else hipLaunchKernelGGL((crc32_small_kernel_pipe<false, 16, 4>), dim3(cus), dim3(1024), 0, 0, s);
-        CHECK(hipDeviceSynchronize());
-        CHECK(hipMemcpy(h2.data(), o2, 4 * n, hipMemcpyDeviceToHost));
-        uint64_t bad = 0;
-        for (uint64_t i = 0; i < n; i++) bad += h1[i] != h2[i];
-        printf("    %s results: %s (%llu of %llu differ from crc)\n", names[v], bad ? "DIFFER" : "equal",
-               (unsigned long long)bad, (unsigned long long)n);
-      }
-    }
-    fflush(stdout);
-    CHECK(hipFree(data));
-    CHECK(hipFree(dp));
-    CHECK(hipFree(dl));
-    CHECK(hipFree(o1));
-    CHECK(hipFree(o2));
-  }
   return 0;
 }

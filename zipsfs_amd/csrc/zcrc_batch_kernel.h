@@ -554,7 +554,7 @@ __device__ void part_accumulate(const BatchArgs &a, uint64_t i, uint32_t parts, 
                            : gf2_mul_uniform(after == 1 ? kQueueShift1 : after == 2 ? kQueueShift2 : kQueueShift3, r);
   unsigned long long *word = reinterpret_cast<unsigned long long *>(a.acc + i);
   unsigned long long expect = 0;
-  for (;;) {
+  for (uint32_t guard = 0; guard < (1u << 16); guard++) {  // (a retry follows another part's update: bounded)
     const unsigned long long want = (((expect >> 32) + 1) << 32) | (uint32_t)((uint32_t)expect ^ contrib);
     const unsigned long long got = atomicCAS(word, expect, want);
     if (got == expect) {
@@ -566,6 +566,7 @@ __device__ void part_accumulate(const BatchArgs &a, uint64_t i, uint32_t parts, 
     }
     expect = got;
   }
+  if (a.fault) atomicOr(a.fault, 4u);  // never expected: reported, never a hang
 }
 
 // ------------------------------------------------------------ the kernel
@@ -1137,11 +1138,15 @@ __global__ __launch_bounds__(kThreads) void crc32_batch_kernel(BatchArgs args) {
         uint32_t *ctr = args.wg_ctr + 2 * g;
         if (nparts > 1) {
           __builtin_amdgcn_s_setprio(0);
-          for (;;) {
+          for (uint32_t guard = 0; guard <= items; guard++) {  // at most items + 1 claims
             uint32_t t = 0;
             if (lane == 0) t = atomicAdd(ctr, 1u);
             t = uni32(t);
             if (t >= items) break;
+            if (guard == items) {  // never expected: reported, never a hang
+              if (lane == 0 && args.fault) atomicOr(args.fault, 2u);
+              break;
+            }
             const uint64_t bs = (uint64_t)(t % nb) * grid + g;
             const uint32_t j = 1u + t / nb;
             const uint64_t ls = uni64(args.lens[bs]);
