@@ -327,37 +327,3 @@ def test_grain_table_shift_equals_x_power():
         r = rnd.getrandbits(32)
         assert km.grain_shift(r, d, g) == km.gf2_mul(km.xpow8(d), r), d
 
-
-def _queue_parts(n: int) -> int:
-    """zcrc_batch_kernel.h queue_parts (kQueuePiece = 16 KiB)."""
-    q = 16 << 10
-    return min(4, n // q) if n >= 2 * q else 1
-
-
-@pytest.mark.parametrize("seed", [1, 2])
-def test_queue_form_parts_and_shifts_rebuild_the_crc(seed):
-    """The per-buffer queue form (kPB form 6): a buffer of n >= 32 KiB is cut
-    from its end into parts of 16 KiB (part 0 takes the rest at the front);
-    part j's raw register, moved over the parts after it by x^(8 * 16384 *
-    after) (kQueueShift1..3) -- or complemented when it ends the buffer -- and
-    xor-ed with the others' equals zlib's CRC (seed injected into part 0 only)."""
-    rnd = random.Random(seed)
-    T = km.tables()
-    q = 16 << 10
-    lens = [1, 5, 4095, 32767, 32768, 40000, 49152, 65535, 65536] + [rnd.randrange(1, 65537) for _ in range(3)]
-    for n in lens:
-        data = np.frombuffer(rnd.randbytes(n + 32), dtype=np.uint8).copy()
-        off = rnd.randrange(0, 16)
-        s = rnd.getrandbits(32)
-        if n < 4:
-            continue  # bytewise in the kernel
-        P = _queue_parts(n)
-        hi0 = n - (P - 1) * q
-        bounds = [(0, hi0)] + [(hi0 + (j - 1) * q, hi0 + j * q) for j in range(1, P)]
-        assert bounds[-1][1] == n and all(b - a >= (q if j else 4) for j, (a, b) in enumerate(bounds))
-        acc = 0
-        for j, (a, b) in enumerate(bounds):
-            r = km.crc_piece(data, off + a, off + b, (~s & 0xFFFFFFFF) if a == 0 else 0, T)
-            after = P - 1 - j
-            acc ^= (~r & 0xFFFFFFFF) if after == 0 else km.gf2_mul(km.xpow8(q * after), r)
-        assert acc == zlib.crc32(data[off:off + n].tobytes(), s), (n, P)

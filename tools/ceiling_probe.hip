@@ -24,12 +24,15 @@
 // mapping (zcrc_small_kernel.h: G lanes per buffer, 256-B blocks, lane l of
 // a group reads 16 B x 16/G of every block, kD blocks in flight, the next
 // descriptor loaded while the current buffer runs):
-//   read-G{4,8,16}   pure reads with the product's descriptor loads
-//   read-G*-strided  the same with addresses computed (no descriptor loads)
-//   crc              the product's small kernel (the split plan's direct mode
-//                    runs the same body inside the batch kernel)
-//   read-G*-pipe     pure reads with the next step's loads issued before the
-//                    current step's bytes are used (two steps in flight)
+//   read-G8/G16  pure reads with the product's descriptor loads
+//   read-G8c     the same, 8 lanes, with lane l reading the chunks at 16 l and
+//                16 l + 128 (each load covers 128 contiguous bytes per buffer)
+//   crc          the product's small kernel (the split plan's direct mode
+//                runs the same body inside the batch kernel)
+//   crc-G8c/G16/G8  the small kernel in those layouts, results compared with
+//                crc's
+// (Round-5 session 4 also measured G4 layouts, strided addressing and a
+// software-pipelined body: all slower; profiles/r05/s4/ceiling_probe.txt.)
 // Every launch is timed by its own dispatch packet (hipExtLaunchKernelGGL
 // events); the figures are averages over the launches, in GB/s of payload.
 //
@@ -217,7 +220,7 @@ __global__ __launch_bounds__(1024) void k_pb_lds(const uint8_t *base, uint32_t *
 // ---------------------------------------------------------------- part 2
 
 // the small body's mapping (zcrc_small_kernel.h small_body), loads only
-template <int G, int kD, bool kDesc>
+template <int G, int kD, bool kDesc, bool kCoal = false>
 __global__ __launch_bounds__(1024) void k_small_read(const uint64_t *ptrs, const uint64_t *lens, const uint8_t *base,
                                                      uint64_t stride, uint64_t len, uint64_t n, uint32_t *out) {
   constexpr int C = 16 / G;
@@ -248,14 +251,14 @@ __global__ __launch_bounds__(1024) void k_small_read(const uint64_t *ptrs, const
     const int32_t rs = (int32_t)(pstart & 15u), re = rs + (int32_t)l, span = (re + 15) & ~15;
     const uint32_t kq = (active && l) ? (uint32_t)(span + 255) >> 8 : 0u;
     const uint32_t kmax = (uint32_t)__builtin_amdgcn_readfirstlane(__reduce_max_sync(0xFFFFFFFFFFFFFFFFull, kq));
-    int32_t rel0 = kq ? span - 256 * (int32_t)kmax + 16 * C * (int32_t)lg : -(1 << 30);
+    int32_t rel0 = kq ? span - 256 * (int32_t)kmax + (kCoal ? 16 : 16 * C) * (int32_t)lg : -(1 << 30);
     for (uint32_t k = 0; k < kmax; k += kD) {
       v4u d[kD][C];
 #pragma unroll
       for (int b = 0; b < kD; b++)
 #pragma unroll
         for (int c = 0; c < C; c++) {
-          const int32_t rel = rel0 + 256 * b + 16 * c;
+          const int32_t rel = rel0 + 256 * b + (kCoal ? 16 * G : 16) * c;
           d[b][c] = (v4u)(0u);
           if (k + b < kmax && rel >= 0) d[b][c] = __builtin_nontemporal_load(reinterpret_cast<const v4u *>(astart + (uint32_t)rel));
         }
@@ -265,82 +268,6 @@ __global__ __launch_bounds__(1024) void k_small_read(const uint64_t *ptrs, const
         for (int c = 0; c < C; c++) acc ^= xr(d[b][c]);
       rel0 += 256 * kD;
     }
-  }
-  if (acc == 0x12345678u) out[tid] = acc;
-}
-
-// The same mapping with the payload software-pipelined: the loads of the
-// next step (the next round of this group, or the first round of the wave's
-// next group, whose descriptor is kept one group further ahead) are issued
-// before the current step's bytes are used -- the batch kernel's two groups
-// in flight, which the small body does not have.
-template <int G, int kD>
-__global__ __launch_bounds__(1024) void k_small_read_pipe(const uint64_t *ptrs, const uint64_t *lens, uint64_t n,
-                                                          uint32_t *out) {
-  constexpr int C = 16 / G;
-  constexpr uint32_t BPW = 64 / G;
-  const uint32_t tid = threadIdx.x, lane = tid & 63u, g = lane / G, lg = lane % G;
-  const uint64_t waves = (uint64_t)gridDim.x * 16;
-  const uint64_t nq = (n + BPW - 1) / BPW;
-  struct Grp {
-    uint64_t astart;
-    int32_t rel0;
-    uint32_t kmax;
-  };
-  auto group = [&](uint64_t q) {
-    Grp r{0, -(1 << 30), 0};
-    const uint64_t bi = BPW * q + g;
-    uint32_t kq = 0;
-    if (q < nq && bi < n) {
-      const uint64_t p = ptrs[bi];
-      const uint32_t l = (uint32_t)lens[bi];
-      r.astart = p & ~(uint64_t)15;
-      const int32_t rs = (int32_t)(p & 15u), re = rs + (int32_t)l, span = (re + 15) & ~15;
-      kq = l ? (uint32_t)(span + 255) >> 8 : 0u;
-      r.rel0 = span;  // finished below
-    }
-    r.kmax = q < nq ? (uint32_t)__builtin_amdgcn_readfirstlane(__reduce_max_sync(0xFFFFFFFFFFFFFFFFull, kq)) : 0u;
-    r.rel0 = kq ? r.rel0 - 256 * (int32_t)r.kmax + 16 * C * (int32_t)lg : -(1 << 30);
-    return r;
-  };
-  auto load = [&](const Grp &x, uint32_t k, v4u (*d)[C]) {
-#pragma unroll
-    for (int b = 0; b < kD; b++)
-#pragma unroll
-      for (int c = 0; c < C; c++) {
-        const int32_t rel = x.rel0 + 256 * (int32_t)(k + b) + 16 * c;
-        d[b][c] = (v4u)(0u);
-        if (k + b < x.kmax && rel >= 0) d[b][c] = __builtin_nontemporal_load(reinterpret_cast<const v4u *>(x.astart + (uint32_t)rel));
-      }
-  };
-  uint64_t q = (uint64_t)blockIdx.x * 16 + (tid >> 6);
-  Grp cur = group(q), nxt = group(q + waves);
-  uint32_t k = 0;
-  v4u da[kD][C], db[kD][C];
-  uint32_t acc = 0;
-  load(cur, 0, da);
-  bool flip = false;
-  while (q < nq) {
-    // the step after (q, k)
-    uint64_t q2 = q;
-    uint32_t k2 = k + kD;
-    Grp g2 = cur;
-    if (k2 >= cur.kmax) q2 = q + waves, k2 = 0, g2 = nxt;
-    if (q2 < nq) {
-      if (flip) load(g2, k2, da);
-      else load(g2, k2, db);
-    }
-#pragma unroll
-    for (int b = 0; b < kD; b++)
-#pragma unroll
-      for (int c = 0; c < C; c++) acc ^= xr(flip ? db[b][c] : da[b][c]);
-    flip = !flip;
-    if (q2 != q) {
-      cur = nxt;
-      nxt = group(q2 + waves);
-    }
-    q = q2;
-    k = k2;
   }
   if (acc == 0x12345678u) out[tid] = acc;
 }
@@ -367,14 +294,11 @@ int main(int argc, char **argv) {
   CHECK(hipMemset(scratch, 0, 1 << 20));
   std::vector<hipEvent_t> ev(2 * kBatches);  // one pair per batch: a variant's launches go back to back
   for (auto &e : ev) CHECK(hipEventCreate(&e));
-  // progress on stderr (unbuffered): the first launch of every variant is
-  // announced before it starts, so that a launch that never ends names itself
-  const char *cur_name = "";
-  int cur_first = 0;
   // launch(b, e0, e1) for b < nb back to back on the null stream (each timed by
-  // its own dispatch packet, as c2_probe), one synchronize, then the times
-  auto timed = [&](int nb, auto launch, std::vector<double> &into) {
-    if (cur_first) fprintf(stderr, "  %s ...", cur_name);
+  // its own dispatch packet, as c2_probe), one synchronize, then the times;
+  // progress on stderr: a launch that never ends names itself
+  auto timed = [&](const char *name, bool first, int nb, auto launch, std::vector<double> &into) {
+    if (first) fprintf(stderr, "  %s ...", name);
     for (int b = 0; b < nb; b++) launch(b, ev[2 * b], ev[2 * b + 1]);
     CHECK(hipGetLastError());
     CHECK(hipDeviceSynchronize());
@@ -382,119 +306,7 @@ int main(int argc, char **argv) {
       float ms = 0;
       CHECK(hipEventElapsedTime(&ms, ev[2 * b], ev[2 * b + 1]));
       into.push_back(ms);
-      if (cur_first && b == 0) fprintf(stderr, " %.1f us\n", ms * 1e3);
-    }
-  };
-
-  auto part2 = [&]() {
-  // ---------------------------------------------------------------- part 2
-    const uint64_t sizes[] = {1024, 2048, 3000, 4096, 8192};
-    fprintf(stderr, "part 2\n");
-    printf("ceiling_probe part 2: uniform small buffers, 2 batches of >= 1 GiB rotated, %d reps\n", reps);
-    for (uint64_t L : sizes) {
-      const uint64_t stride = (L + 15) & ~15ull;
-      const uint64_t n = (1ull << 30) / L;
-      uint8_t *data;
-      CHECK(hipMalloc(&data, 2 * n * stride + 256));
-      uint64_t *dp, *dl;
-      uint32_t *o1, *o2;  // results of "crc" and "crc-pipe" (compared below)
-      CHECK(hipMalloc(&dp, 16 * n));
-      CHECK(hipMalloc(&dl, 16 * n));
-      CHECK(hipMalloc(&o1, 4 * n));
-      CHECK(hipMalloc(&o2, 4 * n));
-      std::vector<uint64_t> hp(2 * n), hl(2 * n, L);
-      for (uint64_t i = 0; i < 2 * n; i++) hp[i] = (uint64_t)(data + i * stride);
-      CHECK(hipMemcpy(dp, hp.data(), 16 * n, hipMemcpyHostToDevice));
-      CHECK(hipMemcpy(dl, hl.data(), 16 * n, hipMemcpyHostToDevice));
-      CHECK(launch_fill_synthetic(dp, dl, 2 * n, 0, 1, 0xC0FFEE, 0));
-      CHECK(hipDeviceSynchronize());
-      const char *names[] = {"read-G4", "read-G8", "read-G16", "read-G4-strided", "read-G8-strided", "read-G16-strided",
-                             "crc", "read-G8-pipe", "read-G16-pipe", "crc-pipe-G8", "crc-pipe-G16", "crc-pipe-G16h"};
-      constexpr int kV = 12;
-      std::vector<std::vector<double>> t(kV);
-      const int lanes = L <= 2048 ? 8 : 16;  // the product's choice (small_lanes)
-      for (int r = 0; r < reps; r++)
-        for (int v = 0; v < kV; v++) {
-            cur_name = names[v];
-            cur_first = r == 0;
-            timed(2, [&](int b, hipEvent_t a, hipEvent_t z) {
-            const uint64_t *p = dp + (uint64_t)b * n, *l = dl + (uint64_t)b * n;
-            const uint8_t *base = data + (uint64_t)b * n * stride;
-              switch (v) {
-                case 0: hipExtLaunchKernelGGL((k_small_read<4, 2, true>), dim3(cus), dim3(1024), 0, 0, a, z, 0, p, l, base, stride, L, n, out); break;
-                case 1: hipExtLaunchKernelGGL((k_small_read<8, 4, true>), dim3(cus), dim3(1024), 0, 0, a, z, 0, p, l, base, stride, L, n, out); break;
-                case 2: hipExtLaunchKernelGGL((k_small_read<16, 8, true>), dim3(cus), dim3(1024), 0, 0, a, z, 0, p, l, base, stride, L, n, out); break;
-                case 3: hipExtLaunchKernelGGL((k_small_read<4, 2, false>), dim3(cus), dim3(1024), 0, 0, a, z, 0, p, l, base, stride, L, n, out); break;
-                case 4: hipExtLaunchKernelGGL((k_small_read<8, 4, false>), dim3(cus), dim3(1024), 0, 0, a, z, 0, p, l, base, stride, L, n, out); break;
-                case 5: hipExtLaunchKernelGGL((k_small_read<16, 8, false>), dim3(cus), dim3(1024), 0, 0, a, z, 0, p, l, base, stride, L, n, out); break;
-                case 7: hipExtLaunchKernelGGL((k_small_read_pipe<8, 4>), dim3(cus), dim3(1024), 0, 0, a, z, 0, p, l, n, out); break;
-                case 8: hipExtLaunchKernelGGL((k_small_read_pipe<16, 8>), dim3(cus), dim3(1024), 0, 0, a, z, 0, p, l, n, out); break;
-                case 9: case 10: case 11: {
-                  SmallArgs s{};
-                  s.ptrs = reinterpret_cast<const uint8_t *const *>(p);
-                  s.lens = l;
-                  s.out = o2;
-                  s.n = n;
-                  s.tab = d_tab;
-                  if (v == 9)
-                    hipExtLaunchKernelGGL((crc32_small_kernel_pipe<false, 8, 2>), dim3(cus), dim3(1024), 0, 0, a, z, 0, s);
-                  else if (v == 10)
-                    hipExtLaunchKernelGGL((crc32_small_kernel_pipe<false, 16, 8>), dim3(cus), dim3(1024), 0, 0, a, z, 0, s);
-                  else
-                    hipExtLaunchKernelGGL((crc32_small_kernel_pipe<false, 16, 4>), dim3(cus), dim3(1024), 0, 0, a, z, 0, s);
-                  break;
-                }
-                default: {
-                  SmallArgs s{};
-                  s.ptrs = reinterpret_cast<const uint8_t *const *>(p);
-                  s.lens = l;
-                  s.out = o1;
-                  s.n = n;
-                  s.tab = d_tab;
-                  if (lanes == 8)
-                    hipExtLaunchKernelGGL((crc32_small_kernel<false, 8, 4>), dim3(cus), dim3(1024), 0, 0, a, z, 0, s);
-                  else
-                    hipExtLaunchKernelGGL((crc32_small_kernel<false, 16, 8>), dim3(cus), dim3(1024), 0, 0, a, z, 0, s);
-                }
-              }
-            }, t[v]);
-        }
-      printf("  L %5llu  n %8llu per batch\n", (unsigned long long)L, (unsigned long long)n);
-      for (int v = 0; v < kV; v++) {
-        double s = 0;
-        for (double x : t[v]) s += x;
-        const double avg = s / t[v].size();
-        printf("    %-17s avg %8.2f us  %7.1f GB/s (avg)  %7.1f GB/s (best)\n", names[v], avg * 1e3,
-               n * L / (avg * 1e-3) / 1e9, n * L / (pct(t[v], 0) * 1e-3) / 1e9);
-      }
-      {  // every crc-pipe form against "crc" (whose last launch ran batch 1), on batch 1
-        std::vector<uint32_t> h1(n), h2(n);
-        CHECK(hipMemcpy(h1.data(), o1, 4 * n, hipMemcpyDeviceToHost));
-        for (int v = 9; v < 12; v++) {
-          CHECK(hipMemset(o2, 0, 4 * n));
-          SmallArgs s{};
-          s.ptrs = reinterpret_cast<const uint8_t *const *>(dp + n);
-          s.lens = dl + n;
-          s.out = o2;
-          s.n = n;
-          s.tab = d_tab;
-          if (v == 9) hipLaunchKernelGGL((crc32_small_kernel_pipe<false, 8, 2>), dim3(cus), dim3(1024), 0, 0, s);
-          else if (v == 10) hipLaunchKernelGGL((crc32_small_kernel_pipe<false, 16, 8>), dim3(cus), dim3(1024), 0, 0, s);
-          else hipLaunchKernelGGL((crc32_small_kernel_pipe<false, 16, 4>), dim3(cus), dim3(1024), 0, 0, s);
-          CHECK(hipDeviceSynchronize());
-          CHECK(hipMemcpy(h2.data(), o2, 4 * n, hipMemcpyDeviceToHost));
-          uint64_t bad = 0;
-          for (uint64_t i = 0; i < n; i++) bad += h1[i] != h2[i];
-          printf("    %s results: %s (%llu of %llu differ from crc)\n", names[v], bad ? "DIFFER" : "equal",
-                 (unsigned long long)bad, (unsigned long long)n);
-        }
-      }
-      fflush(stdout);
-      CHECK(hipFree(data));
-      CHECK(hipFree(dp));
-      CHECK(hipFree(dl));
-      CHECK(hipFree(o1));
-      CHECK(hipFree(o2));
+      if (first && b == 0) fprintf(stderr, " %.1f us\n", ms * 1e3);
     }
   };
 
@@ -512,119 +324,138 @@ int main(int argc, char **argv) {
     CHECK(hipMemcpy(dl, hl.data(), 8 * kN * kBatches, hipMemcpyHostToDevice));
     CHECK(launch_fill_synthetic(dp, dl, kN * kBatches, 0, 1, 0xC0FFEE, 0));
     CHECK(hipDeviceSynchronize());
-    const char *names[] = {"pb", "grid8", "grid16", "wgc", "pb-tail", "crc", "pb-lds4", "pb-lds8", "crc-q6",
-                           "crc-q16", "crc-q26"};
-    constexpr int kV = 11;
-    uint32_t *qout;  // results of the queue forms (compared with crc's below)
-    CHECK(hipMalloc(&qout, 4 * kN * 4));
+    const char *names[] = {"pb", "grid8", "grid16", "wgc", "pb-tail", "crc", "pb-lds4", "pb-lds8"};
+    constexpr int kV = 8;
     std::vector<std::vector<double>> t(kV);
-    // the queue forms (v >= 8) run last, in their own pass (part 3 below):
-    // a form that never ends must not cost the other figures
-    for (int pass = 0; pass < 2; pass++) {
-    if (pass == 1) {
-      printf("ceiling_probe part 1 (queue forms, run last)\n");
-      fflush(stdout);
-    }
     for (int r = 0; r < reps; r++)
-      for (int v = pass ? 8 : 0; v < (pass ? kV : 8); v++) {
-          cur_name = names[v];
-          cur_first = r == 0;
-          timed(kBatches, [&](int b, hipEvent_t a, hipEvent_t z) {
+      for (int v = 0; v < kV; v++)
+        timed(names[v], r == 0, kBatches, [&](int b, hipEvent_t a, hipEvent_t z) {
           const uint8_t *base = data + (uint64_t)b * kBatchBytes;
-            switch (v) {
-              case 0: hipExtLaunchKernelGGL(k_pb, dim3(cus), dim3(1024), 0, 0, a, z, 0, base, out); break;
-              case 1: hipExtLaunchKernelGGL(k_grid8, dim3(cus * 8), dim3(256), 0, 0, a, z, 0, base, out); break;
-              case 2: hipExtLaunchKernelGGL(k_grid16, dim3(cus), dim3(1024), 0, 0, a, z, 0, base, out); break;
-              case 3: hipExtLaunchKernelGGL(k_wgc, dim3(cus), dim3(1024), 0, 0, a, z, 0, base, out); break;
-              case 4:
-                CHECK(hipMemsetAsync(scratch, 0, 16 * 256, 0));
-                hipExtLaunchKernelGGL(k_pb_tail, dim3(cus), dim3(1024), 0, 0, a, z, 0, base, scratch, out);
-                break;
-              case 6: hipExtLaunchKernelGGL(k_pb_lds<4>, dim3(cus), dim3(1024), 0, 0, a, z, 0, base, out); break;
-              case 7: hipExtLaunchKernelGGL(k_pb_lds<8>, dim3(cus), dim3(1024), 0, 0, a, z, 0, base, out); break;
-              case 8: case 9: case 10: {
-                BatchArgs x{};
-                x.ptrs = reinterpret_cast<const uint8_t *const *>(dp + (uint64_t)b * kN);
-                x.lens = dl + (uint64_t)b * kN;
-                x.prefix = dpre;
-                x.out = qout + kN * (uint64_t)(v - 7);
-                x.n = kN;
-                x.tab = d_tab;
-                x.ctr = scratch + 2048;
-                x.done = scratch + 2049;
-                x.acc = reinterpret_cast<uint64_t *>(scratch + 4096);
-                x.wg_ctr = scratch + 65536;
-                x.fault = scratch + 70000;
-                x.dyn_shift = kDynAuto;
-                if (v == 8)
-                  hipExtLaunchKernelGGL((crc32_batch_kernel<false, kDepth, 0, true, false, 1, kLoadNt, true, kWindowed, 6>),
-                                        dim3(cus), dim3(kThreads), 0, 0, a, z, 0, x);
-                else if (v == 9)
-                  hipExtLaunchKernelGGL((crc32_batch_kernel<false, kDepth, 0, true, false, 1, kLoadNt, true, kWindowed, 16>),
-                                        dim3(cus), dim3(kThreads), 0, 0, a, z, 0, x);
-                else
-                  hipExtLaunchKernelGGL((crc32_batch_kernel<false, kDepth, 0, true, false, 1, kLoadNt, true, kWindowed, 26>),
-                                        dim3(cus), dim3(kThreads), 0, 0, a, z, 0, x);
-                break;
-              }
-              default: {
-                BatchArgs x{};
-                x.ptrs = reinterpret_cast<const uint8_t *const *>(dp + (uint64_t)b * kN);
-                x.lens = dl + (uint64_t)b * kN;
-                x.prefix = dpre;
-                x.out = qout;
-                x.n = kN;
-                x.tab = d_tab;
-                x.ctr = scratch + 2048;
-                x.done = scratch + 2049;
-                x.acc = reinterpret_cast<uint64_t *>(scratch + 4096);
-                x.dyn_shift = kDynAuto;
-                hipExtLaunchKernelGGL(
-                    (crc32_batch_kernel<false, kDepth, 0, true, false, 1, kLoadNt, true, kWindowed, kPerBufForm>),
-                    dim3(cus), dim3(kThreads), 0, 0, a, z, 0, x);
-              }
+          switch (v) {
+            case 0: hipExtLaunchKernelGGL(k_pb, dim3(cus), dim3(1024), 0, 0, a, z, 0, base, out); break;
+            case 1: hipExtLaunchKernelGGL(k_grid8, dim3(cus * 8), dim3(256), 0, 0, a, z, 0, base, out); break;
+            case 2: hipExtLaunchKernelGGL(k_grid16, dim3(cus), dim3(1024), 0, 0, a, z, 0, base, out); break;
+            case 3: hipExtLaunchKernelGGL(k_wgc, dim3(cus), dim3(1024), 0, 0, a, z, 0, base, out); break;
+            case 4:
+              CHECK(hipMemsetAsync(scratch, 0, 16 * 256, 0));
+              hipExtLaunchKernelGGL(k_pb_tail, dim3(cus), dim3(1024), 0, 0, a, z, 0, base, scratch, out);
+              break;
+            case 6: hipExtLaunchKernelGGL(k_pb_lds<4>, dim3(cus), dim3(1024), 0, 0, a, z, 0, base, out); break;
+            case 7: hipExtLaunchKernelGGL(k_pb_lds<8>, dim3(cus), dim3(1024), 0, 0, a, z, 0, base, out); break;
+            default: {
+              BatchArgs x{};
+              x.ptrs = reinterpret_cast<const uint8_t *const *>(dp + (uint64_t)b * kN);
+              x.lens = dl + (uint64_t)b * kN;
+              x.prefix = dpre;
+              x.out = out;
+              x.n = kN;
+              x.tab = d_tab;
+              x.ctr = scratch + 2048;
+              x.done = scratch + 2049;
+              x.acc = reinterpret_cast<uint64_t *>(scratch + 4096);
+              x.dyn_shift = kDynAuto;
+              hipExtLaunchKernelGGL(
+                  (crc32_batch_kernel<false, kDepth, 0, true, false, 1, kLoadNt, true, kWindowed, kPerBufForm>),
+                  dim3(cus), dim3(kThreads), 0, 0, a, z, 0, x);
             }
-          }, t[v]);
-      }
-    if (pass == 0)
-      printf("ceiling_probe part 1: config 2 (4096 x 64 KiB), %d CUs, %d batches rotated, %d reps\n", cus, kBatches,
-             reps);
-    for (int v = pass ? 8 : 0; v < (pass ? kV : 8); v++) {
-      double s = 0;
-      for (double x : t[v]) s += x;
-      const double avg = s / t[v].size();
+          }
+        }, t[v]);
+    printf("ceiling_probe part 1: config 2 (4096 x 64 KiB), %d CUs, %d batches rotated, %d reps\n", cus, kBatches,
+           reps);
+    for (int v = 0; v < kV; v++) {
+      double sum = 0;
+      for (double x : t[v]) sum += x;
+      const double avg = sum / t[v].size();
       printf("  %-8s avg %7.2f us  p10 %7.2f  p50 %7.2f  %7.1f GB/s (avg)\n", names[v], avg * 1e3, pct(t[v], 0.1) * 1e3,
              pct(t[v], 0.5) * 1e3, kBatchBytes / (avg * 1e-3) / 1e9);
     }
-    if (pass == 1) {  // the queue forms' CRCs against the product form's (all ran batch 15 last)
-      std::vector<uint32_t> h(4 * kN);
-      CHECK(hipMemcpy(h.data(), qout, 16 * kN, hipMemcpyDeviceToHost));
-      for (int q = 1; q < 4; q++) {
-        uint64_t bad = 0;
-        for (uint64_t i = 0; i < kN; i++) bad += h[q * kN + i] != h[i];
-        printf("  %s results: %s (%llu of %llu differ from crc)\n", names[7 + q], bad ? "DIFFER" : "equal",
-               (unsigned long long)bad, (unsigned long long)kN);
-      }
-      uint32_t z[16], fl = 0;
-      CHECK(hipMemcpy(&fl, scratch + 70000, 4, hipMemcpyDeviceToHost));
-      printf("  queue fault word: %u\n", fl);
-      CHECK(hipMemcpy(z, scratch + 65536, sizeof z, hipMemcpyDeviceToHost));
-      uint32_t nz = 0;
-      for (uint32_t x : z) nz |= x;
-      printf("  queue counters after the launches: %s\n", nz ? "NOT ZERO" : "zero");
-    }
     fflush(stdout);
-    if (pass == 0) {  // part 2 first; then back here for the queue forms
-      part2();
-      fflush(stdout);
-    }
-    }
-    CHECK(hipFree(qout));
     CHECK(hipFree(data));
     CHECK(hipFree(dp));
     CHECK(hipFree(dl));
     CHECK(hipFree(dpre));
   }
 
+  // ---------------------------------------------------------------- part 2
+  const uint64_t sizes[] = {1024, 2048, 3000, 4096, 8192};
+  fprintf(stderr, "part 2\n");
+  printf("ceiling_probe part 2: uniform small buffers, 2 batches of >= 1 GiB rotated, %d reps\n", reps);
+  for (uint64_t L : sizes) {
+    const uint64_t stride = (L + 15) & ~15ull;
+    const uint64_t n = (1ull << 30) / L;
+    uint8_t *data;
+    CHECK(hipMalloc(&data, 2 * n * stride + 256));
+    uint64_t *dp, *dl;
+    uint32_t *o1, *o2;  // "crc" and the other CRC forms (compared below)
+    CHECK(hipMalloc(&dp, 16 * n));
+    CHECK(hipMalloc(&dl, 16 * n));
+    CHECK(hipMalloc(&o1, 4 * n));
+    CHECK(hipMalloc(&o2, 4 * n));
+    std::vector<uint64_t> hp(2 * n), hl(2 * n, L);
+    for (uint64_t i = 0; i < 2 * n; i++) hp[i] = (uint64_t)(data + i * stride);
+    CHECK(hipMemcpy(dp, hp.data(), 16 * n, hipMemcpyHostToDevice));
+    CHECK(hipMemcpy(dl, hl.data(), 16 * n, hipMemcpyHostToDevice));
+    CHECK(launch_fill_synthetic(dp, dl, 2 * n, 0, 1, 0xC0FFEE, 0));
+    CHECK(hipDeviceSynchronize());
+    const char *names[] = {"read-G8", "read-G16", "read-G8c", "crc", "crc-G8c", "crc-G16", "crc-G8"};
+    constexpr int kV = 7;
+    std::vector<std::vector<double>> t(kV);
+    const int lanes = L <= 2048 ? 8 : 16;  // the product's choice (small_lanes)
+    auto crc_launch = [&](int v, const uint64_t *p, const uint64_t *l, uint32_t *o, hipEvent_t a, hipEvent_t z) {
+      SmallArgs sa{};
+      sa.ptrs = reinterpret_cast<const uint8_t *const *>(p);
+      sa.lens = l;
+      sa.n = n;
+      sa.tab = d_tab;
+      sa.out = o;
+      const int form = v == 3 ? (lanes == 8 ? 6 : 5) : v;  // 4: G8c, 5: G16, 6: G8
+      if (form == 4)
+        hipExtLaunchKernelGGL((crc32_small_kernel<false, 8, 4, true>), dim3(cus), dim3(1024), 0, 0, a, z, 0, sa);
+      else if (form == 5)
+        hipExtLaunchKernelGGL((crc32_small_kernel<false, 16, 8>), dim3(cus), dim3(1024), 0, 0, a, z, 0, sa);
+      else
+        hipExtLaunchKernelGGL((crc32_small_kernel<false, 8, 4>), dim3(cus), dim3(1024), 0, 0, a, z, 0, sa);
+    };
+    for (int r = 0; r < reps; r++)
+      for (int v = 0; v < kV; v++)
+        timed(names[v], r == 0, 2, [&](int b, hipEvent_t a, hipEvent_t z) {
+          const uint64_t *p = dp + (uint64_t)b * n, *l = dl + (uint64_t)b * n;
+          const uint8_t *base = data + (uint64_t)b * n * stride;
+          switch (v) {
+            case 0: hipExtLaunchKernelGGL((k_small_read<8, 4, true>), dim3(cus), dim3(1024), 0, 0, a, z, 0, p, l, base, stride, L, n, out); break;
+            case 1: hipExtLaunchKernelGGL((k_small_read<16, 8, true>), dim3(cus), dim3(1024), 0, 0, a, z, 0, p, l, base, stride, L, n, out); break;
+            case 2: hipExtLaunchKernelGGL((k_small_read<8, 4, true, true>), dim3(cus), dim3(1024), 0, 0, a, z, 0, p, l, base, stride, L, n, out); break;
+            default: crc_launch(v, p, l, v == 3 ? o1 : o2, a, z);
+          }
+        }, t[v]);
+    printf("  L %5llu  n %8llu per batch\n", (unsigned long long)L, (unsigned long long)n);
+    for (int v = 0; v < kV; v++) {
+      double sum = 0;
+      for (double x : t[v]) sum += x;
+      const double avg = sum / t[v].size();
+      printf("    %-9s avg %8.2f us  %7.1f GB/s (avg)  %7.1f GB/s (best)\n", names[v], avg * 1e3,
+             n * L / (avg * 1e-3) / 1e9, n * L / (pct(t[v], 0) * 1e-3) / 1e9);
+    }
+    {  // every CRC form against "crc" (whose last launch ran batch 1), on batch 1
+      std::vector<uint32_t> h1(n), h2(n);
+      CHECK(hipMemcpy(h1.data(), o1, 4 * n, hipMemcpyDeviceToHost));
+      for (int v = 4; v < kV; v++) {
+        CHECK(hipMemset(o2, 0, 4 * n));
+        crc_launch(v, dp + n, dl + n, o2, ev[0], ev[1]);
+        CHECK(hipDeviceSynchronize());
+        CHECK(hipMemcpy(h2.data(), o2, 4 * n, hipMemcpyDeviceToHost));
+        uint64_t bad = 0;
+        for (uint64_t i = 0; i < n; i++) bad += h1[i] != h2[i];
+        printf("    %s results: %s (%llu of %llu differ from crc)\n", names[v], bad ? "DIFFER" : "equal",
+               (unsigned long long)bad, (unsigned long long)n);
+      }
+    }
+    fflush(stdout);
+    CHECK(hipFree(data));
+    CHECK(hipFree(dp));
+    CHECK(hipFree(dl));
+    CHECK(hipFree(o1));
+    CHECK(hipFree(o2));
+  }
   return 0;
 }

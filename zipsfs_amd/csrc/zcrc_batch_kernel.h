@@ -527,48 +527,6 @@ __device__ void split_accumulate(const BatchArgs &a, uint64_t i, uint64_t n, uin
   }
 }
 
-// The per-buffer queue form (kPB form 6, round 5): a buffer of at least
-// 2 kQueuePiece bytes is cut, from its end, into up to 4 parts of
-// kQueuePiece bytes (part 0 takes the rest at the front).  Its owner wave
-// checksums part 0; the other parts of the workgroup's buffers are claimed
-// from the workgroup's counter by whichever of its waves is free, so that
-// the waves the SIMDs serve first take more (in round 4's form every wave
-// had its whole 64 KiB: wave slots ended between 27 and 43 us of a 46 us
-// config-2 launch, tools/c2_probe).  Parts meet in the buffer's 64-bit
-// accumulator (count | xor), as split pieces do.
-constexpr uint64_t kQueuePiece = 16ull << 10;
-__device__ __forceinline__ uint32_t queue_parts(uint64_t len) {
-  return len >= 2 * kQueuePiece ? (uint32_t)(len / kQueuePiece < 4 ? len / kQueuePiece : 4) : 1u;
-}
-// x^(8 kQueuePiece d), d = 1..3: moves a part's register over the d parts after it
-constexpr uint32_t kQueueShift1 = MctBasis<17>{}.q[31];  // x^(2^17) = x^(8 * 16384)
-constexpr uint32_t kQueueShift2 = MctBasis<18>{}.q[31];
-constexpr uint32_t kQueueShift3 = gf2_mul(kQueueShift1, kQueueShift2);
-static_assert(kQueuePiece == 16384, "kQueueShift* are x^(8 * 16384 * d)");
-
-// Part contribution of a queue-form buffer i of `parts` parts; `after`: parts
-// behind this one.  The contribution that completes the count stores the CRC
-// and returns the word to zero (split_accumulate's protocol, count = parts).
-__device__ void part_accumulate(const BatchArgs &a, uint64_t i, uint32_t parts, uint32_t after, uint32_t r) {
-  const uint32_t contrib = after == 0 ? ~r
-                           : gf2_mul_uniform(after == 1 ? kQueueShift1 : after == 2 ? kQueueShift2 : kQueueShift3, r);
-  unsigned long long *word = reinterpret_cast<unsigned long long *>(a.acc + i);
-  unsigned long long expect = 0;
-  for (uint32_t guard = 0; guard < (1u << 16); guard++) {  // (a retry follows another part's update: bounded)
-    const unsigned long long want = (((expect >> 32) + 1) << 32) | (uint32_t)((uint32_t)expect ^ contrib);
-    const unsigned long long got = atomicCAS(word, expect, want);
-    if (got == expect) {
-      if ((want >> 32) == parts) {
-        a.out[i] = (uint32_t)want;
-        atomicExch(word, 0ull);
-      }
-      return;
-    }
-    expect = got;
-  }
-  if (a.fault) atomicOr(a.fault, 4u);  // never expected: reported, never a hang
-}
-
 // ------------------------------------------------------------ the kernel
 
 // kD: 1 KiB blocks per register group (two groups in flight); kAblate == 1
@@ -915,7 +873,7 @@ __device__ __forceinline__ uint32_t piece_raw(const uint32_t *s_lds, const uint8
 }
 
 // zcrc_small_kernel.h (included at the end of this header)
-template <bool kStrided, int G, int kD, int kAblate>
+template <bool kStrided, int G, int kD, int kAblate, bool kCoal = false>
 __device__ __forceinline__ void small_body(const SmallArgs &a, uint32_t *s_lds, uint64_t n, uint32_t blk,
                                            uint32_t nblk);
 
@@ -1067,13 +1025,10 @@ __global__ __launch_bounds__(kThreads) void crc32_batch_kernel(BatchArgs args) {
       }
       const bool own = b < args.n && blen <= kPerBufMax;  // wave-uniform
       const uint8_t *bptr = reinterpret_cast<const uint8_t *>(bp);
-      // form 6: the wave's own part is part 0, [0, hi0)
-      const uint32_t nparts = kForm == 6 && own ? queue_parts(blen) : 1u;
-      const uint64_t hi0 = blen - (uint64_t)(nparts - 1) * kQueuePiece;
       uint4 pre[2 * kDP];
       // kPB >= 5: the first payload loads go out as soon as the descriptor is
       // in, ahead of the table build (A/B form)
-      if (kForm >= 5) piece_preload<kDP, kAux>(bptr, 0, hi0, lane, own && blen >= 4, pre);
+      if (kForm >= 5) piece_preload<kDP, kAux>(bptr, 0, blen, lane, own && blen >= 4, pre);
       if (wg_busy) {
         const uint32_t e = braid_gen_lane(lane, slot);
         uint4 *dst = reinterpret_cast<uint4 *>(s_lds);
@@ -1111,13 +1066,10 @@ __global__ __launch_bounds__(kThreads) void crc32_batch_kernel(BatchArgs args) {
           r = ~bseed;
           for (uint32_t p = 0; p < (uint32_t)blen; p++) r = (r >> 8) ^ tab->stdtab[(r ^ bptr[p]) & 0xFFu];
         } else {
-          r = piece_raw<kDP, kAblate, kAux, false, true, kPrioMode == 1>(s_lds, bptr, 0, hi0, bseed, lane, nullptr,
+          r = piece_raw<kDP, kAblate, kAux, false, true, kPrioMode == 1>(s_lds, bptr, 0, blen, bseed, lane, nullptr,
                                                                         pre);
         }
-        if (lane == 0) {
-          if (nparts > 1) part_accumulate(args, b, nparts, nparts - 1, r);
-          else args.out[b] = ~r;
-        }
+        if (lane == 0) args.out[b] = ~r;
         if (kStamp && lane == 0) {  // diagnostic build (tools/c2_probe): this wave's timeline
           const uint64_t w = (uint64_t)blockIdx.x * kWaves + slot;
           args.stamps[8 * w + 0] = t_fill;
@@ -1127,47 +1079,6 @@ __global__ __launch_bounds__(kThreads) void crc32_batch_kernel(BatchArgs args) {
           args.stamps[8 * w + 6] = t_lens;
         }
         if (kPrioMode == 1) __builtin_amdgcn_s_setprio(0);
-      }
-      if (kForm == 6 && wg_busy) {
-        // the workgroup's queue: item t = part 1 + t / nb of its buffer t % nb
-        // (nb = its buffers: slot s has buffer s * grid + blockIdx.x); waves
-        // whose own buffer has parts claim until the items run out
-        const uint32_t g = blockIdx.x;
-        const uint32_t nb = (uint32_t)((args.n - g + grid - 1) / grid);  // <= kWaves
-        const uint32_t items = 3u * nb;
-        uint32_t *ctr = args.wg_ctr + 2 * g;
-        if (nparts > 1) {
-          __builtin_amdgcn_s_setprio(0);
-          for (uint32_t guard = 0; guard <= items; guard++) {  // at most items + 1 claims
-            uint32_t t = 0;
-            if (lane == 0) t = atomicAdd(ctr, 1u);
-            t = uni32(t);
-            if (t >= items) break;
-            if (guard == items) {  // never expected: reported, never a hang
-              if (lane == 0 && args.fault) atomicOr(args.fault, 2u);
-              break;
-            }
-            const uint64_t bs = (uint64_t)(t % nb) * grid + g;
-            const uint32_t j = 1u + t / nb;
-            const uint64_t ls = uni64(args.lens[bs]);
-            if (ls > kPerBufMax) continue;
-            const uint32_t ps = queue_parts(ls);
-            if (j >= ps) continue;
-            const uint8_t *sp = reinterpret_cast<const uint8_t *>(uni64(reinterpret_cast<uint64_t>(args.ptrs[bs])));
-            const uint64_t lo = ls - (uint64_t)(ps - j) * kQueuePiece;
-            const uint32_t r = piece_raw<kDP, kAblate, kAux, false>(s_lds, sp, lo, lo + kQueuePiece, 0u, lane, nullptr);
-            if (lane == 0) part_accumulate(args, bs, ps, ps - 1 - j, r);
-          }
-        }
-        // every wave of the workgroup counts itself out; the last one returns
-        // both counters to zero for the next launch
-        if (lane == 0) {
-          __threadfence();
-          if (atomicAdd(ctr + 1, 1u) + 1u == (uint32_t)kWaves) {
-            atomicExch(ctr, 0u);
-            atomicExch(ctr + 1, 0u);
-          }
-        }
       }
       __syncthreads();  // every wave is done with the tables: the LDS is free
       if (lane == 0) s_lds[slot] = any_big;

@@ -83,12 +83,7 @@ struct BatchArgs {
   const uint32_t *seeds_split;
   const uint4 *sdesc;    // the split plan's small list: SmallArgs::sdesc
   uint32_t *fault;       // nullable: set to nonzero when a piece's prefix bounds are inconsistent
-  // per-buffer queue form (crc32_batch_kernel kPB form 6): per workgroup, a
-  // claim counter and a finished-wave counter (2 words), zero at launch and
-  // left zero by the kernel
-  uint32_t *wg_ctr;
 };
-constexpr uint32_t kMaxQueueWgs = 1024;  // wg_ctr holds 2 x kMaxQueueWgs words
 constexpr size_t kFaultByte = 192;  // the fault word's offset in a scratch's counter area (kCtrBytes)
 
 // Small-buffer kernel (zcrc_small_kernel.h): whole buffers of at most

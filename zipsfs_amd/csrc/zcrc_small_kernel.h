@@ -41,7 +41,13 @@ constexpr uint32_t kXinv8Chunk = 7u * 256u;
 
 // kAblate == 1 (measurement builds, zcrc32_batch_device_read_ceiling): the
 // braid steps become one VALU rotate each -- the same loads, no lookups.
-template <bool kStrided, int G, int kD, int kAblate>
+// kCoal (G = 8): lane l of a group reads the 16-B chunks at 16 l and 16 l +
+// 128 of every 256-B block, so that each load instruction covers 128
+// contiguous bytes per buffer (the round-2 layout gave lane l the chunks at
+// 32 l and 32 l + 16: every load touched half of each 128-B line of its
+// buffer, and a pure read in that layout ran at 6.0 TB/s on 1 KiB buffers
+// against 6.8 for 16 lanes, tools/ceiling_probe, profiles/r05/s4).
+template <bool kStrided, int G, int kD, int kAblate, bool kCoal>
 __device__ __forceinline__ void small_body(const SmallArgs &a, uint32_t *s_lds, uint64_t n, uint32_t blk,
                                            uint32_t nblk) {
   static_assert(G == 8 || G == 16, "lanes per buffer");
@@ -119,14 +125,16 @@ __device__ __forceinline__ void small_body(const SmallArgs &a, uint32_t *s_lds, 
     uint32_t s[NS], q[NS];
 #pragma unroll
     for (int t = 0; t < NS; t++) s[t] = 0u, q[t] = 0u;
-    int32_t rel0 = kq ? span - 256 * (int32_t)kmax + 16 * C * (int32_t)lg : -(1 << 30);
+    // chunk c of lane lg: 16 C lg + 16 c (kCoal: 16 lg + 16 G c) in every block
+    constexpr int32_t kLaneStep = kCoal ? 16 : 16 * C, kChunkStep = kCoal ? 16 * G : 16;
+    int32_t rel0 = kq ? span - 256 * (int32_t)kmax + kLaneStep * (int32_t)lg : -(1 << 30);
     for (uint32_t k = 0; k < kmax; k += kD) {
       small_v4u d[kD][C];
 #pragma unroll
       for (int b = 0; b < kD; b++)
 #pragma unroll
         for (int c = 0; c < C; c++) {
-          const int32_t rel = rel0 + 256 * b + 16 * c;
+          const int32_t rel = rel0 + 256 * b + kChunkStep * c;
           d[b][c] = (small_v4u)(0u);
           if (k + b < kmax && rel >= 0)
             d[b][c] = __builtin_nontemporal_load(reinterpret_cast<const small_v4u *>(astart + (uint32_t)rel));
@@ -136,7 +144,7 @@ __device__ __forceinline__ void small_body(const SmallArgs &a, uint32_t *s_lds, 
         if (k + b < kmax) {
 #pragma unroll
           for (int c = 0; c < C; c++) {
-            const int32_t rel = rel0 + 256 * b + 16 * c;
+            const int32_t rel = rel0 + 256 * b + kChunkStep * c;
             uint4 w = make_uint4(d[b][c].x, d[b][c].y, d[b][c].z, d[b][c].w);
             if (rel >= 0 && (rel < rs + 4 || rel + 16 > re))
               w = fix_chunk(w, clamp_rel(rs - rel), clamp_rel(re - rel), clamp_rel(rs - rel), inj);
@@ -158,17 +166,33 @@ __device__ __forceinline__ void small_body(const SmallArgs &a, uint32_t *s_lds, 
     }
 #pragma unroll
     for (int t = 0; t < NS; t++) s[t] ^= q[t];
-    // fold: the lane's dwords sit 4 B apart, lanes 16 C B apart
+    uint32_t r;
+    if (kCoal && C == 2) {
+      // fold, kCoal: a chunk's dwords 4 and 8 B apart (combine tables 0, 1),
+      // the lane's two chunks 16 G = 128 B apart (table 5), lanes 16 B apart
+      // (tables 2, 3, 4: the table c moves a register back 4 * 2^c bytes)
 #pragma unroll
-    for (int t = 0; t < LOG_NS; t++)
+      for (int m = 0; m < NS; m += 2) s[m] ^= comb_apply(s_lds, 0, s[m + 1]);
+      s[0] ^= comb_apply(s_lds, 1, s[2]);
+      s[4] ^= comb_apply(s_lds, 1, s[6]);
+      s[0] ^= comb_apply(s_lds, 5, s[4]);
+      r = s[0];
+      r ^= row_shl<1>(comb_apply(s_lds, 2, r));
+      r ^= row_shl<2>(comb_apply(s_lds, 3, r));
+      r ^= row_shl<4>(comb_apply(s_lds, 4, r));
+    } else {
+      // fold: the lane's dwords sit 4 B apart, lanes 16 C B apart
 #pragma unroll
-      for (int m = 0; m < NS; m += 2 << t) s[m] ^= comb_apply(s_lds, t, s[m + (1 << t)]);
-    // cross-lane levels inside the group (8 or 16 lanes: within a DPP row)
-    uint32_t r = s[0];
-    r ^= row_shl<1>(comb_apply(s_lds, LOG_NS + 0, r));
-    r ^= row_shl<2>(comb_apply(s_lds, LOG_NS + 1, r));
-    r ^= row_shl<4>(comb_apply(s_lds, LOG_NS + 2, r));
-    if (LOG_G == 4) r ^= row_shl<8>(comb_apply(s_lds, LOG_NS + 3, r));
+      for (int t = 0; t < LOG_NS; t++)
+#pragma unroll
+        for (int m = 0; m < NS; m += 2 << t) s[m] ^= comb_apply(s_lds, t, s[m + (1 << t)]);
+      // cross-lane levels inside the group (8 or 16 lanes: within a DPP row)
+      r = s[0];
+      r ^= row_shl<1>(comb_apply(s_lds, LOG_NS + 0, r));
+      r ^= row_shl<2>(comb_apply(s_lds, LOG_NS + 1, r));
+      r ^= row_shl<4>(comb_apply(s_lds, LOG_NS + 2, r));
+      if (LOG_G == 4) r ^= row_shl<8>(comb_apply(s_lds, LOG_NS + 3, r));
+    }
     const uint32_t tpad = (uint32_t)(span - re), a4 = tpad >> 2;
     if (a4 & 2u) r = comb_apply(s_lds, 1, r);
     if (a4 & 1u) r = comb_apply(s_lds, 0, r);
@@ -188,211 +212,10 @@ __device__ __forceinline__ void small_body(const SmallArgs &a, uint32_t *s_lds, 
   }
 }
 
-// The same body with the payload software-pipelined (round 5 A/B form,
-// tools/ceiling_probe "crc-pipe"): the loads of the next step -- the next
-// kD blocks of this group, or the first kD of the wave's next group -- go out
-// before the current step's braid steps, so that every wave keeps two steps
-// in flight, as the batch kernel keeps two register groups (small_body waits
-// for a group's loads, checksums and folds it, and only then loads the next:
-// a 1 KiB buffer is one step).  The next group's descriptor is kept one
-// group further ahead.  Results are small_body's.
-template <bool kStrided, int G, int kD, int kAblate>
-__device__ __forceinline__ void small_body_pipe(const SmallArgs &a, uint32_t *s_lds, uint64_t n, uint32_t blk,
-                                                uint32_t nblk) {
-  static_assert(G == 8 || G == 16, "lanes per buffer");
-  constexpr int C = 16 / G, NS = 4 * C, LOG_NS = NS == 4 ? 2 : 3, LOG_G = G == 8 ? 3 : 4;
-  constexpr uint32_t BPW = 64 / G;  // buffers per wave
-  const uint32_t tid = threadIdx.x, lane = tid & 63u, g = lane / G, lg = lane % G;
-  const uint64_t waves = (uint64_t)nblk * kWaves;
-  const uint64_t nq = (n + BPW - 1) / BPW;
-  uint64_t q = (uint64_t)blk * kWaves + (tid >> 6);
-  if ((uint64_t)blk * kWaves >= nq) return;  // whole workgroup idle: skip the table fill
-
-  // a lane's list entry: pointer, length, seed, result index (kNone: no
-  // entry); everything else is derived per step, to keep registers free
-  constexpr uint32_t kNone = 0xFFFFFFFFu;
-  struct Ent {
-    uint64_t p;
-    uint32_t len, seed, j;
-  };
-  auto desc = [&](uint64_t qq, Ent &r) {  // this lane's entry of group qq (if any)
-    r = Ent{0, 0, 0, kNone};
-    const uint64_t k = BPW * qq + g;
-    if (qq >= nq || k >= n) return;
-    if (kStrided) {
-      r.j = (uint32_t)k;
-      r.p = reinterpret_cast<uint64_t>(a.base) + k * a.stride;
-      r.len = (uint32_t)a.len;
-    } else if (a.sdesc) {
-      const uint4 d = a.sdesc[k];
-      const uint64_t pw = (uint64_t)d.x | ((uint64_t)d.y << 32);
-      r.j = d.z;
-      r.p = pw & 0xFFFFFFFFFFFFull;
-      r.len = (uint32_t)(pw >> 48);
-      r.seed = d.w;
-      return;
-    } else {
-      r.j = (uint32_t)k;
-      r.p = reinterpret_cast<uint64_t>(a.ptrs[k]);
-      r.len = (uint32_t)(a.lens ? a.lens[k] : a.prefix[k + 1] - a.prefix[k]);
-    }
-    r.seed = a.seeds ? a.seeds[r.j] : 0u;
-  };
-  // blocks of the entry (0 for none and for tiny ones, < 4 bytes: bytewise)
-  auto blocks = [&](const Ent &x) -> uint32_t {
-    const int32_t span = ((int32_t)(x.p & 15u) + (int32_t)x.len + 15) & ~15;
-    return (x.j != kNone && x.len >= 4u) ? (uint32_t)(span + 255) >> 8 : 0u;
-  };
-  auto kmax_of = [&](const Ent &x) -> uint32_t {  // wave-uniform call
-    return uni32(__reduce_max_sync(0xFFFFFFFFFFFFFFFFull, blocks(x)));
-  };
-
-  Ent cur, nxt, far;
-  desc(q, cur);
-  desc(q + waves, nxt);
-  desc(q + 2 * waves, far);  // the entry after next, loaded one group early
-
-  {  // LDS: braided MCT(x^2048) | combine tables (small_body's layout)
-    uint4 *dst = reinterpret_cast<uint4 *>(s_lds);
-    const uint32_t *b = a.tab->braid256;
-#pragma unroll
-    for (int k = 0; k < 8; k++) {
-      const uint32_t o = 16u * (tid + 1024u * k);
-      const uint32_t v = b[(((o >> 16) << 1) | ((o >> 7) & 1u)) * 256u + ((o >> 8) & 255u)];
-      dst[tid + 1024u * k] = make_uint4(v, v, v, v);
-    }
-    const uint4 *cs = reinterpret_cast<const uint4 *>(a.tab->comb);
-    uint4 *cd = reinterpret_cast<uint4 *>(s_lds + kLdsCombDword);
-    cd[tid] = cs[tid];
-    cd[tid + 1024u] = tid >= kXinv8Chunk - 1024u && tid < kXinv8Chunk - 1024u + 64u
-                          ? reinterpret_cast<const uint4 *>(a.tab->xinv8)[tid - (kXinv8Chunk - 1024u)]
-                          : cs[tid + 1024u];
-  }
-  uint32_t kcur = kmax_of(cur), knxt = kmax_of(nxt);
-  __syncthreads();
-  const uint32_t lo0 = (lane & 31u) * 4u;
-  const uint32_t o0 = lo0, o1 = lo0 + 128u, o2 = lo0 + 65536u, o3 = lo0 + 65536u + 128u;
-
-  // chunk-relative offset of block 0 of the entry's aligned span for this lane
-  auto rel0_of = [&](const Ent &x, uint32_t kmax) -> int32_t {
-    const int32_t span = ((int32_t)(x.p & 15u) + (int32_t)x.len + 15) & ~15;
-    return blocks(x) ? span - 256 * (int32_t)kmax + 16 * C * (int32_t)lg : -(1 << 30);
-  };
-  auto load = [&](const Ent &x, uint32_t kmax, uint32_t k, small_v4u (&d)[kD][C]) {
-    const int32_t rel0 = rel0_of(x, kmax);
-    const uint64_t astart = x.p & ~(uint64_t)15;
-#pragma unroll
-    for (int b = 0; b < kD; b++)
-#pragma unroll
-      for (int c = 0; c < C; c++) {
-        const int32_t rel = rel0 + 256 * ((int32_t)k + b) + 16 * c;
-        d[b][c] = (small_v4u)(0u);
-        if (k + (uint32_t)b < kmax && rel >= 0)
-          d[b][c] = __builtin_nontemporal_load(reinterpret_cast<const small_v4u *>(astart + (uint32_t)rel));
-      }
-  };
-  uint32_t s[NS], qv[NS];
-#pragma unroll
-  for (int t = 0; t < NS; t++) s[t] = 0u, qv[t] = 0u;
-  auto consume = [&](const Ent &x, uint32_t kmax, uint32_t k, small_v4u (&d)[kD][C]) {
-    const uint32_t inj = ~x.seed;
-    const int32_t rel0 = rel0_of(x, kmax), rs = (int32_t)(x.p & 15u), re = rs + (int32_t)x.len;
-#pragma unroll
-    for (int b = 0; b < kD; b++) {
-      if (k + (uint32_t)b < kmax) {
-#pragma unroll
-        for (int c = 0; c < C; c++) {
-          const int32_t rel = rel0 + 256 * ((int32_t)k + b) + 16 * c;
-          uint4 w = make_uint4(d[b][c].x, d[b][c].y, d[b][c].z, d[b][c].w);
-          if (rel >= 0 && (rel < rs + 4 || rel + 16 > re))
-            w = fix_chunk(w, clamp_rel(rs - rel), clamp_rel(re - rel), clamp_rel(rs - rel), inj);
-          if (kAblate == 1) {
-            s[4 * c + 0] = __builtin_amdgcn_alignbit(s[4 * c + 0] ^ w.x, s[4 * c + 0] ^ w.x, 5);
-            s[4 * c + 1] = __builtin_amdgcn_alignbit(s[4 * c + 1] ^ w.y, s[4 * c + 1] ^ w.y, 5);
-            s[4 * c + 2] = __builtin_amdgcn_alignbit(s[4 * c + 2] ^ w.z, s[4 * c + 2] ^ w.z, 5);
-            s[4 * c + 3] = __builtin_amdgcn_alignbit(s[4 * c + 3] ^ w.w, s[4 * c + 3] ^ w.w, 5);
-          } else {
-            braid_step2(s_lds, s[4 * c + 0], qv[4 * c + 0], w.x, o0, o1, o2, o3);
-            braid_step2(s_lds, s[4 * c + 1], qv[4 * c + 1], w.y, o0, o1, o2, o3);
-            braid_step2(s_lds, s[4 * c + 2], qv[4 * c + 2], w.z, o0, o1, o2, o3);
-            braid_step2(s_lds, s[4 * c + 3], qv[4 * c + 3], w.w, o0, o1, o2, o3);
-          }
-        }
-      }
-    }
-  };
-  auto finish = [&](const Ent &x) {  // fold, undo the trailing padding, store; registers back to zero
-#pragma unroll
-    for (int t = 0; t < NS; t++) s[t] ^= qv[t];
-#pragma unroll
-    for (int t = 0; t < LOG_NS; t++)
-#pragma unroll
-      for (int m = 0; m < NS; m += 2 << t) s[m] ^= comb_apply(s_lds, t, s[m + (1 << t)]);
-    uint32_t r = s[0];
-    r ^= row_shl<1>(comb_apply(s_lds, LOG_NS + 0, r));
-    r ^= row_shl<2>(comb_apply(s_lds, LOG_NS + 1, r));
-    r ^= row_shl<4>(comb_apply(s_lds, LOG_NS + 2, r));
-    if (LOG_G == 4) r ^= row_shl<8>(comb_apply(s_lds, LOG_NS + 3, r));
-    const int32_t re = (int32_t)(x.p & 15u) + (int32_t)x.len;
-    const uint32_t tpad = (uint32_t)(((re + 15) & ~15) - re), a4 = tpad >> 2;
-    if (a4 & 2u) r = comb_apply(s_lds, 1, r);
-    if (a4 & 1u) r = comb_apply(s_lds, 0, r);
-    const uint32_t *xinv8 = s_lds + kLdsCombDword + 4u * kXinv8Chunk;
-    for (uint32_t b = 0; b < 3u; b++)
-      if (b < (tpad & 3u)) r = (r << 8) ^ xinv8[r >> 24];
-    if (x.j != kNone && lg == 0) {
-      if (x.len < 4u) {
-        const uint8_t *bp = reinterpret_cast<const uint8_t *>(x.p);
-        r = ~x.seed;
-        for (uint32_t p = 0; p < x.len; p++) r = (r >> 8) ^ a.tab->stdtab[(r ^ bp[p]) & 0xFFu];
-      }
-      a.out[x.j] = ~r;
-    }
-#pragma unroll
-    for (int t = 0; t < NS; t++) s[t] = 0u, qv[t] = 0u;
-  };
-
-  small_v4u da[kD][C], db[kD][C];
-  uint32_t k = 0;
-  load(cur, kcur, 0, da);
-  // one step: issue the step after (q, k) into `fill`, checksum `use`; false
-  // when the wave's last group is done
-  auto step = [&](small_v4u (&use)[kD][C], small_v4u (&fill)[kD][C]) -> bool {
-    const bool same = k + kD < kcur;
-    if (same) load(cur, kcur, k + kD, fill);
-    else if (q + waves < nq) load(nxt, knxt, 0, fill);
-    consume(cur, kcur, k, use);
-    if (same) {
-      k += kD;
-      return true;
-    }
-    finish(cur);
-    q += waves;
-    if (q >= nq) return false;
-    cur = nxt;
-    kcur = knxt;
-    nxt = far;
-    knxt = kmax_of(nxt);
-    desc(q + 2 * waves, far);
-    k = 0;
-    return true;
-  };
-  for (;;) {
-    if (!step(da, db)) break;
-    if (!step(db, da)) break;
-  }
-}
-
-template <bool kStrided, int G, int kD, int kAblate = 0>
-__global__ __launch_bounds__(1024) void crc32_small_kernel_pipe(SmallArgs a) {
-  __shared__ __attribute__((aligned(16))) uint32_t s_lds[kLdsBytes / 4];
-  small_body_pipe<kStrided, G, kD, kAblate>(a, s_lds, a.n, blockIdx.x, gridDim.x);
-}
-
-template <bool kStrided, int G, int kD>
+template <bool kStrided, int G, int kD, bool kCoal = false>
 __global__ __launch_bounds__(1024) void crc32_small_kernel(SmallArgs a) {
   __shared__ __attribute__((aligned(16))) uint32_t s_lds[kLdsBytes / 4];
-  small_body<kStrided, G, kD, 0>(a, s_lds, a.n, blockIdx.x, gridDim.x);
+  small_body<kStrided, G, kD, 0, kCoal>(a, s_lds, a.n, blockIdx.x, gridDim.x);
 }
 
 }  // namespace zcrc
