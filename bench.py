@@ -389,6 +389,8 @@ def main() -> None:
     ap.add_argument("--cpu-budget-s", type=float, default=12.0)
     ap.add_argument("--cpu-sample-gib", type=float, default=4.0,
                     help="host-resident CPU-baseline sample (>= 2x the host L3)")
+    ap.add_argument("--no-read-ceiling", action="store_true",
+                    help="skip the same-process read ceiling (profiling runs: only the product kernel launches)")
     ap.add_argument("--host-resident-gib", type=float, default=4.0,
                     help="configs 3/5: host-resident zcrc32_batch over this many GiB of the workload's buffers "
                          "(0: skip); at N > 1 rank 0 runs it over every visible GPU")
@@ -501,7 +503,8 @@ def main() -> None:
         glob = result["global"].cpu().numpy().view(np.uint32)
         parity = golden_check(cfg, glob) if rank == 0 else None
         try:  # measurement beside the line's numbers: never fails the run
-            ceiling = read_ceiling(wl, out, steps)
+            ceiling = (read_ceiling(wl, out, steps) if not args.no_read_ceiling else
+                       {"skipped": "--no-read-ceiling", "read_ceiling_gbs": None})
         except Exception as e:
             ceiling = {"error": f"{type(e).__name__}: {e}", "read_ceiling_gbs": None}
         extra_res = extra(wl, out.cpu().numpy().view(np.uint32)) if extra else None

@@ -19,7 +19,8 @@ CFG=${2:-3}
 export TMPDIR=/tmp
 W=gpurun_out/prof_c${CFG}
 mkdir -p "$OUT" "$W"
-BENCH=(python3 bench.py --config "$CFG" --steps 5 --warmup 1 --no-cpu-baseline --no-secondary)
+BENCH=(python3 bench.py --config "$CFG" --steps 5 --warmup 1 --no-cpu-baseline --no-secondary --no-read-ceiling
+       --host-resident-gib 0)
 
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$W/kt" -o bench -- "${BENCH[@]}" > "$W/kt.log" 2>&1
 timeout -k 10 400 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$W/fetch" -o bench -- "${BENCH[@]}" > "$W/fetch.log" 2>&1

@@ -17,13 +17,18 @@ import statistics
 import sys
 
 KERNEL = "crc32_batch_kernel"
+ABLATED = "crc32_batch_kernel<false, 4u, 1,"  # the read-ceiling form (kAblate = 1): never the product's
+
+
+def product(name: str) -> bool:
+    return KERNEL in name and ABLATED not in name
 
 
 def per_dispatch(d, counter):
     vals = {}
     for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
         for r in csv.DictReader(open(f)):
-            if KERNEL in r["Kernel_Name"] and r["Counter_Name"] == counter:
+            if product(r["Kernel_Name"]) and r["Counter_Name"] == counter:
                 vals.setdefault(r["Dispatch_Id"], 0.0)
                 vals[r["Dispatch_Id"]] += float(r["Counter_Value"])
     return list(vals.values())
@@ -34,7 +39,7 @@ def main():
     durs = []
     for f in glob.glob(os.path.join(kt, "**", "*kernel_trace.csv"), recursive=True):
         for r in csv.DictReader(open(f)):
-            if KERNEL in r["Kernel_Name"]:
+            if product(r["Kernel_Name"]):
                 durs.append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-9)
     stats = {}
     for f in glob.glob(os.path.join(kt, "**", "*kernel_stats.csv"), recursive=True):

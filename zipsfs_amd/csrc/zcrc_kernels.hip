@@ -462,18 +462,20 @@ const char *product_kernel_name() {
 }
 
 // Small whole buffers: 16 lanes per buffer with 8 blocks in flight, or 8
-// lanes with 4 (same 32 VGPRs of loads, twice the buffers: pays below ~2 KiB).
+// lanes with 4 (same 32 VGPRs of loads, twice the buffers: pays below ~2 KiB)
+// in the coalesced layout (round 5: 1 KiB 5.08 -> 5.45 TB/s, 2 KiB 5.29 ->
+// 5.92, tools/ceiling_probe, profiles/r05/s6).
 hipError_t launch_small(const SmallArgs &args, bool strided, int lanes, int num_cus, hipStream_t stream,
                         hipEvent_t t0, hipEvent_t t1) {
   const dim3 grid((unsigned)num_cus), block(kThreads);
   if (strided) {
     if (lanes == 8)
-      hipExtLaunchKernelGGL((crc32_small_kernel<true, 8, 4>), grid, block, 0, stream, t0, t1, 0, args);
+      hipExtLaunchKernelGGL((crc32_small_kernel<true, 8, 4, true>), grid, block, 0, stream, t0, t1, 0, args);
     else
       hipExtLaunchKernelGGL((crc32_small_kernel<true, 16, 8>), grid, block, 0, stream, t0, t1, 0, args);
   } else {
     if (lanes == 8)
-      hipExtLaunchKernelGGL((crc32_small_kernel<false, 8, 4>), grid, block, 0, stream, t0, t1, 0, args);
+      hipExtLaunchKernelGGL((crc32_small_kernel<false, 8, 4, true>), grid, block, 0, stream, t0, t1, 0, args);
     else
       hipExtLaunchKernelGGL((crc32_small_kernel<false, 16, 8>), grid, block, 0, stream, t0, t1, 0, args);
   }
@@ -493,7 +495,7 @@ const char *fused_kernel_name() {
 
 // the general-form small kernels as rocprofv3 names them
 const char *small_kernel_name(int lanes) {
-  return lanes == 8 ? "zcrc::crc32_small_kernel<false, 8, 4>" : "zcrc::crc32_small_kernel<false, 16, 8>";
+  return lanes == 8 ? "zcrc::crc32_small_kernel<false, 8, 4, true>" : "zcrc::crc32_small_kernel<false, 16, 8, false>";
 }
 
 hipError_t launch_plan(const uint64_t *d_lens, uint64_t n, uint64_t *d_prefix, uint64_t *d_tile_sum,
