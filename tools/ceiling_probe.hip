@@ -16,6 +16,7 @@
 //             all buffers claimed from one counter by the waves that finish
 //             first
 //   crc       the product's one-launch per-buffer CRC form (kPerBufForm)
+//   crc-17    the product form with an LDS-only table barrier (lds_barrier)
 //   pb-lds4/8 per-CU queue: the workgroup's 16 buffers cut into 4 (8)
 //             pieces; wave s reads piece 0 of its own buffer, then claims
 //             pieces from an LDS counter
@@ -324,8 +325,10 @@ int main(int argc, char **argv) {
     CHECK(hipMemcpy(dl, hl.data(), 8 * kN * kBatches, hipMemcpyHostToDevice));
     CHECK(launch_fill_synthetic(dp, dl, kN * kBatches, 0, 1, 0xC0FFEE, 0));
     CHECK(hipDeviceSynchronize());
-    const char *names[] = {"pb", "grid8", "grid16", "wgc", "pb-tail", "crc", "pb-lds4", "pb-lds8"};
-    constexpr int kV = 8;
+    const char *names[] = {"pb", "grid8", "grid16", "wgc", "pb-tail", "crc", "pb-lds4", "pb-lds8", "crc-17"};
+    constexpr int kV = 9;
+    uint32_t *o17;  // crc-17's results (compared with crc's)
+    CHECK(hipMalloc(&o17, 4 * kN));
     std::vector<std::vector<double>> t(kV);
     for (int r = 0; r < reps; r++)
       for (int v = 0; v < kV; v++)
@@ -347,16 +350,20 @@ int main(int argc, char **argv) {
               x.ptrs = reinterpret_cast<const uint8_t *const *>(dp + (uint64_t)b * kN);
               x.lens = dl + (uint64_t)b * kN;
               x.prefix = dpre;
-              x.out = out;
+              x.out = v == 8 ? o17 : out;
               x.n = kN;
               x.tab = d_tab;
               x.ctr = scratch + 2048;
               x.done = scratch + 2049;
               x.acc = reinterpret_cast<uint64_t *>(scratch + 4096);
               x.dyn_shift = kDynAuto;
-              hipExtLaunchKernelGGL(
-                  (crc32_batch_kernel<false, kDepth, 0, true, false, 1, kLoadNt, true, kWindowed, kPerBufForm>),
-                  dim3(cus), dim3(kThreads), 0, 0, a, z, 0, x);
+              if (v == 8)
+                hipExtLaunchKernelGGL((crc32_batch_kernel<false, kDepth, 0, true, false, 1, kLoadNt, true, kWindowed, 17>),
+                                      dim3(cus), dim3(kThreads), 0, 0, a, z, 0, x);
+              else
+                hipExtLaunchKernelGGL(
+                    (crc32_batch_kernel<false, kDepth, 0, true, false, 1, kLoadNt, true, kWindowed, kPerBufForm>),
+                    dim3(cus), dim3(kThreads), 0, 0, a, z, 0, x);
             }
           }
         }, t[v]);
@@ -369,7 +376,17 @@ int main(int argc, char **argv) {
       printf("  %-8s avg %7.2f us  p10 %7.2f  p50 %7.2f  %7.1f GB/s (avg)\n", names[v], avg * 1e3, pct(t[v], 0.1) * 1e3,
              pct(t[v], 0.5) * 1e3, kBatchBytes / (avg * 1e-3) / 1e9);
     }
+    {  // crc-17 against crc (both ran batch 15 last)
+      std::vector<uint32_t> h1(kN), h2(kN);
+      CHECK(hipMemcpy(h1.data(), out, 4 * kN, hipMemcpyDeviceToHost));
+      CHECK(hipMemcpy(h2.data(), o17, 4 * kN, hipMemcpyDeviceToHost));
+      uint64_t bad = 0;
+      for (uint64_t i = 0; i < kN; i++) bad += h1[i] != h2[i];
+      printf("  crc-17 results: %s (%llu of %llu differ from crc)\n", bad ? "DIFFER" : "equal", (unsigned long long)bad,
+             (unsigned long long)kN);
+    }
     fflush(stdout);
+    CHECK(hipFree(o17));
     CHECK(hipFree(data));
     CHECK(hipFree(dp));
     CHECK(hipFree(dl));

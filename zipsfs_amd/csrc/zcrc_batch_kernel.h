@@ -166,6 +166,18 @@ __device__ __forceinline__ uint32_t row_shl(uint32_t x) {
   return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x100 + kD, 0xF, 0xF, false);
 }
 
+// A workgroup barrier that orders LDS alone: it waits for this wave's LDS
+// operations (lgkmcnt(0)), not for its outstanding global and buffer loads.
+// (__syncthreads() is a workgroup fence on every address space: in the
+// per-buffer mode it made every wave wait, at the table barrier, for the
+// batch lengths it had loaded for the decision taken after the work --
+// loads queued behind the other waves' payload preloads.)
+__device__ __forceinline__ void lds_barrier() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
 // r * c for one of the 8 combine constants resident in LDS.
 __device__ __forceinline__ uint32_t comb_apply(const uint32_t *lds, int c, uint32_t r) {
   const uint32_t *t = lds + kLdsCombDword + c * 1024;
@@ -879,8 +891,9 @@ __device__ __forceinline__ void small_body(const SmallArgs &a, uint32_t *s_lds, 
 
 // kPB: the per-buffer mode's form (fused only): 4 = round 4 (tables built in
 // registers, the decision after the work), 5 = the same with the first
-// payload loads issued before the table build, 3 = round 3 (tables and
-// lengths in front of the one barrier); 3 and 5 are A/B forms for tools/.
+// payload loads issued before the table build, 7 = 5 with an LDS-only table
+// barrier (lds_barrier), 3 = round 3 (tables and lengths in front of the one
+// barrier); 3, 5 and 7 are A/B forms for tools/.
 // kPB + 10: priority by progress through the buffer instead of by wave slot
 // (piece_raw kProg); kPB + 20: no priorities (A/B forms, tools/c2_probe).
 template <bool kStrided, uint32_t kD = kDepth, int kAblate = 0, bool kRotate = true, bool kStamp = false,
@@ -1018,17 +1031,27 @@ __global__ __launch_bounds__(kThreads) void crc32_batch_kernel(BatchArgs args) {
         bseed = args.seeds ? uni32(args.seeds[b]) : 0u;
       }
       uint64_t L[8];  // the decision's lengths (thread t: buffers t + 1024 j), clamped, unguarded
+      auto load_lens = [&]() {
 #pragma unroll
-      for (uint32_t j = 0; j < 8; j++) {
-        const uint64_t idx = tid + 1024u * j;
-        L[j] = args.lens[idx < args.n ? idx : args.n - 1];
-      }
+        for (uint32_t j = 0; j < 8; j++) {
+          const uint64_t idx = tid + 1024u * j;
+          L[j] = args.lens[idx < args.n ? idx : args.n - 1];
+        }
+      };
+      if (kForm < 7) load_lens();
       const bool own = b < args.n && blen <= kPerBufMax;  // wave-uniform
       const uint8_t *bptr = reinterpret_cast<const uint8_t *>(bp);
       uint4 pre[2 * kDP];
       // kPB >= 5: the first payload loads go out as soon as the descriptor is
       // in, ahead of the table build (A/B form)
       if (kForm >= 5) piece_preload<kDP, kAux>(bptr, 0, blen, lane, own && blen >= 4, pre);
+      if (kForm >= 7) {
+        // form >= 7: the decision's lengths behind the preload, so that the
+        // first group's wait (vmcnt, counted in issue order) is not a wait for
+        // them too
+        __builtin_amdgcn_sched_barrier(0);
+        load_lens();
+      }
       if (wg_busy) {
         const uint32_t e = braid_gen_lane(lane, slot);
         uint4 *dst = reinterpret_cast<uint4 *>(s_lds);
@@ -1045,13 +1068,22 @@ __global__ __launch_bounds__(kThreads) void crc32_batch_kernel(BatchArgs args) {
         cdst[tid + 1024u] = cm1;
       }
       const uint64_t t_lens = kStamp ? __builtin_amdgcn_s_memrealtime() : 0;  // diagnostic: tables written
-      __syncthreads();  // the tables are in LDS
+      // the tables are in LDS (form >= 7: an LDS-only barrier, the decision
+      // lengths and the preloads may still be in flight)
+      if (kForm >= 7) lds_barrier();
+      else __syncthreads();
       const uint64_t t_fill = kStamp ? __builtin_amdgcn_s_memrealtime() : 0;
       if (kForm < 5) piece_preload<kDP, kAux>(bptr, 0, blen, lane, own && blen >= 4, pre);
-      bool big = false;
+      // the decision over the lengths L: forms < 7 here, where the compiler
+      // hoisted it (and the waits for L) in front of the table barrier; form
+      // >= 7 after the wave's piece, when L has long arrived
+      auto decide = [&]() -> uint32_t {
+        bool big = false;
 #pragma unroll
-      for (uint32_t j = 0; j < 8; j++) big |= (tid + 1024u * j < args.n) & (L[j] > kPerBufMax);
-      const uint32_t any_big = __ballot(big) ? 1u : 0u;
+        for (uint32_t j = 0; j < 8; j++) big |= (tid + 1024u * j < args.n) & (L[j] > kPerBufMax);
+        return __ballot(big) ? 1u : 0u;
+      };
+      uint32_t any_big = kForm >= 7 ? 0u : decide();
       if (own) {
         // younger wave slots issue first (the round-3 per-buffer form below)
         if (kPrioMode == 0) {
@@ -1080,6 +1112,7 @@ __global__ __launch_bounds__(kThreads) void crc32_batch_kernel(BatchArgs args) {
         }
         if (kPrioMode == 1) __builtin_amdgcn_s_setprio(0);
       }
+      if (kForm >= 7) any_big = decide();
       __syncthreads();  // every wave is done with the tables: the LDS is free
       if (lane == 0) s_lds[slot] = any_big;
       __syncthreads();
