@@ -639,9 +639,12 @@ def main() -> None:
         secondary = {}
         for c in (2, 4):
             # config 2's 50 us steps: 200 of them, so that the first launch's
-            # latency (~30 us) does not weigh on the per-step figure
+            # latency (~30 us) does not weigh on the per-step figure, behind
+            # >= 20 ms of untimed warmup (3 warmup steps left the timed steps
+            # 2-3 us slower than the same launches a few ms later, in the read
+            # ceiling's pairs: profiles/r05/s4, s7)
             ks = max(args.steps, 200 if c == 2 else 20)
-            r = measure(c, ks, max(args.warmup, 3))
+            r = measure(c, ks, max(args.warmup, 400 if c == 2 else 10))
             ach = r["bytes_main"] / (r["avg_kernel_ms"] * 1e-3) / 1e9
             tr, _ = pmc_traffic(c, r["bytes_local"])
             ce = r["ceiling"]

@@ -12,14 +12,22 @@
 //             wave w of W reads blocks w, w + W, ...
 //   wgc       workgroup-cooperative: workgroup g owns buffers g + grid k; its
 //             16 waves interleave 1 KiB blocks over them
-//   pb-tail   per-buffer heads (the first 48 KiB), then the 16 KiB tails of
-//             all buffers claimed from one counter by the waves that finish
-//             first
+//   pb-desc   pb with each buffer's address and length loaded from the
+//             descriptor arrays (the CRC kernel's), not computed
 //   crc       the product's one-launch per-buffer CRC form (kPerBufForm)
-//   crc-17    the product form with an LDS-only table barrier (lds_barrier)
-//   pb-lds4/8 per-CU queue: the workgroup's 16 buffers cut into 4 (8)
-//             pieces; wave s reads piece 0 of its own buffer, then claims
-//             pieces from an LDS counter
+//   abl       the product form with its table lookups replaced by one VALU
+//             op (kAblate = 1: the bench line's read ceiling); -nt: no table
+//             build either; -nd: no table build and no decision at the end;
+//             -nl: no decision lengths (the end barriers kept); -nb: -nd
+//             without the table barrier; -nf: -nb without the fold
+//             (diagnostics: where the product's time over pb goes)
+//   crc-18/nl/19/fm/19fm  per-buffer forms (zcrc_batch_kernel.h kPB): 18 =
+//             decision after the piece; nl = no decision (right whenever no
+//             buffer exceeds 64 KiB); 19 = 18 with the lengths in 16-B buffer
+//             loads; fm = the fold's lane levels masked to the lanes read
+//             next; results compared with crc's
+// (Round-5 sessions 9-13 also measured forms 17 and the slot priorities of
+// form 5 in the ablated kernel: profiles/r05/s13.)
 // Part 2, uniform small buffers (1024, 2048, 3000, 4096, 8192 B; >= 1 GiB
 // per batch, two batches rotated), whole buffers in the small body's lane
 // mapping (zcrc_small_kernel.h: G lanes per buffer, 256-B blocks, lane l of
@@ -37,7 +45,7 @@
 // Every launch is timed by its own dispatch packet (hipExtLaunchKernelGGL
 // events); the figures are averages over the launches, in GB/s of payload.
 //
-//   make -C tools ceiling_probe && tools/ceiling_probe [reps]
+//   make -C tools ceiling_probe && tools/ceiling_probe [reps [1: part 1 only]]
 #include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -100,6 +108,20 @@ __global__ __launch_bounds__(1024) void k_pb(const uint8_t *base, uint32_t *out)
   if (acc == 0x12345678u) out[w] = acc;
 }
 
+// k_pb with the buffer's address and length loaded from the batch's
+// descriptor arrays (as the CRC kernel does) instead of computed
+__global__ __launch_bounds__(1024) void k_pb_desc(const uint64_t *ptrs, const uint64_t *lens, uint32_t *out) {
+  const uint32_t lane = threadIdx.x & 63u, slot = threadIdx.x >> 6;
+  const uint64_t w = (uint64_t)slot * gridDim.x + blockIdx.x;
+  slot_prio(slot);
+  if (w >= kN) return;
+  const uint64_t p = uni64(ptrs[w]);  // (an int-typed readfirstlane widened with sign extension faulted here)
+  const uint32_t len = (uint32_t)uni64(lens[w]);
+  const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc((void *)p, (short)0, (int)len, 0x00020000);
+  const uint32_t acc = read_blocks(r, 0, len >> 10, lane);
+  if (acc == 0x12345678u) out[w] = acc;
+}
+
 __global__ __launch_bounds__(256) void k_grid8(const uint8_t *base, uint32_t *out) {
   const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc((void *)base, (short)0, 0x7FFFFFFF, 0x00020000);
   uint32_t acc = 0;
@@ -154,37 +176,6 @@ __global__ __launch_bounds__(1024) void k_wgc(const uint8_t *base, uint32_t *out
     for (int u = 0; u < 8; u++) acc ^= xr(v[u]);
   }
   if (acc == 0x12345678u) out[g * 16 + wv] = acc;
-}
-
-// tails are claimed from 16 counters 256 B apart (counter c owns the tails of
-// buffers c, c + 16, ...; a wave starts at the counter of its slot and moves
-// on when it runs dry), so that 4096 claims do not serialise on one address
-// (~11 ns each there: 4096 of them would take ~47 us)
-__global__ __launch_bounds__(1024) void k_pb_tail(const uint8_t *base, uint32_t *ctr, uint32_t *out) {
-  const uint32_t lane = threadIdx.x & 63u, slot = threadIdx.x >> 6;
-  const uint64_t w = (uint64_t)slot * gridDim.x + blockIdx.x;
-  slot_prio(slot);
-  uint32_t acc = 0;
-  if (w < kN) {
-    const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc((void *)(base + w * kLen), (short)0,
-                                                                        (int)kLen, 0x00020000);
-    acc ^= read_blocks(r, 0, 48, lane);
-  }
-  __builtin_amdgcn_s_setprio(0);
-  for (uint32_t c = 0, guard = 0; c < 16 && guard < 4u * kN; guard++) {
-    const uint32_t home = (slot + c) & 15u;
-    uint32_t t = 0;
-    if (lane == 0) t = atomicAdd(ctr + 64 * home, 1u);
-    t = home + 16u * (uint32_t)__builtin_amdgcn_readfirstlane((int)t);
-    if (t >= kN) {
-      c++;
-      continue;
-    }
-    const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc((void *)(base + (uint64_t)t * kLen), (short)0,
-                                                                        (int)kLen, 0x00020000);
-    acc ^= read_blocks(r, 48, 64, lane);
-  }
-  if (acc == 0x12345678u) out[w] = acc;
 }
 
 // Per-CU queue: workgroup g owns buffers g + grid k (k < 16), cut into
@@ -325,10 +316,14 @@ int main(int argc, char **argv) {
     CHECK(hipMemcpy(dl, hl.data(), 8 * kN * kBatches, hipMemcpyHostToDevice));
     CHECK(launch_fill_synthetic(dp, dl, kN * kBatches, 0, 1, 0xC0FFEE, 0));
     CHECK(hipDeviceSynchronize());
-    const char *names[] = {"pb", "grid8", "grid16", "wgc", "pb-tail", "crc", "pb-lds4", "pb-lds8", "crc-17"};
-    constexpr int kV = 9;
-    uint32_t *o17;  // crc-17's results (compared with crc's)
-    CHECK(hipMalloc(&o17, 4 * kN));
+    // v >= 8: per-buffer kernel forms; the real ones (v >= kReal) write their
+    // results to ov, compared with crc's below
+    const char *names[] = {"pb",     "grid8",  "grid16", "wgc",    "pb-desc", "crc",    "pb-lds4",
+                           "pb-lds8", "abl",    "abl-nt", "abl-nd", "abl-nl",  "abl-nb", "abl-nf",
+                           "crc-18", "crc-nl", "crc-19", "crc-fm", "crc-19fm"};
+    constexpr int kV = 19, kReal = 14;
+    uint32_t *ov;
+    CHECK(hipMalloc(&ov, (kV - kReal) * 4 * kN));
     std::vector<std::vector<double>> t(kV);
     for (int r = 0; r < reps; r++)
       for (int v = 0; v < kV; v++)
@@ -340,8 +335,8 @@ int main(int argc, char **argv) {
             case 2: hipExtLaunchKernelGGL(k_grid16, dim3(cus), dim3(1024), 0, 0, a, z, 0, base, out); break;
             case 3: hipExtLaunchKernelGGL(k_wgc, dim3(cus), dim3(1024), 0, 0, a, z, 0, base, out); break;
             case 4:
-              CHECK(hipMemsetAsync(scratch, 0, 16 * 256, 0));
-              hipExtLaunchKernelGGL(k_pb_tail, dim3(cus), dim3(1024), 0, 0, a, z, 0, base, scratch, out);
+              hipExtLaunchKernelGGL(k_pb_desc, dim3(cus), dim3(1024), 0, 0, a, z, 0, dp + (uint64_t)b * kN,
+                                    dl + (uint64_t)b * kN, out);
               break;
             case 6: hipExtLaunchKernelGGL(k_pb_lds<4>, dim3(cus), dim3(1024), 0, 0, a, z, 0, base, out); break;
             case 7: hipExtLaunchKernelGGL(k_pb_lds<8>, dim3(cus), dim3(1024), 0, 0, a, z, 0, base, out); break;
@@ -350,20 +345,32 @@ int main(int argc, char **argv) {
               x.ptrs = reinterpret_cast<const uint8_t *const *>(dp + (uint64_t)b * kN);
               x.lens = dl + (uint64_t)b * kN;
               x.prefix = dpre;
-              x.out = v == 8 ? o17 : out;
+              // the ablated forms' results are not CRCs
+              x.out = v >= kReal ? ov + (v - kReal) * kN : v >= 8 ? scratch + 65536 : out;
               x.n = kN;
               x.tab = d_tab;
               x.ctr = scratch + 2048;
               x.done = scratch + 2049;
               x.acc = reinterpret_cast<uint64_t *>(scratch + 4096);
               x.dyn_shift = kDynAuto;
-              if (v == 8)
-                hipExtLaunchKernelGGL((crc32_batch_kernel<false, kDepth, 0, true, false, 1, kLoadNt, true, kWindowed, 17>),
-                                      dim3(cus), dim3(kThreads), 0, 0, a, z, 0, x);
-              else
-                hipExtLaunchKernelGGL(
-                    (crc32_batch_kernel<false, kDepth, 0, true, false, 1, kLoadNt, true, kWindowed, kPerBufForm>),
-                    dim3(cus), dim3(kThreads), 0, 0, a, z, 0, x);
+#define ZCRC_PB(abl, form)                                                                                \
+  hipExtLaunchKernelGGL((crc32_batch_kernel<false, kDepth, abl, true, false, 1, kLoadNt, true, kWindowed, form>), \
+                        dim3(cus), dim3(kThreads), 0, 0, a, z, 0, x)
+              switch (v) {
+                case 8: ZCRC_PB(1, kPerBufForm); break;
+                case 9: ZCRC_PB(1, 1000 + kPerBufForm); break;
+                case 10: ZCRC_PB(1, 2000 + kPerBufForm); break;
+                case 11: ZCRC_PB(1, 3000 + kPerBufForm); break;
+                case 12: ZCRC_PB(1, 4000 + kPerBufForm); break;
+                case 13: ZCRC_PB(1, 5000 + kPerBufForm); break;
+                case 14: ZCRC_PB(0, 18); break;
+                case 15: ZCRC_PB(0, 3000 + kPerBufForm); break;  // right whenever no buffer exceeds kPerBufMax
+                case 16: ZCRC_PB(0, 19); break;
+                case 17: ZCRC_PB(0, 6000 + kPerBufForm); break;
+                case 18: ZCRC_PB(0, 6019); break;
+                default: ZCRC_PB(0, kPerBufForm);
+              }
+#undef ZCRC_PB
             }
           }
         }, t[v]);
@@ -376,17 +383,19 @@ int main(int argc, char **argv) {
       printf("  %-8s avg %7.2f us  p10 %7.2f  p50 %7.2f  %7.1f GB/s (avg)\n", names[v], avg * 1e3, pct(t[v], 0.1) * 1e3,
              pct(t[v], 0.5) * 1e3, kBatchBytes / (avg * 1e-3) / 1e9);
     }
-    {  // crc-17 against crc (both ran batch 15 last)
-      std::vector<uint32_t> h1(kN), h2(kN);
-      CHECK(hipMemcpy(h1.data(), out, 4 * kN, hipMemcpyDeviceToHost));
-      CHECK(hipMemcpy(h2.data(), o17, 4 * kN, hipMemcpyDeviceToHost));
-      uint64_t bad = 0;
-      for (uint64_t i = 0; i < kN; i++) bad += h1[i] != h2[i];
-      printf("  crc-17 results: %s (%llu of %llu differ from crc)\n", bad ? "DIFFER" : "equal", (unsigned long long)bad,
-             (unsigned long long)kN);
+    {  // the real forms against crc (all ran batch 15 last)
+      std::vector<uint32_t> h0(kN), h1((kV - kReal) * kN);
+      CHECK(hipMemcpy(h0.data(), out, 4 * kN, hipMemcpyDeviceToHost));
+      CHECK(hipMemcpy(h1.data(), ov, (kV - kReal) * 4 * kN, hipMemcpyDeviceToHost));
+      for (int k = 0; k < kV - kReal; k++) {
+        uint64_t bad = 0;
+        for (uint64_t i = 0; i < kN; i++) bad += h0[i] != h1[k * kN + i];
+        printf("  %s results: %s (%llu of %llu differ from crc)\n", names[kReal + k], bad ? "DIFFER" : "equal",
+               (unsigned long long)bad, (unsigned long long)kN);
+      }
     }
     fflush(stdout);
-    CHECK(hipFree(o17));
+    CHECK(hipFree(ov));
     CHECK(hipFree(data));
     CHECK(hipFree(dp));
     CHECK(hipFree(dl));
@@ -394,6 +403,7 @@ int main(int argc, char **argv) {
   }
 
   // ---------------------------------------------------------------- part 2
+  if (argc > 2 && atoi(argv[2]) == 1) return 0;  // part 1 only
   const uint64_t sizes[] = {1024, 2048, 3000, 4096, 8192};
   fprintf(stderr, "part 2\n");
   printf("ceiling_probe part 2: uniform small buffers, 2 batches of >= 1 GiB rotated, %d reps\n", reps);

@@ -16,6 +16,8 @@
 #   small                  uniform small device batches (tools/small_batches.py)
 #   probe:<tool>:<args>    a built tools/<tool> binary (commas for spaces)
 #   py:<script>:<args>     python3 <script> <args> (commas for spaces)
+#   kt:<script>:<args>     the same under rocprofv3 --kernel-trace --stats
+#                          (csv under gpurun_out/<name>/kt<step>/)
 #   export:<VAR>=<value>   set an environment variable for the steps after it
 #   unset:<VAR>            remove it again
 set -o pipefail
@@ -58,6 +60,11 @@ for step in "$@"; do
       script=${arg%%:*}; pargs=${arg#*:}; [ "$pargs" = "$arg" ] && pargs=""
       # shellcheck disable=SC2086
       timeout -k 10 600 python3 -u "$script" ${pargs//,/ } > "$log" 2>&1 ;;
+    kt)
+      script=${arg%%:*}; pargs=${arg#*:}; [ "$pargs" = "$arg" ] && pargs=""
+      # shellcheck disable=SC2086
+      timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/kt$n" -o kt -- \
+        python3 -u "$script" ${pargs//,/ } > "$log" 2>&1 ;;
     export)
       export "${arg?}"; echo "    $arg" >> "$O/steps.txt"; continue ;;
     unset)

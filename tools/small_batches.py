@@ -11,7 +11,7 @@ calls (plans and launch gaps included; no per-launch events, which leave a
 ~10 us bubble before each launch: profiles/r03/s2).  Results of all four
 routes are compared.
 
-  python tools/small_batches.py [reps] [len,len,...] > out.jsonl
+  python tools/small_batches.py [reps] [len,len,... | len len ...] > out.jsonl
 """
 import json
 import os
@@ -26,7 +26,8 @@ import zipsfs_amd as z  # noqa: E402
 
 def main():
     reps = int(sys.argv[1]) if len(sys.argv) > 1 else 10
-    lengths = [int(x) for x in sys.argv[2].split(",")] if len(sys.argv) > 2 else [1024, 2048, 3000, 4096, 8192, 16384]
+    lengths = ([int(x) for a in sys.argv[2:] for x in a.split(",")] if len(sys.argv) > 2
+               else [1024, 2048, 3000, 4096, 8192, 16384])
     dev = "cuda:0"
     for L in lengths:
         n = (1 << 30) // L

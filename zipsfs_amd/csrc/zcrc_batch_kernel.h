@@ -547,7 +547,7 @@ __device__ void split_accumulate(const BatchArgs &a, uint64_t i, uint64_t n, uin
 // Process every piece of the byte range [S0, S1) of the concatenated batch
 // (S0, S1 snapped; `last_range` also takes the trailing empty buffers).
 // Returns the number of pieces.  Wave-uniform; no barriers.
-template <uint32_t kD, int kAblate, int kAux, bool kStamp, bool kPre = false, bool kProg = false>
+template <uint32_t kD, int kAblate, int kAux, bool kStamp, bool kPre = false, bool kProg = false, int kFold = 0>
 __device__ __forceinline__ uint32_t piece_raw(const uint32_t *s_lds, const uint8_t *bptr, uint64_t rel_lo,
                                               uint64_t rel_hi, uint32_t seed, uint32_t lane, uint64_t *t_tail,
                                               const uint4 *pre = nullptr);
@@ -749,7 +749,7 @@ __device__ __forceinline__ void piece_preload(const uint8_t *bptr, uint64_t rel_
 // kProg (per-buffer mode A/B): the wave's priority falls with its progress
 // through the piece, 3 in the first quarter of its groups .. 0 in the last,
 // so that waves behind issue first and the waves of a CU end together
-template <uint32_t kD, int kAblate, int kAux, bool kStamp, bool kPre, bool kProg>
+template <uint32_t kD, int kAblate, int kAux, bool kStamp, bool kPre, bool kProg, int kFold>
 __device__ __forceinline__ uint32_t piece_raw(const uint32_t *s_lds, const uint8_t *bptr, uint64_t rel_lo,
                                               uint64_t rel_hi, uint32_t seed, uint32_t lane, uint64_t *t_tail,
                                               const uint4 *pre) {
@@ -863,13 +863,31 @@ __device__ __forceinline__ uint32_t piece_raw(const uint32_t *s_lds, const uint8
     // ---- fold 256 stream registers into one raw register at `aend` -------
     // stream (lane l, dword q) sits at aend + 16 l + 4 q
     s0 ^= q0, s1 ^= q1, s2 ^= q2, s3 ^= q3;
+    if (kFold == 1) return uni32(s0 ^ s1 ^ s2 ^ s3);  // diagnostic (tools/ceiling_probe): no fold
     uint32_t r = (s0 ^ comb_apply(s_lds, 0, s1)) ^ comb_apply(s_lds, 1, s2 ^ comb_apply(s_lds, 0, s3));
     // cross-lane levels x^(-128 * 2^j): j < 4 inside 16-lane rows (DPP);
-    // the last two on the four row results, read into scalars
-    r ^= row_shl<1>(comb_apply(s_lds, 2, r));
-    r ^= row_shl<2>(comb_apply(s_lds, 3, r));
-    r ^= row_shl<4>(comb_apply(s_lds, 4, r));
-    r ^= row_shl<8>(comb_apply(s_lds, 5, r));
+    // the last two on the four row results, read into scalars.  kFold == 2
+    // (A/B): each level's lookups only in the lanes whose result the next
+    // level reads (lane 0 of each row ends with the row's fold)
+    if (kFold == 2) {
+      uint32_t t = 0;
+      if ((lane & 1u) == 1u) t = comb_apply(s_lds, 2, r);
+      r ^= row_shl<1>(t);
+      t = 0;
+      if ((lane & 3u) == 2u) t = comb_apply(s_lds, 3, r);
+      r ^= row_shl<2>(t);
+      t = 0;
+      if ((lane & 7u) == 4u) t = comb_apply(s_lds, 4, r);
+      r ^= row_shl<4>(t);
+      t = 0;
+      if ((lane & 15u) == 8u) t = comb_apply(s_lds, 5, r);
+      r ^= row_shl<8>(t);
+    } else {
+      r ^= row_shl<1>(comb_apply(s_lds, 2, r));
+      r ^= row_shl<2>(comb_apply(s_lds, 3, r));
+      r ^= row_shl<4>(comb_apply(s_lds, 4, r));
+      r ^= row_shl<8>(comb_apply(s_lds, 5, r));
+    }
     {
       const uint32_t r0 = uni32(r);
       const uint32_t r16 = (uint32_t)__builtin_amdgcn_readlane((int)r, 16);
@@ -891,9 +909,12 @@ __device__ __forceinline__ void small_body(const SmallArgs &a, uint32_t *s_lds, 
 
 // kPB: the per-buffer mode's form (fused only): 4 = round 4 (tables built in
 // registers, the decision after the work), 5 = the same with the first
-// payload loads issued before the table build, 7 = 5 with an LDS-only table
-// barrier (lds_barrier), 3 = round 3 (tables and lengths in front of the one
-// barrier); 3, 5 and 7 are A/B forms for tools/.
+// payload loads issued before the table build, 7 = 5 with the decision's
+// lengths loaded behind the preload, decided after the piece, and an
+// LDS-only table barrier (lds_barrier), 8 = 5 with the decision taken after
+// the piece (lengths loaded first), 9 = 8 with the lengths in four 16-B
+// buffer loads per thread, 3 = round 3 (tables and lengths in front of the
+// one barrier); 3, 5, 7, 8 and 9 are A/B forms for tools/.
 // kPB + 10: priority by progress through the buffer instead of by wave slot
 // (piece_raw kProg); kPB + 20: no priorities (A/B forms, tools/c2_probe).
 template <bool kStrided, uint32_t kD = kDepth, int kAblate = 0, bool kRotate = true, bool kStamp = false,
@@ -1007,7 +1028,19 @@ __global__ __launch_bounds__(kThreads) void crc32_batch_kernel(BatchArgs args) {
     // kPrioMode: 0 by slot, 1 by progress, 2 none; kDP: blocks per register
     // group in the per-buffer path (kPB + 100: 6, + 200: 8; two groups in flight)
     constexpr int kForm = kPB % 10, kPrioMode = (kPB / 10) % 10;
-    constexpr uint32_t kDP = (kPB / 100) == 1 ? 6u : (kPB / 100) == 2 ? 8u : kD;
+    constexpr uint32_t kDP = (kPB / 100) % 10 == 1 ? 6u : (kPB / 100) % 10 == 2 ? 8u : kD;
+    // kPB + 1000 / + 2000 (diagnostics for tools/ceiling_probe, with kAblate
+    // only: the results are wrong): no table build / no table build and no
+    // decision at the end; + 4000: + 2000 without the table barrier either;
+    // + 5000: + 4000 without the fold; kPB + 3000: no decision lengths (the
+    // end barriers kept; right only when no buffer exceeds kPerBufMax)
+    constexpr int kDiag = kPB / 1000;
+    constexpr bool kNoTab = kDiag == 1 || kDiag == 2 || kDiag == 4 || kDiag == 5;
+    constexpr bool kNoEnd = kDiag == 2 || kDiag == 4 || kDiag == 5;
+    constexpr bool kNoLens = kDiag >= 2 && kDiag != 6, kNoBar = kDiag == 4 || kDiag == 5;
+    // kPB + 6000 (A/B): the fold's lane levels masked to the lanes read next
+    constexpr int kFoldMode = kDiag == 5 ? 1 : kDiag == 6 ? 2 : 0;
+    static_assert(!kNoTab || kAblate, "the table-less diagnostic forms are read-ceiling variants");
     if (kForm >= 4 && args.n <= (uint64_t)grid * kWaves) {
       // Round 4: nothing in front of the payload waits on memory but the
       // wave's own descriptor.  The braid and combine tables are built in
@@ -1032,27 +1065,41 @@ __global__ __launch_bounds__(kThreads) void crc32_batch_kernel(BatchArgs args) {
       }
       uint64_t L[8];  // the decision's lengths (thread t: buffers t + 1024 j), clamped, unguarded
       auto load_lens = [&]() {
+        if (kForm == 9) {
+          // form 9: four 16-B buffer loads over [lens, lens + n) (thread t:
+          // buffers 2 t + 2048 j and the next), past the end zeros -- no
+          // clamped duplicates, half the load instructions
+          const __amdgpu_buffer_rsrc_t lr =
+              __builtin_amdgcn_make_buffer_rsrc((void *)args.lens, (short)0, (int)(8u * args.n), 0x00020000);
+#pragma unroll
+          for (uint32_t j = 0; j < 4; j++) {
+            auto v = __builtin_amdgcn_raw_buffer_load_b128(lr, 16u * tid + 16384u * j, 0, 0);
+            L[2 * j] = (uint64_t)v[0] | ((uint64_t)v[1] << 32);
+            L[2 * j + 1] = (uint64_t)v[2] | ((uint64_t)v[3] << 32);
+          }
+          return;
+        }
 #pragma unroll
         for (uint32_t j = 0; j < 8; j++) {
           const uint64_t idx = tid + 1024u * j;
           L[j] = args.lens[idx < args.n ? idx : args.n - 1];
         }
       };
-      if (kForm < 7) load_lens();
+      if ((kForm < 7 || kForm >= 8) && !kNoLens) load_lens();
       const bool own = b < args.n && blen <= kPerBufMax;  // wave-uniform
       const uint8_t *bptr = reinterpret_cast<const uint8_t *>(bp);
       uint4 pre[2 * kDP];
       // kPB >= 5: the first payload loads go out as soon as the descriptor is
       // in, ahead of the table build (A/B form)
       if (kForm >= 5) piece_preload<kDP, kAux>(bptr, 0, blen, lane, own && blen >= 4, pre);
-      if (kForm >= 7) {
-        // form >= 7: the decision's lengths behind the preload, so that the
+      if (kForm == 7 && !kNoLens) {
+        // form 7: the decision's lengths behind the preload, so that the
         // first group's wait (vmcnt, counted in issue order) is not a wait for
         // them too
         __builtin_amdgcn_sched_barrier(0);
         load_lens();
       }
-      if (wg_busy) {
+      if (wg_busy && !kNoTab) {
         const uint32_t e = braid_gen_lane(lane, slot);
         uint4 *dst = reinterpret_cast<uint4 *>(s_lds);
 #pragma unroll
@@ -1068,22 +1115,26 @@ __global__ __launch_bounds__(kThreads) void crc32_batch_kernel(BatchArgs args) {
         cdst[tid + 1024u] = cm1;
       }
       const uint64_t t_lens = kStamp ? __builtin_amdgcn_s_memrealtime() : 0;  // diagnostic: tables written
-      // the tables are in LDS (form >= 7: an LDS-only barrier, the decision
+      // the tables are in LDS (form 7: an LDS-only barrier, the decision
       // lengths and the preloads may still be in flight)
-      if (kForm >= 7) lds_barrier();
-      else __syncthreads();
+      if (kNoBar) {
+      } else if (kForm == 7) {
+        lds_barrier();
+      } else {
+        __syncthreads();
+      }
       const uint64_t t_fill = kStamp ? __builtin_amdgcn_s_memrealtime() : 0;
       if (kForm < 5) piece_preload<kDP, kAux>(bptr, 0, blen, lane, own && blen >= 4, pre);
       // the decision over the lengths L: forms < 7 here, where the compiler
-      // hoisted it (and the waits for L) in front of the table barrier; form
-      // >= 7 after the wave's piece, when L has long arrived
+      // hoisted it (and the waits for L) in front of the table barrier; forms
+      // 7 and 8 after the wave's piece, when L has long arrived
       auto decide = [&]() -> uint32_t {
         bool big = false;
 #pragma unroll
-        for (uint32_t j = 0; j < 8; j++) big |= (tid + 1024u * j < args.n) & (L[j] > kPerBufMax);
+        for (uint32_t j = 0; j < 8; j++) big |= (kForm == 9 || tid + 1024u * j < args.n) & (L[j] > kPerBufMax);
         return __ballot(big) ? 1u : 0u;
       };
-      uint32_t any_big = kForm >= 7 ? 0u : decide();
+      uint32_t any_big = (kForm >= 7 || kNoLens) ? 0u : decide();
       if (own) {
         // younger wave slots issue first (the round-3 per-buffer form below)
         if (kPrioMode == 0) {
@@ -1098,8 +1149,8 @@ __global__ __launch_bounds__(kThreads) void crc32_batch_kernel(BatchArgs args) {
           r = ~bseed;
           for (uint32_t p = 0; p < (uint32_t)blen; p++) r = (r >> 8) ^ tab->stdtab[(r ^ bptr[p]) & 0xFFu];
         } else {
-          r = piece_raw<kDP, kAblate, kAux, false, true, kPrioMode == 1>(s_lds, bptr, 0, blen, bseed, lane, nullptr,
-                                                                        pre);
+          r = piece_raw<kDP, kAblate, kAux, false, true, kPrioMode == 1, kFoldMode>(s_lds, bptr, 0, blen, bseed, lane,
+                                                                                 nullptr, pre);
         }
         if (lane == 0) args.out[b] = ~r;
         if (kStamp && lane == 0) {  // diagnostic build (tools/c2_probe): this wave's timeline
@@ -1112,7 +1163,8 @@ __global__ __launch_bounds__(kThreads) void crc32_batch_kernel(BatchArgs args) {
         }
         if (kPrioMode == 1) __builtin_amdgcn_s_setprio(0);
       }
-      if (kForm >= 7) any_big = decide();
+      if (kNoEnd) return;
+      if (kForm >= 7 && !kNoLens) any_big = decide();
       __syncthreads();  // every wave is done with the tables: the LDS is free
       if (lane == 0) s_lds[slot] = any_big;
       __syncthreads();
