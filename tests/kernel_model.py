@@ -120,6 +120,7 @@ class Tables:
     def __init__(self):
         self.braid = mct(xpow8(1024))
         self.braid256 = mct(xpow8(256))  # the small-buffer kernel's table
+        self.braid128 = mct(xpow8(128))  # its table for 128-B blocks (8 lanes)
         self.comb = [mct(xinvpow8(b)) for b in (4, 8, 16, 32, 64, 128, 256, 512)]
         self.tshift = [mct(xinvpow8(t)) for t in range(16)]
         # r * x^-8 = (r << 8) ^ xinv8[r >> 24] (zcrc_gf2.h build_xinv8_table)
@@ -402,29 +403,30 @@ def run_one_launch(batch: Batch, num_cus: int = 256) -> np.ndarray:
 # ------------------------------------------------------------ small-buffer kernel
 
 def crc_small_group(mem: np.ndarray, pstart: int, length: int, seed: int, G: int, T: Tables,
-                    extra_blocks: int = 0) -> int:
-    """zcrc_small_kernel.h small_body for one buffer: G lanes, 256-B blocks,
-    C = 16/G chunks per lane, end-aligned; `extra_blocks` leading blocks that
-    load nothing (the wave runs its largest buffer's block count)."""
+                    extra_blocks: int = 0, blk: int = 256) -> int:
+    """zcrc_small_kernel.h small_body for one buffer: G lanes, `blk`-byte
+    blocks (256: MCT(x^2048); 128: MCT(x^1024), the product's 8-lane form),
+    C = blk/16/G chunks per lane, end-aligned; `extra_blocks` leading blocks
+    that load nothing (the wave runs its largest buffer's block count)."""
     if length < 4:
         r = (~seed) & 0xFFFFFFFF
         for p in range(length):
             r = (r >> 8) ^ int(T.stdtab[(r ^ int(mem[pstart + p])) & 0xFF])
         return (~r) & 0xFFFFFFFF
-    C = 16 // G
+    C = blk // 16 // G
     astart = pstart & ~15
     rs = pstart - astart
     re = rs + length
     span = (re + 15) & ~15
-    K = (span + 255) >> 8
+    K = (span + blk - 1) // blk
     kmax = K + extra_blocks
     inj = (~seed) & 0xFFFFFFFF
     lanes = np.arange(G, dtype=np.int64)
     s = np.zeros((G, 4 * C), dtype=np.uint32)
-    rel0 = span - 256 * kmax + 16 * C * lanes
+    rel0 = span - blk * kmax + 16 * C * lanes
     for k in range(kmax):
         for c in range(C):
-            rel = rel0 + 256 * k + 16 * c
+            rel = rel0 + blk * k + 16 * c
             data = np.zeros((G, 16), dtype=np.uint8)
             for l in range(G):
                 if rel[l] >= 0:
@@ -438,7 +440,7 @@ def crc_small_group(mem: np.ndarray, pstart: int, length: int, seed: int, G: int
                 fixed = ((words[:, q] & m) ^ _inj_word(inj, lo - 4 * q)) & np.uint64(0xFFFFFFFF)
                 words[:, q] = np.where(edge, fixed, words[:, q])
             x = (s[:, 4 * c:4 * c + 4].astype(np.uint64) ^ words).astype(np.uint32)
-            s[:, 4 * c:4 * c + 4] = mct_apply(T.braid256, x)
+            s[:, 4 * c:4 * c + 4] = mct_apply(T.braid256 if blk == 256 else T.braid128, x)
     ns = 4 * C
     v = [s[:, m].copy() for m in range(ns)]
     t = 0

@@ -158,21 +158,22 @@ def test_device_search_and_first_buffer(shape):
 
 # ------------------------------------------------------------ small-buffer kernel model
 
-@pytest.mark.parametrize("G", [16, 8])
-def test_small_group_model_matches_oracle(G):
-    """The small body's algebra (256-B blocks on MCT(x^2048), end alignment,
-    in-lane and cross-lane folds, padding undone) reproduces zlib's CRC for
-    every length 0..600 and the block boundaries, at every 16-B misalignment
-    of a sample, with seeds and with extra leading empty blocks."""
+@pytest.mark.parametrize("G,blk", [(16, 256), (8, 256), (8, 128)])
+def test_small_group_model_matches_oracle(G, blk):
+    """The small body's algebra (256-B blocks on MCT(x^2048), or the 8-lane
+    form's 128-B blocks on MCT(x^1024); end alignment, in-lane and cross-lane
+    folds, padding undone) reproduces zlib's CRC for every length 0..600 and
+    the block boundaries, at every 16-B misalignment of a sample, with seeds
+    and with extra leading empty blocks."""
     T = km.tables()
-    rng = np.random.default_rng(G)
+    rng = np.random.default_rng(G + blk)
     mem = rng.integers(0, 256, 9000 + 64, dtype=np.uint8)
     lengths = list(range(0, 601, 7)) + [255, 256, 257, 511, 512, 1023, 1024, 1025, 2048, 4095, 4096, 8191, 8192]
     for L in lengths:
         for off in (0, 3, 13):
             seed = int(rng.integers(0, 2**32)) if L % 3 else 0
-            got = km.crc_small_group(mem, 16 + off, L, seed, G, T, extra_blocks=L % 2)
-            assert got == zlib.crc32(mem[16 + off:16 + off + L].tobytes(), seed), (L, off, G)
+            got = km.crc_small_group(mem, 16 + off, L, seed, G, T, extra_blocks=L % 2, blk=blk)
+            assert got == zlib.crc32(mem[16 + off:16 + off + L].tobytes(), seed), (L, off, G, blk)
 
 
 def test_split_plan_model_lists():

@@ -27,7 +27,7 @@
 //             loads; fm = the fold's lane levels masked to the lanes read
 //             next; results compared with crc's
 // (Round-5 sessions 9-13 also measured forms 17 and the slot priorities of
-// form 5 in the ablated kernel: profiles/r05/s13.)
+// form 5 in the ablated kernel: profiles/r05/c2_bisect/.)
 // Part 2, uniform small buffers (1024, 2048, 3000, 4096, 8192 B; >= 1 GiB
 // per batch, two batches rotated), whole buffers in the small body's lane
 // mapping (zcrc_small_kernel.h: G lanes per buffer, 256-B blocks, lane l of
@@ -36,16 +36,21 @@
 //   read-G8/G16  pure reads with the product's descriptor loads
 //   read-G8c     the same, 8 lanes, with lane l reading the chunks at 16 l and
 //                16 l + 128 (each load covers 128 contiguous bytes per buffer)
-//   crc          the product's small kernel (the split plan's direct mode
-//                runs the same body inside the batch kernel)
-//   crc-G8c/G16/G8  the small kernel in those layouts, results compared with
-//                crc's
-// (Round-5 session 4 also measured G4 layouts, strided addressing and a
-// software-pipelined body: all slower; profiles/r05/s4/ceiling_probe.txt.)
+//   crc          the product's small kernel (8 lanes on 128-B blocks up to
+//                2 KiB, else 16 lanes on 256-B blocks; the split plan's
+//                direct mode runs the same body inside the batch kernel)
+//   crc-G8c/G16  8 lanes on 256-B blocks (coalesced), 16 lanes; crc-str:
+//                the product's form with strided addressing (the strided
+//                API); crc-G8cp: G8c with the pipelined walk (small_pipe);
+//                results compared with crc's
+// (Round-5 sessions 16-18 also measured the pipelined 16-lane walk, 8 lanes
+// on 128-B blocks with 4 blocks in flight, and the bodies without lookups or
+// without the fold: profiles/r05/s15_s20/, DESIGN.md 7e.  Session 4 measured G4
+// layouts and strided addressing of the pure reads.)
 // Every launch is timed by its own dispatch packet (hipExtLaunchKernelGGL
 // events); the figures are averages over the launches, in GB/s of payload.
 //
-//   make -C tools ceiling_probe && tools/ceiling_probe [reps [1: part 1 only]]
+//   make -C tools ceiling_probe && tools/ceiling_probe [reps [1: part 1 only | 2: part 2 only]]
 #include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -303,7 +308,7 @@ int main(int argc, char **argv) {
   };
 
   // ---------------------------------------------------------------- part 1
-  {
+  if (!(argc > 2 && atoi(argv[2]) == 2)) {  // (2: part 2 only)
     uint8_t *data;
     CHECK(hipMalloc(&data, kBatchBytes * kBatches));
     std::vector<uint64_t> hp(kN * kBatches), hl(kN * kBatches, kLen);
@@ -424,24 +429,43 @@ int main(int argc, char **argv) {
     CHECK(hipMemcpy(dl, hl.data(), 16 * n, hipMemcpyHostToDevice));
     CHECK(launch_fill_synthetic(dp, dl, 2 * n, 0, 1, 0xC0FFEE, 0));
     CHECK(hipDeviceSynchronize());
-    const char *names[] = {"read-G8", "read-G16", "read-G8c", "crc", "crc-G8c", "crc-G16", "crc-G8"};
-    constexpr int kV = 7;
+    const char *names[] = {"read-G8", "read-G16", "read-G8c", "crc", "crc-G8c", "crc-G16", "crc-str", "crc-G8cp"};
+    constexpr int kV = 8, kCmp = 8;  // forms below kCmp: results compared with crc's
     std::vector<std::vector<double>> t(kV);
     const int lanes = L <= 2048 ? 8 : 16;  // the product's choice (small_lanes)
-    auto crc_launch = [&](int v, const uint64_t *p, const uint64_t *l, uint32_t *o, hipEvent_t a, hipEvent_t z) {
+    auto crc_launch = [&](int v, const uint64_t *p, const uint64_t *l, const uint8_t *base, uint32_t *o, hipEvent_t a,
+                          hipEvent_t z) {
       SmallArgs sa{};
       sa.ptrs = reinterpret_cast<const uint8_t *const *>(p);
       sa.lens = l;
       sa.n = n;
       sa.tab = d_tab;
       sa.out = o;
-      const int form = v == 3 ? (lanes == 8 ? 6 : 5) : v;  // 4: G8c, 5: G16, 6: G8
+      // 3 ("crc"): the product's form (8 lanes on 128-B blocks up to 2 KiB,
+      // else 16 on 256-B blocks); 4: 8 lanes on 256-B blocks, coalesced; 5:
+      // 16 lanes; 6: the product's form, strided addressing; 7: 4 with the
+      // pipelined walk
+      if (v == 6) {
+        sa.base = base;
+        sa.stride = stride;
+        sa.len = L;
+        if (lanes == 8)
+          hipExtLaunchKernelGGL((crc32_small_kernel<true, 8, 8, false, false, 0, 128>), dim3(cus), dim3(1024), 0, 0, a,
+                                z, 0, sa);
+        else
+          hipExtLaunchKernelGGL((crc32_small_kernel<true, 16, 8>), dim3(cus), dim3(1024), 0, 0, a, z, 0, sa);
+        return;
+      }
+      const int form = v == 3 ? (lanes == 8 ? 8 : 5) : v;
       if (form == 4)
         hipExtLaunchKernelGGL((crc32_small_kernel<false, 8, 4, true>), dim3(cus), dim3(1024), 0, 0, a, z, 0, sa);
       else if (form == 5)
         hipExtLaunchKernelGGL((crc32_small_kernel<false, 16, 8>), dim3(cus), dim3(1024), 0, 0, a, z, 0, sa);
+      else if (form == 7)
+        hipExtLaunchKernelGGL((crc32_small_kernel<false, 8, 4, true, true>), dim3(cus), dim3(1024), 0, 0, a, z, 0, sa);
       else
-        hipExtLaunchKernelGGL((crc32_small_kernel<false, 8, 4>), dim3(cus), dim3(1024), 0, 0, a, z, 0, sa);
+        hipExtLaunchKernelGGL((crc32_small_kernel<false, 8, 8, false, false, 0, 128>), dim3(cus), dim3(1024), 0, 0, a,
+                              z, 0, sa);
     };
     for (int r = 0; r < reps; r++)
       for (int v = 0; v < kV; v++)
@@ -452,7 +476,7 @@ int main(int argc, char **argv) {
             case 0: hipExtLaunchKernelGGL((k_small_read<8, 4, true>), dim3(cus), dim3(1024), 0, 0, a, z, 0, p, l, base, stride, L, n, out); break;
             case 1: hipExtLaunchKernelGGL((k_small_read<16, 8, true>), dim3(cus), dim3(1024), 0, 0, a, z, 0, p, l, base, stride, L, n, out); break;
             case 2: hipExtLaunchKernelGGL((k_small_read<8, 4, true, true>), dim3(cus), dim3(1024), 0, 0, a, z, 0, p, l, base, stride, L, n, out); break;
-            default: crc_launch(v, p, l, v == 3 ? o1 : o2, a, z);
+            default: crc_launch(v, p, l, base, v == 3 ? o1 : o2, a, z);
           }
         }, t[v]);
     printf("  L %5llu  n %8llu per batch\n", (unsigned long long)L, (unsigned long long)n);
@@ -466,9 +490,9 @@ int main(int argc, char **argv) {
     {  // every CRC form against "crc" (whose last launch ran batch 1), on batch 1
       std::vector<uint32_t> h1(n), h2(n);
       CHECK(hipMemcpy(h1.data(), o1, 4 * n, hipMemcpyDeviceToHost));
-      for (int v = 4; v < kV; v++) {
+      for (int v = 4; v < kCmp; v++) {
         CHECK(hipMemset(o2, 0, 4 * n));
-        crc_launch(v, dp + n, dl + n, o2, ev[0], ev[1]);
+        crc_launch(v, dp + n, dl + n, data + n * stride, o2, ev[0], ev[1]);
         CHECK(hipDeviceSynchronize());
         CHECK(hipMemcpy(h2.data(), o2, 4 * n, hipMemcpyDeviceToHost));
         uint64_t bad = 0;

@@ -26,6 +26,11 @@ NAME=${1:?usage: session.sh <name> <step>...}
 shift
 O=gpurun_out/$NAME
 mkdir -p "$O"
+# heartbeat: a slow but healthy step (the first import torch on a fresh box,
+# a quiet test) must not read as a hang; every step keeps its own time limit
+( while sleep 30; do date +%T >> "$O/heartbeat"; done ) &
+HB=$!
+trap 'kill $HB 2>/dev/null' EXIT
 n=0
 for step in "$@"; do
   n=$((n + 1))
@@ -40,7 +45,7 @@ for step in "$@"; do
         timeout -k 10 900 python3 -u -m pytest tests -m gpu -x -v -rP --timeout 300 --timeout-method thread \
           -k "$arg" > "$log" 2>&1
       else
-        timeout -k 10 900 python3 -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread \
+        timeout -k 10 900 python3 -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread \
           > "$log" 2>&1
       fi ;;
     smoke)

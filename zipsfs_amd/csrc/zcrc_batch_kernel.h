@@ -903,7 +903,7 @@ __device__ __forceinline__ uint32_t piece_raw(const uint32_t *s_lds, const uint8
 }
 
 // zcrc_small_kernel.h (included at the end of this header)
-template <bool kStrided, int G, int kD, int kAblate, bool kCoal = false>
+template <bool kStrided, int G, int kD, int kAblate, bool kCoal = false, bool kPipe = false, int kBlk = 256>
 __device__ __forceinline__ void small_body(const SmallArgs &a, uint32_t *s_lds, uint64_t n, uint32_t blk,
                                            uint32_t nblk);
 
@@ -941,7 +941,7 @@ __global__ __launch_bounds__(kThreads) void crc32_batch_kernel(BatchArgs args) {
         const uint64_t ns = uni64(args.n_dev[1]);
         const uint32_t blk = blockIdx.x - (gridDim.x - nsm);
         const uint64_t t_small = kStamp ? __builtin_amdgcn_s_memrealtime() : 0;
-        if (uni64(args.n_dev[3]) == 8) small_body<false, 8, 4, kAblate, true>(sa, s_lds, ns, blk, nsm);
+        if (uni64(args.n_dev[3]) == 8) small_body<false, 8, 8, kAblate, false, false, 128>(sa, s_lds, ns, blk, nsm);
         else small_body<false, 16, 8, kAblate>(sa, s_lds, ns, blk, nsm);
         if (kStamp && (threadIdx.x & 63u) == 0) {  // diagnostic build: a small-list wave (npieces ~0)
           const uint64_t w = (uint64_t)blockIdx.x * kWaves + (threadIdx.x >> 6);

@@ -32,7 +32,7 @@ constexpr uint64_t kPlanTile = 1024 * kPlanPerThread;
 // one launch covers at most this many bytes (keeps every piece < 2 GiB)
 constexpr uint64_t kMaxLaunchBytes = 1ull << 42;
 
-// Multiply-by-constant tables, uploaded once per device (~106 KiB).
+// Multiply-by-constant tables, uploaded once per device (~110 KiB).
 struct TableBlob {
   uint32_t braid[4 * 256];       // MCT(x^(8*1024)): the hot-loop table
   uint32_t comb[8 * 4 * 256];    // x^-32, x^-64, x^-128 .. x^-4096 (combine tree)
@@ -42,6 +42,7 @@ struct TableBlob {
   uint32_t braid256[4 * 256];    // MCT(x^(8*256)): the small-buffer kernel's table
   uint32_t xinv8[256];           // r * x^-8 = (r << 8) ^ xinv8[r >> 24] (one zero byte taken off)
   uint32_t x8grain[4][256];      // x^(8 * 65536 * m * 256^j): a split piece's shift by whole 64 KiB grains
+  uint32_t braid128[4 * 256];    // MCT(x^(8*128)): the small-buffer kernel's table for 128-B blocks
 };
 
 struct BatchArgs {

@@ -461,21 +461,25 @@ const char *product_kernel_name() {
   return name;
 }
 
-// Small whole buffers: 16 lanes per buffer with 8 blocks in flight, or 8
-// lanes with 4 (same 32 VGPRs of loads, twice the buffers: pays below ~2 KiB)
-// in the coalesced layout (round 5: 1 KiB 5.08 -> 5.45 TB/s, 2 KiB 5.29 ->
-// 5.92, tools/ceiling_probe, profiles/r05/s6).
+// Small whole buffers: 16 lanes per buffer on 256-B blocks with 8 blocks in
+// flight, or 8 lanes (twice the buffers: pays below ~2 KiB) on 128-B blocks
+// with 8 in flight -- the same 32 VGPRs of loads, one 16-B chunk a lane and
+// block, so 4 streams a lane and a 6-step fold instead of the 10 of 256-B
+// blocks (round 5: 1 KiB 190.4 -> 183.5 us per GiB batch, 2 KiB 173.3 ->
+// 171.9, same process, bit-exact; tools/ceiling_probe, profiles/r05/s15_s20/s18_ceiling_probe.txt).
 hipError_t launch_small(const SmallArgs &args, bool strided, int lanes, int num_cus, hipStream_t stream,
                         hipEvent_t t0, hipEvent_t t1) {
   const dim3 grid((unsigned)num_cus), block(kThreads);
   if (strided) {
     if (lanes == 8)
-      hipExtLaunchKernelGGL((crc32_small_kernel<true, 8, 4, true>), grid, block, 0, stream, t0, t1, 0, args);
+      hipExtLaunchKernelGGL((crc32_small_kernel<true, 8, 8, false, false, 0, 128>), grid, block, 0, stream, t0, t1, 0,
+                            args);
     else
       hipExtLaunchKernelGGL((crc32_small_kernel<true, 16, 8>), grid, block, 0, stream, t0, t1, 0, args);
   } else {
     if (lanes == 8)
-      hipExtLaunchKernelGGL((crc32_small_kernel<false, 8, 4, true>), grid, block, 0, stream, t0, t1, 0, args);
+      hipExtLaunchKernelGGL((crc32_small_kernel<false, 8, 8, false, false, 0, 128>), grid, block, 0, stream, t0, t1, 0,
+                            args);
     else
       hipExtLaunchKernelGGL((crc32_small_kernel<false, 16, 8>), grid, block, 0, stream, t0, t1, 0, args);
   }
@@ -495,7 +499,8 @@ const char *fused_kernel_name() {
 
 // the general-form small kernels as rocprofv3 names them
 const char *small_kernel_name(int lanes) {
-  return lanes == 8 ? "zcrc::crc32_small_kernel<false, 8, 4, true>" : "zcrc::crc32_small_kernel<false, 16, 8, false>";
+  return lanes == 8 ? "zcrc::crc32_small_kernel<false, 8, 8, false, false, 0, 128>"
+                    : "zcrc::crc32_small_kernel<false, 16, 8, false, false, 0, 256>";
 }
 
 hipError_t launch_plan(const uint64_t *d_lens, uint64_t n, uint64_t *d_prefix, uint64_t *d_tile_sum,

@@ -39,6 +39,233 @@ typedef unsigned int small_v4u __attribute__((ext_vector_type(4)));
 // chunk of the combine area where the x^-8 byte table goes (table 7's)
 constexpr uint32_t kXinv8Chunk = 7u * 256u;
 
+// 16-B non-temporal load through the global address space: global_load
+// (a flat load also counts in lgkmcnt, so every wait for an LDS lookup
+// waited for the payload loads still in flight as well)
+typedef const __attribute__((address_space(1))) small_v4u *small_gptr;
+__device__ __forceinline__ small_v4u small_gload(uint64_t addr) {
+  return __builtin_nontemporal_load(reinterpret_cast<small_gptr>(addr));
+}
+
+// A group's buffer as the pipelined walk sees it (per lane; nch wave-uniform).
+// The buffer is [astart + rs, astart + re); span = re rounded up to 16.
+struct SmallGeo {
+  uint64_t astart;  // 16-B aligned (a valid dummy when there is no byte to load)
+  int32_t rs, re, rel0;
+  uint32_t seed, j;  // j: the result index (split-plan lists only; else from the group index)
+  uint32_t nch;
+  bool active;
+};
+
+// Round 5: the pipelined walk (kPipe).  The small body above loads a group's
+// blocks, waits for all of them, runs its braid steps and fold and only then
+// loads the next group: every wave alternates between memory and compute, and
+// a 1 KiB batch read at 0.82 of the same mapping's pure read
+// (tools/ceiling_probe part 2).  Here a group's blocks go in chunks of H =
+// kD / 2 blocks through two register sets: the loads of chunk i + 2 -- of the
+// same group or of the next one -- are issued as soon as chunk i is consumed,
+// so kD blocks stay in flight through the braid steps and the fold.  Every
+// group has an even number of chunks, at least two (kmax rounded up; the
+// extra leading blocks are zeros in the raw domain), so a group starts in the
+// first register set and the chunk two ahead is at most one group ahead;
+// descriptors are loaded two groups ahead.  Loads are unconditional
+// (clamped into the buffer's own 16-B granules, or a dummy address for lanes
+// with nothing to load, the data zeroed afterwards), so that the waits for
+// them stay counted ones.
+// kDM: where the descriptors come from -- 0 strided, 1 pointer and length
+// arrays, 2 pointers and a prefix, 3 the split plan's 16-B list entries.
+template <int kDM, int G, int kD, int kAblate, bool kCoal>
+__device__ __forceinline__ void small_pipe(const SmallArgs &a, const uint32_t *s_lds, uint64_t n, uint32_t blk,
+                                           uint32_t nblk) {
+  constexpr int C = 16 / G, NS = 4 * C, LOG_NS = NS == 4 ? 2 : 3, LOG_G = G == 8 ? 3 : 4;
+  constexpr uint32_t BPW = 64 / G, H = kD / 2;
+  static_assert(kD % 2 == 0 && H >= 1, "two chunks of kD / 2 blocks");
+  const uint32_t tid = threadIdx.x, lane = tid & 63u, g = lane / G, lg = lane % G;
+  const uint64_t waves = (uint64_t)nblk * kWaves;
+  const uint64_t nq = (n + BPW - 1) / BPW;
+  uint64_t qc = uni64((uint64_t)blk * kWaves + (tid >> 6));  // wave-uniform: scalar loop control
+  if (qc >= nq) return;
+  constexpr int32_t kLaneStep = kCoal ? 16 : 16 * C, kChunkStep = kCoal ? 16 * G : 16;
+  const uint32_t lo0 = (lane & 31u) * 4u;
+  const uint32_t o0 = lo0, o1 = lo0 + 128u, o2 = lo0 + 65536u, o3 = lo0 + 65536u + 128u;
+  const uint64_t dummy = reinterpret_cast<uint64_t>(a.tab) & ~15ull;
+
+  // descriptor of list entry k: clamped, and every load unconditional and
+  // nothing computed from it here (a branch around a load, or a value
+  // computed from one, made the compiler wait for the loads at once -- the
+  // descriptor of the group after next then stalled the pipeline)
+  constexpr bool kSd = kDM == 3;
+  const uint32_t *const zero32 = &a.tab->stdtab[0];  // CRC table entry 0: zero
+  struct Desc {
+    uint64_t p;
+    uint32_t l1, l0, j, sd;  // lengths: the low words (small buffers; a dead high word's register was
+                             // reused while its load was in flight, behind a wait for every load)
+    bool act;
+  };
+  auto load_desc = [&](uint64_t k) -> Desc {
+    Desc d;
+    d.act = k < n;
+    const uint64_t kc = d.act ? k : n - 1;
+    d.j = 0;
+    d.l0 = 0;
+    d.sd = *(a.seeds ? a.seeds + kc : zero32);
+    if (kDM == 0) {
+      d.p = reinterpret_cast<uint64_t>(a.base) + kc * a.stride;
+      d.l1 = (uint32_t)a.len;
+    } else if (kDM == 3) {  // pointer | length << 48, index, seed in one 16-B load
+      const uint4 v = a.sdesc[kc];
+      d.p = (uint64_t)v.x | ((uint64_t)v.y << 32);
+      d.l1 = 0;
+      d.j = v.z;
+      d.sd = v.w;
+    } else {
+      d.p = reinterpret_cast<uint64_t>(a.ptrs[kc]);
+      d.l1 = *reinterpret_cast<const uint32_t *>(kDM == 1 ? a.lens + kc : a.prefix + kc + 1);
+      if (kDM == 2) d.l0 = *reinterpret_cast<const uint32_t *>(a.prefix + kc);  // the difference mod 2^32
+    }
+    return d;
+  };
+  auto make_geo = [&](const Desc &d) -> SmallGeo {
+    SmallGeo e;
+    uint64_t p = d.p;
+    uint32_t l = d.l1 - d.l0;
+    if (kSd) l = (uint32_t)(p >> 48), p &= 0xFFFFFFFFFFFFull;
+    e.active = d.act;
+    e.j = d.j;
+    e.seed = d.sd;
+    const uint32_t len = d.act ? l : 0u;
+    const bool ld = len >= 4u;  // below 4 bytes: bytewise (the seed injection needs 4)
+    // a buffer with a byte keeps its own granules (tiny ones: read bytewise
+    // from astart + rs), an empty or absent one loads from the dummy
+    const uint64_t ps = len ? p : dummy;
+    e.astart = ps & ~15ull;
+    e.rs = (int32_t)(ps & 15u);
+    e.re = e.rs + (int32_t)len;
+    const int32_t span = (e.re + 15) & ~15;
+    const uint32_t kq = ld ? (uint32_t)(span + 255) >> 8 : 0u;
+    const uint32_t kmax = uni32(__reduce_max_sync(0xFFFFFFFFFFFFFFFFull, kq));
+    const uint32_t ke = kmax <= 2 * H ? 2 * H : (kmax + 2 * H - 1) / (2 * H) * (2 * H);  // an even chunk count
+    e.nch = ke / H;
+    e.rel0 = ld ? span - 256 * (int32_t)ke + kLaneStep * (int32_t)lg : -(1 << 30);
+    return e;
+  };
+  typedef small_v4u Chunk[H][C];
+  auto issue = [&](uint64_t astart, int32_t rel0, uint32_t ch, Chunk &X) {
+#pragma unroll
+    for (uint32_t b = 0; b < H; b++)
+#pragma unroll
+      for (int c = 0; c < C; c++) {
+        const int32_t rel = rel0 + 256 * (int32_t)(ch * H + b) + kChunkStep * c;
+        X[b][c] = small_gload(astart + (uint32_t)(rel >= 0 ? rel : 0));
+      }
+  };
+  constexpr bool kQ = true;  // braid_step2 (s ^ q); one word (braid_step) spilled more
+  uint32_t s[NS], q[NS];
+#pragma unroll
+  for (int t = 0; t < NS; t++) s[t] = 0u, q[t] = 0u;
+  auto consume = [&](const SmallGeo &e, uint32_t ch, const Chunk &X) {
+#pragma unroll
+    for (uint32_t b = 0; b < H; b++)
+#pragma unroll
+      for (int c = 0; c < C; c++) {
+        const int32_t rel = e.rel0 + 256 * (int32_t)(ch * H + b) + kChunkStep * c;
+        uint4 w = rel >= 0 ? make_uint4(X[b][c].x, X[b][c].y, X[b][c].z, X[b][c].w) : make_uint4(0, 0, 0, 0);
+        if (rel >= 0 && (rel < e.rs + 4 || rel + 16 > e.re))
+          w = fix_chunk(w, clamp_rel(e.rs - rel), clamp_rel(e.re - rel), clamp_rel(e.rs - rel), ~e.seed);
+        if (kAblate == 1) {
+          s[4 * c + 0] = __builtin_amdgcn_alignbit(s[4 * c + 0] ^ w.x, s[4 * c + 0] ^ w.x, 5);
+          s[4 * c + 1] = __builtin_amdgcn_alignbit(s[4 * c + 1] ^ w.y, s[4 * c + 1] ^ w.y, 5);
+          s[4 * c + 2] = __builtin_amdgcn_alignbit(s[4 * c + 2] ^ w.z, s[4 * c + 2] ^ w.z, 5);
+          s[4 * c + 3] = __builtin_amdgcn_alignbit(s[4 * c + 3] ^ w.w, s[4 * c + 3] ^ w.w, 5);
+        } else if (kQ) {
+          braid_step2(s_lds, s[4 * c + 0], q[4 * c + 0], w.x, o0, o1, o2, o3);
+          braid_step2(s_lds, s[4 * c + 1], q[4 * c + 1], w.y, o0, o1, o2, o3);
+          braid_step2(s_lds, s[4 * c + 2], q[4 * c + 2], w.z, o0, o1, o2, o3);
+          braid_step2(s_lds, s[4 * c + 3], q[4 * c + 3], w.w, o0, o1, o2, o3);
+        } else {
+          s[4 * c + 0] = braid_step(s_lds, s[4 * c + 0] ^ w.x, o0, o1, o2, o3);
+          s[4 * c + 1] = braid_step(s_lds, s[4 * c + 1] ^ w.y, o0, o1, o2, o3);
+          s[4 * c + 2] = braid_step(s_lds, s[4 * c + 2] ^ w.z, o0, o1, o2, o3);
+          s[4 * c + 3] = braid_step(s_lds, s[4 * c + 3] ^ w.w, o0, o1, o2, o3);
+        }
+      }
+  };
+  // the group's fold (small_body's), its result stored; the registers reset
+  auto fold_store = [&](const SmallGeo &e) {
+#pragma unroll
+    for (int t = 0; t < NS; t++) s[t] ^= q[t];
+    uint32_t r;
+    if (kCoal && C == 2) {
+#pragma unroll
+      for (int m = 0; m < NS; m += 2) s[m] ^= comb_apply(s_lds, 0, s[m + 1]);
+      s[0] ^= comb_apply(s_lds, 1, s[2]);
+      s[4] ^= comb_apply(s_lds, 1, s[6]);
+      s[0] ^= comb_apply(s_lds, 5, s[4]);
+      r = s[0];
+      r ^= row_shl<1>(comb_apply(s_lds, 2, r));
+      r ^= row_shl<2>(comb_apply(s_lds, 3, r));
+      r ^= row_shl<4>(comb_apply(s_lds, 4, r));
+    } else {
+#pragma unroll
+      for (int t = 0; t < LOG_NS; t++)
+#pragma unroll
+        for (int m = 0; m < NS; m += 2 << t) s[m] ^= comb_apply(s_lds, t, s[m + (1 << t)]);
+      r = s[0];
+      r ^= row_shl<1>(comb_apply(s_lds, LOG_NS + 0, r));
+      r ^= row_shl<2>(comb_apply(s_lds, LOG_NS + 1, r));
+      r ^= row_shl<4>(comb_apply(s_lds, LOG_NS + 2, r));
+      if (LOG_G == 4) r ^= row_shl<8>(comb_apply(s_lds, LOG_NS + 3, r));
+    }
+    const uint32_t tpad = (uint32_t)(-e.re) & 15u, a4 = tpad >> 2;
+    if (a4 & 2u) r = comb_apply(s_lds, 1, r);
+    if (a4 & 1u) r = comb_apply(s_lds, 0, r);
+    const uint32_t *xinv8 = s_lds + kLdsCombDword + 4u * kXinv8Chunk;
+    for (uint32_t b = 0; b < 3u; b++)
+      if (b < (tpad & 3u)) r = (r << 8) ^ xinv8[r >> 24];
+    if (e.active && lg == 0) {
+      const uint32_t len = (uint32_t)(e.re - e.rs);
+      if (len < 4u) {  // unrolled, global loads: a loop of loads here cost the waits above their counts
+        typedef const __attribute__((address_space(1))) uint8_t *gbyte;
+        const gbyte bp = reinterpret_cast<gbyte>(e.astart + (uint32_t)e.rs);
+        r = ~e.seed;
+#pragma unroll
+        for (uint32_t p = 0; p < 3u; p++)
+          if (p < len) r = (r >> 8) ^ a.tab->stdtab[(r ^ bp[p]) & 0xFFu];
+      }
+      a.out[kSd ? (uint64_t)e.j : BPW * qc + g] = ~r;
+    }
+#pragma unroll
+    for (int t = 0; t < NS; t++) s[t] = 0u, q[t] = 0u;
+  };
+
+  SmallGeo cur = make_geo(load_desc(BPW * qc + g));
+  SmallGeo nxt = make_geo(load_desc(BPW * (qc + waves) + g));  // all lanes inactive past the list: a dummy group
+  Chunk A, B;
+  issue(cur.astart, cur.rel0, 0, A);
+  issue(cur.astart, cur.rel0, 1, B);
+  for (;;) {  // one group per iteration
+    // the descriptor of the group after next, taken in at the end of this
+    // iteration (not carried around the loop: a loop-carried load result was
+    // copied, behind a wait for every load in flight)
+    const Desc dn = load_desc(BPW * (qc + 2 * waves) + g);
+    // chunk pairs: A holds chunk ci, B chunk ci + 1 (nch even: a group starts
+    // in A); each is refilled with the chunk two ahead once consumed
+    for (uint32_t ci = 0; ci < cur.nch; ci += 2) {
+      const bool last = ci + 2 == cur.nch;  // wave-uniform
+      consume(cur, ci, A);
+      issue(last ? nxt.astart : cur.astart, last ? nxt.rel0 : cur.rel0, last ? 0u : ci + 2, A);
+      consume(cur, ci + 1, B);
+      issue(last ? nxt.astart : cur.astart, last ? nxt.rel0 : cur.rel0, last ? 1u : ci + 3, B);
+    }
+    fold_store(cur);
+    qc += waves;
+    if (qc >= nq) break;
+    cur = nxt;
+    nxt = make_geo(dn);
+  }
+  __builtin_amdgcn_s_waitcnt(0);  // the refills past the last group land before the wave ends
+}
+
 // kAblate == 1 (measurement builds, zcrc32_batch_device_read_ceiling): the
 // braid steps become one VALU rotate each -- the same loads, no lookups.
 // kCoal (G = 8): lane l of a group reads the 16-B chunks at 16 l and 16 l +
@@ -47,11 +274,17 @@ constexpr uint32_t kXinv8Chunk = 7u * 256u;
 // 32 l and 32 l + 16: every load touched half of each 128-B line of its
 // buffer, and a pure read in that layout ran at 6.0 TB/s on 1 KiB buffers
 // against 6.8 for 16 lanes, tools/ceiling_probe, profiles/r05/s4).
-template <bool kStrided, int G, int kD, int kAblate, bool kCoal>
+// kPipe: the pipelined walk (small_pipe) after the table fill.
+// kBlk: bytes per block -- 256 (TableBlob::braid256), or 128 (braid128; with
+// 8 lanes one 16-B chunk per lane and block: 4 streams a lane instead of 8,
+// so the fold takes 6 combine steps per lane instead of 10).
+template <bool kStrided, int G, int kD, int kAblate, bool kCoal, bool kPipe, int kBlk>
 __device__ __forceinline__ void small_body(const SmallArgs &a, uint32_t *s_lds, uint64_t n, uint32_t blk,
                                            uint32_t nblk) {
   static_assert(G == 8 || G == 16, "lanes per buffer");
-  constexpr int C = 16 / G, NS = 4 * C, LOG_NS = NS == 4 ? 2 : 3, LOG_G = G == 8 ? 3 : 4;
+  static_assert(kBlk == 256 || (kBlk == 128 && G == 8 && !kPipe), "block size");
+  constexpr int C = kBlk / 16 / G, NS = 4 * C, LOG_NS = NS == 4 ? 2 : 3, LOG_G = G == 8 ? 3 : 4;
+  constexpr uint32_t kBlkShift = kBlk == 256 ? 8 : 7;
   constexpr uint32_t BPW = 64 / G;  // buffers per wave
   const uint32_t tid = threadIdx.x, lane = tid & 63u, g = lane / G, lg = lane % G;
   const uint64_t waves = (uint64_t)nblk * kWaves;
@@ -87,7 +320,7 @@ __device__ __forceinline__ void small_body(const SmallArgs &a, uint32_t *s_lds, 
 
   {  // LDS: braided MCT(x^2048) | combine tables (batch kernel's layout)
     uint4 *dst = reinterpret_cast<uint4 *>(s_lds);
-    const uint32_t *b = a.tab->braid256;
+    const uint32_t *b = kBlk == 256 ? a.tab->braid256 : a.tab->braid128;
 #pragma unroll
     for (int k = 0; k < 8; k++) {
       const uint32_t o = 16u * (tid + 1024u * k);
@@ -104,6 +337,13 @@ __device__ __forceinline__ void small_body(const SmallArgs &a, uint32_t *s_lds, 
                           : cs[tid + 1024u];
   }
   __syncthreads();
+  if (kPipe) {
+    if (kStrided) small_pipe<0, G, kD, kAblate, kCoal>(a, s_lds, n, blk, nblk);
+    else if (a.sdesc) small_pipe<3, G, kD, kAblate, kCoal>(a, s_lds, n, blk, nblk);
+    else if (a.lens) small_pipe<1, G, kD, kAblate, kCoal>(a, s_lds, n, blk, nblk);
+    else small_pipe<2, G, kD, kAblate, kCoal>(a, s_lds, n, blk, nblk);
+    return;
+  }
   const uint32_t lo0 = (lane & 31u) * 4u;
   const uint32_t o0 = lo0, o1 = lo0 + 128u, o2 = lo0 + 65536u, o3 = lo0 + 65536u + 128u;
 
@@ -117,7 +357,7 @@ __device__ __forceinline__ void small_body(const SmallArgs &a, uint32_t *s_lds, 
     const uint64_t astart = pstart & ~(uint64_t)15;
     const int32_t rs = (int32_t)(pstart & 15u), re = rs + (int32_t)len, span = (re + 15) & ~15;
     const uint32_t inj = ~seed;
-    const uint32_t kq = (active && !tiny) ? (uint32_t)(span + 255) >> 8 : 0u;
+    const uint32_t kq = (active && !tiny) ? (uint32_t)(span + kBlk - 1) >> kBlkShift : 0u;
     const uint32_t kmax = uni32(__reduce_max_sync(0xFFFFFFFFFFFFFFFFull, kq));
     // stream t's register is s[t] ^ q[t] (q: the last step's fourth lookup,
     // taken into the next index by a three-input xor; zcrc_batch_kernel.h
@@ -127,14 +367,14 @@ __device__ __forceinline__ void small_body(const SmallArgs &a, uint32_t *s_lds, 
     for (int t = 0; t < NS; t++) s[t] = 0u, q[t] = 0u;
     // chunk c of lane lg: 16 C lg + 16 c (kCoal: 16 lg + 16 G c) in every block
     constexpr int32_t kLaneStep = kCoal ? 16 : 16 * C, kChunkStep = kCoal ? 16 * G : 16;
-    int32_t rel0 = kq ? span - 256 * (int32_t)kmax + kLaneStep * (int32_t)lg : -(1 << 30);
+    int32_t rel0 = kq ? span - kBlk * (int32_t)kmax + kLaneStep * (int32_t)lg : -(1 << 30);
     for (uint32_t k = 0; k < kmax; k += kD) {
       small_v4u d[kD][C];
 #pragma unroll
       for (int b = 0; b < kD; b++)
 #pragma unroll
         for (int c = 0; c < C; c++) {
-          const int32_t rel = rel0 + 256 * b + kChunkStep * c;
+          const int32_t rel = rel0 + kBlk * b + kChunkStep * c;
           d[b][c] = (small_v4u)(0u);
           if (k + b < kmax && rel >= 0)
             d[b][c] = __builtin_nontemporal_load(reinterpret_cast<const small_v4u *>(astart + (uint32_t)rel));
@@ -144,7 +384,7 @@ __device__ __forceinline__ void small_body(const SmallArgs &a, uint32_t *s_lds, 
         if (k + b < kmax) {
 #pragma unroll
           for (int c = 0; c < C; c++) {
-            const int32_t rel = rel0 + 256 * b + kChunkStep * c;
+            const int32_t rel = rel0 + kBlk * b + kChunkStep * c;
             uint4 w = make_uint4(d[b][c].x, d[b][c].y, d[b][c].z, d[b][c].w);
             if (rel >= 0 && (rel < rs + 4 || rel + 16 > re))
               w = fix_chunk(w, clamp_rel(rs - rel), clamp_rel(re - rel), clamp_rel(rs - rel), inj);
@@ -162,12 +402,16 @@ __device__ __forceinline__ void small_body(const SmallArgs &a, uint32_t *s_lds, 
           }
         }
       }
-      rel0 += 256 * kD;
+      rel0 += kBlk * kD;
     }
 #pragma unroll
     for (int t = 0; t < NS; t++) s[t] ^= q[t];
     uint32_t r;
-    if (kCoal && C == 2) {
+    if (kAblate == 3) {  // diagnostic: no fold
+      r = s[0];
+#pragma unroll
+      for (int t = 1; t < NS; t++) r ^= s[t];
+    } else if (kCoal && C == 2) {
       // fold, kCoal: a chunk's dwords 4 and 8 B apart (combine tables 0, 1),
       // the lane's two chunks 16 G = 128 B apart (table 5), lanes 16 B apart
       // (tables 2, 3, 4: the table c moves a register back 4 * 2^c bytes)
@@ -212,10 +456,12 @@ __device__ __forceinline__ void small_body(const SmallArgs &a, uint32_t *s_lds, 
   }
 }
 
-template <bool kStrided, int G, int kD, bool kCoal = false>
+// kAbl (tools/ceiling_probe diagnostics): 1 = the read ceiling's body, 3 =
+// the braid steps without the fold (wrong results)
+template <bool kStrided, int G, int kD, bool kCoal = false, bool kPipe = false, int kAbl = 0, int kBlk = 256>
 __global__ __launch_bounds__(1024) void crc32_small_kernel(SmallArgs a) {
   __shared__ __attribute__((aligned(16))) uint32_t s_lds[kLdsBytes / 4];
-  small_body<kStrided, G, kD, 0, kCoal>(a, s_lds, a.n, blockIdx.x, gridDim.x);
+  small_body<kStrided, G, kD, kAbl, kCoal, kPipe, kBlk>(a, s_lds, a.n, blockIdx.x, gridDim.x);
 }
 
 }  // namespace zcrc

@@ -7,6 +7,7 @@ namespace zcrc {
 
 // braid  = MCT(x^(8*1024))            hot loop: 1 KiB per stream step
 // braid256 = MCT(x^(8*256))           small-buffer kernel: 256 B per step
+// braid128 = MCT(x^(8*128))           small-buffer kernel, 128-B blocks
 // comb   = MCT(x^-32 .. x^-4096)      in-lane and cross-lane combine tree
 // tshift = MCT(x^(-8t)), t < 16       16-B alignment padding at a piece end
 // xinv8  = r * x^-8 byte table         the small-buffer kernel's last 0-3 padding bytes
@@ -17,6 +18,7 @@ inline void build_tables(TableBlob &tb) {
   build_xpow_table(xp);
   build_mct(gf2_xpow8(xp, 1024), tb.braid);
   build_mct(gf2_xpow8(xp, 256), tb.braid256);
+  build_mct(gf2_xpow8(xp, 128), tb.braid128);
   const uint32_t comb_bytes[8] = {4, 8, 16, 32, 64, 128, 256, 512};
   for (int c = 0; c < 8; c++) build_mct(gf2_xinvpow8_small(comb_bytes[c]), tb.comb + c * 1024);
   for (int t = 0; t < 16; t++) build_mct(gf2_xinvpow8_small((uint32_t)t), tb.tshift + t * 1024);
