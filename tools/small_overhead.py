@@ -35,7 +35,7 @@ def main():
             lens = torch.full((n,), L, dtype=torch.int64, device=dev)
             z.fill_synthetic(ptrs, lens, index0=7 * b, seed=0xC0FFEE)
             bat.append((mem, ptrs, lens, torch.empty(n, dtype=torch.int32, device=dev)))
-        for api in ("strided", "device"):
+        for api in ("device", "strided", "device", "strided"):  # twice: order effects
             def call(b):
                 mem, ptrs, lens, out = bat[b]
                 if api == "device":
