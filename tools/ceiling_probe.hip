@@ -42,7 +42,10 @@
 //   crc-G8c/G16  8 lanes on 256-B blocks (coalesced), 16 lanes; crc-str:
 //                the product's form with strided addressing (the strided
 //                API); crc-G8cp: G8c with the pipelined walk (small_pipe);
-//                results compared with crc's
+//                results compared with crc's (session 23: the product's
+//                forms with a uniform group loop and unconditional loads ran
+//                1.8x slower -- the descriptor prefetch's wait moved in front
+//                of the group's loads)
 // (Round-5 sessions 16-18 also measured the pipelined 16-lane walk, 8 lanes
 // on 128-B blocks with 4 blocks in flight, and the bodies without lookups or
 // without the fold: profiles/r05/s15_s20/, DESIGN.md 7e.  Session 4 measured G4
@@ -456,7 +459,7 @@ int main(int argc, char **argv) {
           hipExtLaunchKernelGGL((crc32_small_kernel<true, 16, 8>), dim3(cus), dim3(1024), 0, 0, a, z, 0, sa);
         return;
       }
-      const int form = v == 3 ? (lanes == 8 ? 8 : 5) : v;
+      const int form = v == 3 ? (lanes == 8 ? 10 : 5) : v;
       if (form == 4)
         hipExtLaunchKernelGGL((crc32_small_kernel<false, 8, 4, true>), dim3(cus), dim3(1024), 0, 0, a, z, 0, sa);
       else if (form == 5)
