@@ -53,7 +53,7 @@
 // Every launch is timed by its own dispatch packet (hipExtLaunchKernelGGL
 // events); the figures are averages over the launches, in GB/s of payload.
 //
-//   make -C tools ceiling_probe && tools/ceiling_probe [reps [1: part 1 only | 2: part 2 only]]
+//   make -C tools ceiling_probe && tools/ceiling_probe [reps [1: part 1 only | 2: part 2 only | 3: part 3 only]]
 #include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -128,6 +128,100 @@ __global__ __launch_bounds__(1024) void k_pb_desc(const uint64_t *ptrs, const ui
   const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc((void *)p, (short)0, (int)len, 0x00020000);
   const uint32_t acc = read_blocks(r, 0, len >> 10, lane);
   if (acc == 0x12345678u) out[w] = acc;
+}
+
+// Part 3: a grid-stride sweep of `bytes` contiguous bytes with 64-bit
+// global addressing (nt 16-B loads, 4 in flight per thread per step)
+template <int kThr>
+__global__ __launch_bounds__(kThr) void k_sweep(const uint8_t *base, uint64_t bytes, uint32_t *out) {
+  typedef const __attribute__((address_space(1))) v4u *gv4u;
+  uint32_t acc = 0;
+  const uint64_t step = (uint64_t)gridDim.x * kThr * 64;
+  for (uint64_t o = ((uint64_t)blockIdx.x * kThr * 4 + threadIdx.x) * 16; o + (uint64_t)(3 * kThr + 1) * 16 <= bytes;
+       o += step) {
+    v4u v[4];
+#pragma unroll
+    for (int u = 0; u < 4; u++)
+      v[u] = __builtin_nontemporal_load(reinterpret_cast<gv4u>(reinterpret_cast<uint64_t>(base) + o + (uint64_t)u * kThr * 16));
+#pragma unroll
+    for (int u = 0; u < 4; u++) acc ^= xr(v[u]);
+  }
+  if (acc == 0x12345678u) out[threadIdx.x] = acc;
+}
+
+// Part 3: the sweep's variants -- 1024-thread workgroups, kL loads per
+// thread per step; kWaveContig: a wave's kL loads are consecutive KiB (the
+// workgroup still covers 16 kL KiB contiguous per step) instead of 16 KiB
+// apart; the grid covers #WG x 16 kL KiB per step
+template <int kL, bool kWaveContig>
+__global__ __launch_bounds__(1024) void k_sweep2(const uint8_t *base, uint64_t bytes, uint32_t *out) {
+  typedef const __attribute__((address_space(1))) v4u *gv4u;
+  const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+  const uint64_t wg_bytes = 16384ull * kL, step = (uint64_t)gridDim.x * wg_bytes;
+  const uint64_t b0 = reinterpret_cast<uint64_t>(base);
+  uint32_t acc = 0;
+  for (uint64_t o = (uint64_t)blockIdx.x * wg_bytes; o + wg_bytes <= bytes; o += step) {
+    v4u v[kL];
+#pragma unroll
+    for (int u = 0; u < kL; u++) {
+      const uint64_t blk = kWaveContig ? (uint64_t)wv * kL + u : (uint64_t)u * 16 + wv;  // KiB within the WG's chunk
+      v[u] = __builtin_nontemporal_load(reinterpret_cast<gv4u>(b0 + o + 1024 * blk + 16u * lane));
+    }
+#pragma unroll
+    for (int u = 0; u < kL; u++) acc ^= xr(v[u]);
+  }
+  if (acc == 0x12345678u) out[threadIdx.x] = acc;
+}
+
+// Part 3 pure reads in CRC-compatible wave mappings over `bytes`: kPiece ==
+// 0: wave w of W reads the contiguous range [w per, (w + 1) per) (the
+// product's static ranges); kPiece > 0: wave w reads pieces w, w + W, ...
+// of kPiece bytes (all waves in lockstep rows of W pieces).  1 KiB blocks,
+// 8 in flight per wave.
+template <uint64_t kPiece, int kLd = 8>
+__global__ __launch_bounds__(1024) void k_waves(const uint8_t *base, uint64_t bytes, uint32_t *out) {
+  typedef const __attribute__((address_space(1))) v4u *gv4u;
+  const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+  const uint64_t W = (uint64_t)gridDim.x * 16, w = (uint64_t)blockIdx.x * 16 + wv;
+  const uint64_t b0 = reinterpret_cast<uint64_t>(base);
+  uint32_t acc = 0;
+  auto piece = [&](uint64_t off, uint64_t len) {
+    for (uint64_t b = 0; b < len; b += 1024 * kLd) {
+      v4u v[kLd];
+#pragma unroll
+      for (int u = 0; u < kLd; u++)
+        v[u] = __builtin_nontemporal_load(reinterpret_cast<gv4u>(b0 + off + b + 1024u * u + 16u * lane));
+#pragma unroll
+      for (int u = 0; u < kLd; u++) acc ^= xr(v[u]);
+    }
+  };
+  if (kPiece == 0) {
+    const uint64_t per = (bytes / W) & ~(1024ull * kLd - 1);
+    piece(w * per, per);
+  } else {
+    for (uint64_t p = w; (p + 1) * kPiece <= bytes; p += W) piece(p * kPiece, kPiece);
+  }
+  if (acc == 0x12345678u) out[threadIdx.x] = acc;
+}
+
+// Part 3: workgroup-cooperative ranges: workgroup g of G reads [g per,
+// (g + 1) per), its wave w the 1 KiB blocks w, w + 16, w + 32, ... of it
+// (kDepth blocks in flight per wave, 16 KiB apart)
+template <int kDepthW>
+__global__ __launch_bounds__(1024) void k_wgc_range(const uint8_t *base, uint64_t bytes, uint32_t *out) {
+  typedef const __attribute__((address_space(1))) v4u *gv4u;
+  const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+  const uint64_t per = (bytes / gridDim.x) & ~((uint64_t)kDepthW * 16384 - 1);
+  const uint64_t b0 = reinterpret_cast<uint64_t>(base) + (uint64_t)blockIdx.x * per + 1024u * wv + 16u * lane;
+  uint32_t acc = 0;
+  for (uint64_t o = 0; o < per; o += (uint64_t)kDepthW * 16384) {
+    v4u v[kDepthW];
+#pragma unroll
+    for (int u = 0; u < kDepthW; u++) v[u] = __builtin_nontemporal_load(reinterpret_cast<gv4u>(b0 + o + 16384u * u));
+#pragma unroll
+    for (int u = 0; u < kDepthW; u++) acc ^= xr(v[u]);
+  }
+  if (acc == 0x12345678u) out[threadIdx.x] = acc;
 }
 
 __global__ __launch_bounds__(256) void k_grid8(const uint8_t *base, uint32_t *out) {
@@ -311,7 +405,7 @@ int main(int argc, char **argv) {
   };
 
   // ---------------------------------------------------------------- part 1
-  if (!(argc > 2 && atoi(argv[2]) == 2)) {  // (2: part 2 only)
+  if (!(argc > 2 && atoi(argv[2]) >= 2)) {  // (2: part 2 only)
     uint8_t *data;
     CHECK(hipMalloc(&data, kBatchBytes * kBatches));
     std::vector<uint64_t> hp(kN * kBatches), hl(kN * kBatches, kLen);
@@ -408,6 +502,96 @@ int main(int argc, char **argv) {
     CHECK(hipFree(dp));
     CHECK(hipFree(dl));
     CHECK(hipFree(dpre));
+  }
+
+  // ---------------------------------------------------------------- part 3
+  // (3: part 3 only) the sustained read of config 3's and config 4's payload
+  // regions as one contiguous sweep -- the bound for any mapping of their
+  // buffers (config 4: the bench's layout, 16-B aligned bounded power law)
+  if (argc > 2 && atoi(argv[2]) == 3) {
+    const uint64_t c3 = 65536ull << 20;
+    uint64_t c4 = 0;
+    {
+      // bench.py zipf_lens: the same mix64 hash and bounded power law
+      for (uint64_t i = 0; i < 100000; i++) {
+        uint64_t z = 0x5A1F5EEDull ^ ((i + 1) * 0xD1B54A32D192ED03ull);
+        z += 0x9E3779B97F4A7C15ull;
+        z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+        z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+        z ^= z >> 31;
+        const double u = (double)(z >> 11) * (1.0 / 9007199254740992.0);
+        const double t = 1.0 - u * 127.0 / 128.0;
+        double L = 1024.0 / (t * t);
+        L = L < 1024 ? 1024 : (L > (1 << 24) ? (1 << 24) : L);
+        c4 += ((uint64_t)L + 15) & ~15ull;
+      }
+    }
+    uint8_t *mem;
+    CHECK(hipMalloc(&mem, c3));
+    CHECK(hipMemset(mem, 1, c3));
+    CHECK(hipDeviceSynchronize());
+    // crc-c3 / abl-c3: the product's batch kernel on config 3 in its strided
+    // form (65,536 x 1 MiB; static ranges per wave, then dynamic units) and
+    // its read-ceiling form, launched as zcrc32_batch_device_strided does
+    const char *nm[] = {"sweep8-c3", "sweep16-c3", "sweep8-c4", "sweep16-c4", "crc-c3",  "abl-c3",
+                        "range-c3",  "range2-c3",  "range4-c3", "crc-d2-c3",  "abl-d2-c3"};
+    constexpr int kV3 = 11;
+    uint32_t *o3;
+    CHECK(hipMalloc(&o3, 4 * 65536));
+    std::vector<std::vector<double>> t(kV3);
+    for (int r = 0; r < reps; r++)
+      for (int v = 0; v < kV3; v++) {
+        if (v == 4 || v == 5 || v >= 9) {
+          CHECK(hipMemsetAsync(o3, 0, 4 * 65536, 0));
+          CHECK(hipMemsetAsync(scratch + 2048, 0, 64, 0));
+        }
+        timed(nm[v], r == 0, 1, [&](int, hipEvent_t a, hipEvent_t z) {
+          const uint64_t bytes = v < 2 ? c3 : c4;
+          const uint8_t *base = v < 2 ? mem : mem + (r & 1) * (c3 / 2);  // config 4: two distinct regions
+          if (v == 4 || v == 5 || v >= 9) {
+            BatchArgs x{};
+            x.base = mem;
+            x.stride = 1u << 20;
+            x.len = 1u << 20;
+            x.n = 65536;
+            x.out = o3;
+            x.tab = d_tab;
+            x.ctr = scratch + 2048;
+            x.dyn_shift = kDynAuto;
+            if (v == 4)
+              hipExtLaunchKernelGGL((crc32_batch_kernel<true, kDepth, 0>), dim3(cus), dim3(kThreads), 0, 0, a, z, 0, x);
+            else if (v == 5)
+              hipExtLaunchKernelGGL((crc32_batch_kernel<true, kDepth, 1>), dim3(cus), dim3(kThreads), 0, 0, a, z, 0, x);
+            else if (v == 9)
+              hipExtLaunchKernelGGL((crc32_batch_kernel<true, 2, 0>), dim3(cus), dim3(kThreads), 0, 0, a, z, 0, x);
+            else
+              hipExtLaunchKernelGGL((crc32_batch_kernel<true, 2, 1>), dim3(cus), dim3(kThreads), 0, 0, a, z, 0, x);
+          } else if (v >= 6 && v <= 8) {
+            switch (v) {
+              case 6: hipExtLaunchKernelGGL((k_waves<0>), dim3(cus), dim3(1024), 0, 0, a, z, 0, mem, c3, out); break;
+              case 7: hipExtLaunchKernelGGL((k_waves<0, 2>), dim3(cus), dim3(1024), 0, 0, a, z, 0, mem, c3, out); break;
+              case 8: hipExtLaunchKernelGGL((k_waves<0, 4>), dim3(cus), dim3(1024), 0, 0, a, z, 0, mem, c3, out); break;
+            }
+          } else if (v % 2 == 0) {
+            hipExtLaunchKernelGGL((k_sweep<256>), dim3(cus * 8), dim3(256), 0, 0, a, z, 0, base, bytes, out);
+          } else {
+            hipExtLaunchKernelGGL((k_sweep<1024>), dim3(cus), dim3(1024), 0, 0, a, z, 0, base, bytes, out);
+          }
+        }, t[v]);
+      }
+    printf("ceiling_probe part 3: contiguous sweeps, config 3 (%llu B) and config 4 (%llu B) regions, %d reps\n",
+           (unsigned long long)c3, (unsigned long long)c4, reps);
+    for (int v = 0; v < kV3; v++) {
+      double sum = 0;
+      for (double x : t[v]) sum += x;
+      const double avg = sum / t[v].size();
+      const uint64_t bytes = v == 2 || v == 3 ? c4 : c3;
+      printf("  %-10s avg %9.3f ms  %7.1f GB/s (avg)  %7.1f GB/s (best)\n", nm[v], avg, bytes / (avg * 1e-3) / 1e9,
+             bytes / (pct(t[v], 0) * 1e-3) / 1e9);
+    }
+    CHECK(hipFree(mem));
+    CHECK(hipFree(o3));
+    return 0;
   }
 
   // ---------------------------------------------------------------- part 2

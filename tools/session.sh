@@ -18,6 +18,9 @@
 #   py:<script>:<args>     python3 <script> <args> (commas for spaces)
 #   kt:<script>:<args>     the same under rocprofv3 --kernel-trace --stats
 #                          (csv under gpurun_out/<name>/kt<step>/)
+#   ab:<config>:<rounds>:<steps>:<lib>,<lib>...  tools/ab_libs.sh (bench.py per
+#                          library build, interleaved; no secondaries, ceiling
+#                          or host-resident line) into gpurun_out/<name>/ab_<config>.jsonl
 #   export:<VAR>=<value>   set an environment variable for the steps after it
 #   unset:<VAR>            remove it again
 set -o pipefail
@@ -70,6 +73,11 @@ for step in "$@"; do
       # shellcheck disable=SC2086
       timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/kt$n" -o kt -- \
         python3 -u "$script" ${pargs//,/ } > "$log" 2>&1 ;;
+    ab)
+      IFS=: read -r cfg rounds steps libs <<< "$arg"
+      # shellcheck disable=SC2086
+      AB_BENCH_ARGS="--no-secondary --no-read-ceiling --host-resident-gib 0" timeout -k 10 1000 \
+        bash tools/ab_libs.sh "$O/ab_$cfg.jsonl" "$cfg" "$rounds" "$steps" ${libs//,/ } > "$log" 2>&1 ;;
     export)
       export "${arg?}"; echo "    $arg" >> "$O/steps.txt"; continue ;;
     unset)
