@@ -7,7 +7,8 @@
  *      launches still queued, then another batch (other buffers, other
  *      lengths) on a fresh stream s2 -- which may get s1's handle back --
  *      and so on for the one-launch (n <= 16 x CUs), two-launch and split-plan
- *      forms; results checked against zlib after one device synchronize;
+ *      forms; results checked against zlib once events recorded before
+ *      each destroy have completed (destroy_queued);
  *   B. one-stream inflate (zcrc_inflate_device) of two different deflated
  *      entries on two fresh streams, the first destroyed before the second is
  *      queued; then the host-memory inflate (zcrc_inflate_batch) of entries
@@ -21,7 +22,7 @@
  * src/ZIPsFS_preloadfileram.c:243 (the CRC after the preload, which libzip's
  * inflate produced).
  *
- * Usage: stream_churn <rounds> <threads>
+ * Usage: stream_churn <rounds> <threads>   (STREAM_CHURN_PARTS=abc: parts run)
  * Output: one JSON line; exit status 1 on any mismatch or error. */
 #include <hip/hip_runtime_api.h>
 #include <pthread.h>
@@ -68,6 +69,26 @@ static long g_checks = 0, g_fail = 0;
       return -1;                                                                  \
     }                                                                             \
   } while (0)
+
+/* Destroy a stream with its work still queued, after recording `ev` on it.
+ * The checks wait on the event, not on hipDeviceSynchronize: on ROCm 7.2
+ * neither hipStreamDestroy nor a later hipDeviceSynchronize always waits for
+ * work queued on a destroyed stream (round 5: results read after both arrived
+ * 200 ms later; profiles/r05/stream_destroy/). */
+static int destroy_queued(hipStream_t s, hipEvent_t *ev) {
+  if (hipEventCreateWithFlags(ev, hipEventDisableTiming) != hipSuccess) return -1;
+  if (hipEventRecord(*ev, s) != hipSuccess) return -1;
+  return hipStreamDestroy(s) == hipSuccess ? 0 : -1;
+}
+
+static int wait_queued(hipEvent_t *ev, int n) {
+  int rc = 0;
+  for (int k = 0; k < n; k++) {
+    rc |= hipEventSynchronize(ev[k]) != hipSuccess;
+    rc |= hipEventDestroy(ev[k]) != hipSuccess;
+  }
+  return rc ? -1 : 0;
+}
 
 static void count(long ok, long bad) {
   pthread_mutex_lock(&g_mu);
@@ -199,13 +220,15 @@ static int part_a(uint64_t seed) {
   batch_t b[8];
   for (int k = 0; k < 8; k++)
     if (batch_make(&b[k], shapes[k % 4][0], shapes[k % 4][1], seed * 16 + (uint64_t)k)) return -1;
+  hipEvent_t ev[8];
   for (int k = 0; k < 8; k++) {
     hipStream_t s;
     HIPCHK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
     ZCHK(zcrc32_batch_device((const void *const *)b[k].d_ptrs, b[k].d_lens, NULL, b[k].d_out, b[k].n, s));
-    HIPCHK(hipStreamDestroy(s)); /* launches still queued: the next stream may get this handle */
+    /* launches still queued: the next stream may get this handle */
+    if (destroy_queued(s, &ev[k])) FAILF("destroy_queued");
   }
-  HIPCHK(hipDeviceSynchronize());
+  if (wait_queued(ev, 8)) FAILF("wait_queued");
   for (int k = 0; k < 8; k++) batch_check(&b[k], "device batch on a churned stream");
   for (int k = 0; k < 8; k++) batch_free(&b[k]);
   return 0;
@@ -235,30 +258,49 @@ static int part_b(uint64_t seed) {
   void *d_src[2], *d_dst[2];
   uint64_t *d_olen[2];
   int32_t *d_st[2];
+  /* the results start as 0xEE sentinels and the output has a 4 KiB canary of
+   * 0xEE behind it: a failure then tells "never written" from "overwritten",
+   * and an overrun of the output from a short one */
+  const size_t canary = 4096;
   for (int e = 0; e < 2; e++) {
     HIPCHK(hipMalloc(&d_src[e], clen[e]));
     HIPCHK(hipMemcpy(d_src[e], comp[e], clen[e], hipMemcpyHostToDevice));
-    HIPCHK(hipMalloc(&d_dst[e], n));
+    HIPCHK(hipMalloc(&d_dst[e], n + canary));
+    HIPCHK(hipMemset((uint8_t *)d_dst[e] + n, 0xEE, canary));
     HIPCHK(hipMalloc((void **)&d_olen[e], 8));
     HIPCHK(hipMalloc((void **)&d_st[e], 4));
+    HIPCHK(hipMemset(d_olen[e], 0xEE, 8));
+    HIPCHK(hipMemset(d_st[e], 0xEE, 4));
   }
+  HIPCHK(hipDeviceSynchronize());
+  hipEvent_t ev[2];
   for (int e = 0; e < 2; e++) {
     hipStream_t s;
     HIPCHK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
     ZCHK(zcrc_inflate_device(d_src[e], clen[e], d_dst[e], n, d_olen[e], d_st[e], 0, s));
-    HIPCHK(hipStreamDestroy(s));
+    if (destroy_queued(s, &ev[e])) FAILF("destroy_queued");
   }
-  HIPCHK(hipDeviceSynchronize());
-  uint8_t *back = malloc(n);
+  if (wait_queued(ev, 2)) FAILF("wait_queued");
+  uint8_t *back = malloc(n + canary);
   for (int e = 0; e < 2; e++) {
     uint64_t olen = 0;
     int32_t st = -1;
     HIPCHK(hipMemcpy(&olen, d_olen[e], 8, hipMemcpyDeviceToHost));
     HIPCHK(hipMemcpy(&st, d_st[e], 4, hipMemcpyDeviceToHost));
-    HIPCHK(hipMemcpy(back, d_dst[e], n, hipMemcpyDeviceToHost));
-    const int ok = st == 0 && olen == n && !memcmp(back, raw[e], n);
-    if (!ok) LOGF("zcrc_inflate_device entry %d: status %d, %llu bytes, bytes %s", e, st,
-                   (unsigned long long)olen, memcmp(back, raw[e], n) ? "differ" : "equal");
+    HIPCHK(hipMemcpy(back, d_dst[e], n + canary, hipMemcpyDeviceToHost));
+    size_t canary_bad = 0;
+    for (size_t i = n; i < n + canary; i++) canary_bad += back[i] != 0xEE;
+    const int ok = st == 0 && olen == n && !memcmp(back, raw[e], n) && !canary_bad;
+    if (!ok) {
+      size_t first = n, ndiff = 0;
+      for (size_t i = 0; i < n; i++)
+        if (back[i] != raw[e][i]) ndiff++, first = first < i ? first : i;
+      LOGF("zcrc_inflate_device entry %d (seed %llu, %zu compressed bytes): status %d%s, %llu bytes%s, %zu bytes "
+           "differ (first at %zu), %zu canary bytes overwritten",
+           e, (unsigned long long)seed, clen[e], st, st == (int32_t)0xEEEEEEEE ? " (never written)" : "",
+           (unsigned long long)olen, olen == 0xEEEEEEEEEEEEEEEEull ? " (never written)" : "", ndiff, first,
+           canary_bad);
+    }
     count(ok, !ok);
     hipFree(d_src[e]);
     hipFree(d_dst[e]);
@@ -406,11 +448,15 @@ static int part_c(uint64_t seed) {
   return 0;
 }
 
+static const char *g_parts = "abc"; /* STREAM_CHURN_PARTS: which parts each round runs */
+
 static void *worker(void *arg) {
   const uint64_t t = (uint64_t)(uintptr_t)arg;
   for (int r = 0; r < g_rounds; r++) {
     const uint64_t seed = 1000 * t + (uint64_t)r + 1;
-    if (part_a(seed) || part_b(seed) || part_c(seed)) break;
+    if ((strchr(g_parts, 'a') && part_a(seed)) || (strchr(g_parts, 'b') && part_b(seed)) ||
+        (strchr(g_parts, 'c') && part_c(seed)))
+      break;
   }
   return NULL;
 }
@@ -419,6 +465,7 @@ int main(int argc, char **argv) {
   g_rounds = argc > 1 ? atoi(argv[1]) : 3;
   const int threads = argc > 2 ? atoi(argv[2]) : 2;
   if (g_rounds < 1 || threads < 1 || threads > 16) return 2;
+  if (getenv("STREAM_CHURN_PARTS")) g_parts = getenv("STREAM_CHURN_PARTS");
   pthread_t th[16];
   for (int t = 0; t < threads; t++) pthread_create(&th[t], NULL, worker, (void *)(uintptr_t)t);
   for (int t = 0; t < threads; t++) pthread_join(th[t], NULL);
@@ -426,9 +473,13 @@ int main(int argc, char **argv) {
   zcrc_cache_info(0, &entries, &bytes, &tl);
   uint64_t freed = 0;
   const int rrc = zcrc_release_cached(&freed);
+  uint64_t left = 0, left_bytes = 0;
+  zcrc_cache_info(0, &left, &left_bytes, NULL);
   printf("{\"rounds\": %d, \"threads\": %d, \"checks\": %ld, \"failures\": %ld, \"scratch_entries\": %llu, "
-         "\"scratch_bytes\": %llu, \"thread_local_bytes\": %llu, \"release_rc\": %d, \"released_bytes\": %llu}\n",
+         "\"scratch_bytes\": %llu, \"thread_local_bytes\": %llu, \"release_rc\": %d, \"released_bytes\": %llu, "
+         "\"entries_left\": %llu, \"bytes_left\": %llu}\n",
          g_rounds, threads, g_checks, g_fail, (unsigned long long)entries, (unsigned long long)bytes,
-         (unsigned long long)tl, rrc, (unsigned long long)freed);
+         (unsigned long long)tl, rrc, (unsigned long long)freed, (unsigned long long)left,
+         (unsigned long long)left_bytes);
   return g_fail ? 1 : 0;
 }

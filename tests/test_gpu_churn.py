@@ -4,8 +4,13 @@ process, in several threads at once.
 tests/dropin/stream_churn.c queues device batches, one-stream inflates and
 ZIP verifications on fresh HIP streams and destroys each stream with its work
 still queued, so that a later stream may get the same handle back; the
-library's scratch is leased per call and ordered by events (zcrc_runtime.hip,
-ScratchCache), so every result must be bit-exact (zlib is the checker).  With
+library's scratch is leased per call and keyed by the stream's handle and,
+where the HIP runtime has hipStreamGetId (ROCm >= 7.1, as a C process links
+it), its unique id (zcrc_runtime.hip, ScratchCache), so every result must be
+bit-exact (zlib is the checker).  The program waits for each destroyed
+stream's work on an event recorded before the destroy: on ROCm 7.2 neither
+hipStreamDestroy nor hipDeviceSynchronize always waits for it (round 5,
+profiles/r05/stream_destroy/).  With
 ZCRC_TL_EXACT=1 every thread-local device buffer is allocated at exactly the
 size asked, behind a canary the library checks after each call: an
 out-of-bounds write by the split inflate, the batch inflate or the ZIP
@@ -51,6 +56,8 @@ def test_streams_destroyed_between_calls_three_threads(tmp_path):
     # every thread-round: 8 device batches (~64k buffers), 2 + 3 inflates, 3 x 24 ZIP entries
     assert d["checks"] >= 3 * 3 * (60000 + 5 + 72), d
     assert d["release_rc"] == 0 and d["released_bytes"] > 0, d
+    # every idle entry -- those of destroyed streams included -- is freed
+    assert d["entries_left"] == 0 and d["bytes_left"] == 0, d
 
 
 @pytest.mark.timeout(300)

@@ -21,6 +21,7 @@
 #   ab:<config>:<rounds>:<steps>:<lib>,<lib>...  tools/ab_libs.sh (bench.py per
 #                          library build, interleaved; no secondaries, ceiling
 #                          or host-resident line) into gpurun_out/<name>/ab_<config>.jsonl
+#   churn:<reps>,<spec>... tools/churn_stress.sh (specs "label|ENV=V|parts|rounds|threads")
 #   export:<VAR>=<value>   set an environment variable for the steps after it
 #   unset:<VAR>            remove it again
 set -o pipefail
@@ -78,6 +79,9 @@ for step in "$@"; do
       # shellcheck disable=SC2086
       AB_BENCH_ARGS="--no-secondary --no-read-ceiling --host-resident-gib 0" timeout -k 10 1000 \
         bash tools/ab_libs.sh "$O/ab_$cfg.jsonl" "$cfg" "$rounds" "$steps" ${libs//,/ } > "$log" 2>&1 ;;
+    churn)
+      # shellcheck disable=SC2086
+      timeout -k 10 1100 bash tools/churn_stress.sh "$O/churn$n" ${arg//,/ } > "$log" 2>&1 ;;
     export)
       export "${arg?}"; echo "    $arg" >> "$O/steps.txt"; continue ;;
     unset)

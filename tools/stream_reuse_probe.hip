@@ -9,7 +9,7 @@
 // kernel's completion flag was set when hipDeviceSynchronize returned.
 //
 //   hipcc --offload-arch=gfx950 -O2 tools/stream_reuse_probe.hip -o tools/stream_reuse_probe
-//   tools/stream_reuse_probe [rounds] [ms]
+//   tools/stream_reuse_probe [rounds] [ms] [threads]
 #include <hip/hip_runtime.h>
 
 #include <chrono>
@@ -33,9 +33,61 @@ __global__ void spin(unsigned *flag, unsigned tag, unsigned long long ticks) {
   if (threadIdx.x == 0) flag[0] = tag;
 }
 
+// Threaded form (argv[3] = threads > 0): each thread, `rounds` times, queues
+// one spin kernel of 1..ms ms on a fresh stream, destroys the stream at once,
+// calls hipDeviceSynchronize and reads its flag.  Counts the reads that came
+// back before the kernel's store ("early"): work of a destroyed stream that
+// neither the destroy nor the device synchronize waited for.
+#include <atomic>
+#include <thread>
+#include <vector>
+static std::atomic<long> g_early{0}, g_total{0};
+static std::atomic<long long> g_destroy_max_us{0};
+
+static void thread_rounds(int t, int rounds, double ms, int khz) {
+  unsigned *flag = nullptr;
+  CHK(hipMalloc(&flag, 4));
+  for (int r = 1; r <= rounds; r++) {
+    const unsigned tag = (unsigned)(t << 16 | r);
+    CHK(hipMemset(flag, 0, 4));
+    CHK(hipDeviceSynchronize());
+    hipStream_t s = nullptr;
+    CHK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    const double this_ms = 1.0 + (ms - 1.0) * (double)((r * 7919 + t * 104729) % 97) / 96.0;
+    hipLaunchKernelGGL(spin, dim3(1), dim3(64), 0, s, flag, tag, (unsigned long long)(this_ms * khz));
+    CHK(hipGetLastError());
+    const auto t0 = std::chrono::steady_clock::now();
+    CHK(hipStreamDestroy(s));
+    const long long us =
+        (long long)std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
+    long long m = g_destroy_max_us.load();
+    while (us > m && !g_destroy_max_us.compare_exchange_weak(m, us)) {
+    }
+    CHK(hipDeviceSynchronize());
+    unsigned got = 0;
+    CHK(hipMemcpy(&got, flag, 4, hipMemcpyDeviceToHost));
+    g_total++;
+    if (got != tag) g_early++;
+  }
+  CHK(hipDeviceSynchronize());
+  CHK(hipFree(flag));
+}
+
 int main(int argc, char **argv) {
   const int rounds = argc > 1 ? atoi(argv[1]) : 4;
   const double ms = argc > 2 ? atof(argv[2]) : 50.0;
+  const int threads = argc > 3 ? atoi(argv[3]) : 0;
+  if (threads > 0) {
+    int khz0 = 0;
+    CHK(hipDeviceGetAttribute(&khz0, hipDeviceAttributeWallClockRate, 0));
+    std::vector<std::thread> th;
+    for (int t = 0; t < threads && t < 16; t++) th.emplace_back(thread_rounds, t, rounds, ms, khz0);
+    for (auto &x : th) x.join();
+    printf("{\"threads\": %d, \"rounds\": %d, \"max_spin_ms\": %.1f, \"reads\": %ld, \"early\": %ld, "
+           "\"destroy_max_us\": %lld}\n",
+           threads, rounds, ms, g_total.load(), g_early.load(), g_destroy_max_us.load());
+    return 0;
+  }
   int khz = 0;
   CHK(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, 0));
   const unsigned long long ticks = (unsigned long long)(ms * khz);
@@ -71,6 +123,13 @@ int main(int argc, char **argv) {
            "\"id_new\": %llu, \"flag_on_new_stream\": %u, \"device_sync_us\": %.1f, \"flag_after_sync\": %u}\n",
            r, ms, us(t0, t1), old == s, id_old, id_new, before, us(t2, t3), after);
     fflush(stdout);
+  }
+  {  // host cost of hipStreamGetId (the library calls it once per leased call)
+    unsigned long long id = 0;
+    const auto t0 = std::chrono::steady_clock::now();
+    for (int i = 0; i < 100000; i++) CHK(hipStreamGetId(s, &id));
+    const double ns = std::chrono::duration<double, std::nano>(std::chrono::steady_clock::now() - t0).count() / 1e5;
+    printf("{\"hipStreamGetId_ns\": %.1f}\n", ns);
   }
   CHK(hipStreamDestroy(s));
   CHK(hipFree(flag));
