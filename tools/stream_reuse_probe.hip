@@ -9,7 +9,7 @@
 // kernel's completion flag was set when hipDeviceSynchronize returned.
 //
 //   hipcc --offload-arch=gfx950 -O2 tools/stream_reuse_probe.hip -o tools/stream_reuse_probe
-//   tools/stream_reuse_probe [rounds] [ms] [threads]
+//   tools/stream_reuse_probe [rounds] [ms] [threads] [launches per stream] [realloc]
 #include <hip/hip_runtime.h>
 
 #include <chrono>
@@ -30,7 +30,7 @@
 __global__ void spin(unsigned *flag, unsigned tag, unsigned long long ticks) {
   const unsigned long long t0 = wall_clock64();
   while (wall_clock64() - t0 < ticks) __builtin_amdgcn_s_sleep(10);
-  if (threadIdx.x == 0) flag[0] = tag;
+  if (threadIdx.x == 0 && tag) flag[0] = tag;  // (tag 0: a chain member that stores nothing)
 }
 
 // Threaded form (argv[3] = threads > 0): each thread, `rounds` times, queues
@@ -44,18 +44,28 @@ __global__ void spin(unsigned *flag, unsigned tag, unsigned long long ticks) {
 static std::atomic<long> g_early{0}, g_total{0};
 static std::atomic<long long> g_destroy_max_us{0};
 
+static int g_chain = 1, g_realloc = 0;
+
 static void thread_rounds(int t, int rounds, double ms, int khz) {
   unsigned *flag = nullptr;
   CHK(hipMalloc(&flag, 4));
   for (int r = 1; r <= rounds; r++) {
+    if (g_realloc) {  // a fresh allocation per round (the library-level repro needed it)
+      CHK(hipFree(flag));
+      CHK(hipMalloc(&flag, 4));
+    }
     const unsigned tag = (unsigned)(t << 16 | r);
     CHK(hipMemset(flag, 0, 4));
     CHK(hipDeviceSynchronize());
     hipStream_t s = nullptr;
     CHK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
     const double this_ms = 1.0 + (ms - 1.0) * (double)((r * 7919 + t * 104729) % 97) / 96.0;
-    hipLaunchKernelGGL(spin, dim3(1), dim3(64), 0, s, flag, tag, (unsigned long long)(this_ms * khz));
-    CHK(hipGetLastError());
+    // g_chain launches of this_ms / g_chain each; only the last stores the tag
+    for (int k = 0; k < g_chain; k++) {
+      hipLaunchKernelGGL(spin, dim3(1), dim3(64), 0, s, flag, k + 1 == g_chain ? tag : 0u,
+                         (unsigned long long)(this_ms / g_chain * khz));
+      CHK(hipGetLastError());
+    }
     const auto t0 = std::chrono::steady_clock::now();
     CHK(hipStreamDestroy(s));
     const long long us =
@@ -77,15 +87,18 @@ int main(int argc, char **argv) {
   const int rounds = argc > 1 ? atoi(argv[1]) : 4;
   const double ms = argc > 2 ? atof(argv[2]) : 50.0;
   const int threads = argc > 3 ? atoi(argv[3]) : 0;
+  g_chain = argc > 4 ? atoi(argv[4]) : 1;
+  g_realloc = argc > 5 ? atoi(argv[5]) : 0;
+  if (g_chain < 1) g_chain = 1;
   if (threads > 0) {
     int khz0 = 0;
     CHK(hipDeviceGetAttribute(&khz0, hipDeviceAttributeWallClockRate, 0));
     std::vector<std::thread> th;
     for (int t = 0; t < threads && t < 16; t++) th.emplace_back(thread_rounds, t, rounds, ms, khz0);
     for (auto &x : th) x.join();
-    printf("{\"threads\": %d, \"rounds\": %d, \"max_spin_ms\": %.1f, \"reads\": %ld, \"early\": %ld, "
-           "\"destroy_max_us\": %lld}\n",
-           threads, rounds, ms, g_total.load(), g_early.load(), g_destroy_max_us.load());
+    printf("{\"threads\": %d, \"rounds\": %d, \"max_spin_ms\": %.1f, \"launches_per_stream\": %d, "
+           "\"realloc\": %d, \"reads\": %ld, \"early\": %ld, \"destroy_max_us\": %lld}\n",
+           threads, rounds, ms, g_chain, g_realloc, g_total.load(), g_early.load(), g_destroy_max_us.load());
     return 0;
   }
   int khz = 0;
