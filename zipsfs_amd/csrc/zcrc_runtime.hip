@@ -520,10 +520,12 @@ class ScratchCache {
   // (entries inside it stay, over the budget, until a later release)
   void trim_locked(int dev) {
     uint64_t idle = 0;
-    bool any = false;
     for (ScratchEntry *x : entries_)
-      if (!x->busy && x->dev == dev) idle += x->cap, any |= freeable(x, dev);
-    if (idle <= budget_ || !any || !device_quiet(dev)) return;
+      if (!x->busy && x->dev == dev) idle += x->cap;
+    if (idle <= budget_) return;  // (the common case: no clock reads or event queries)
+    bool any = false;
+    for (ScratchEntry *x : entries_) any = any || freeable(x, dev);
+    if (!any || !device_quiet(dev)) return;
     while (idle > budget_) {
       ScratchEntry *lru = nullptr;
       for (ScratchEntry *x : entries_)
