@@ -85,10 +85,15 @@ int zcrc32_batch(const void *const *ptrs, const size_t *lens, const uint32_t *se
  * 8*ceil(n/8192) bytes; above 8192 buffers the split plan's layout instead,
  * 16*n + (312 + 24*n + 96*T rounded up to 16) bytes with T = ceil(n/(1024*p))
  * tiles, p the smallest of 1, 2, 4, 8 for which T <= 256) is a grow-only
- * buffer from a cache, leased per call and never shared between streams,
- * so streams may be created and destroyed freely; idle entries above
- * ZCRC_SCRATCH_CACHE_MIB (default 2048) per device are freed after a device
- * synchronize (stream-ordered allocations under graph capture).  Above 8192
+ * buffer from a cache, leased per call and never shared between streams
+ * (keyed by handle and, where the runtime has it, hipStreamGetId: a recycled
+ * handle gets fresh scratch), so streams may be created and destroyed
+ * freely; idle entries above ZCRC_SCRATCH_CACHE_MIB (default 2048) per
+ * device are freed after a device synchronize and 2 s idle (stream-ordered
+ * allocations under graph capture).  To read the results of work queued on a
+ * stream that is then destroyed, wait on an event recorded before the
+ * destroy: ROCm 7.2's hipDeviceSynchronize does not always wait for it
+ * (DESIGN.md 7e).  Above 8192
  * buffers the plan may
  * split the batch on the device: when buffers of at most 8 KiB are worth at
  * least two of the CRC kernel's workgroups, some workgroups of the same
