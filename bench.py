@@ -63,6 +63,7 @@ class Workload:
         import zipsfs_amd as z
         self.cfg, self.rank, self.world = cfg, rank, world
         self.batches = []  # list of (ptrs, lens) device tensors
+        self.regions = []  # per batch: (device address, bytes) of the contiguous region holding its buffers
         self.mem = []
         if cfg in (3, 5):
             n = n_override or (65536 if cfg == 3 else 131072)
@@ -96,6 +97,7 @@ class Workload:
                 z.fill_synthetic(ptrs[sl], lens[sl], index0=idx0, index_step=world, seed=PAYLOAD_SEED)
             self.mem.append(mem)
             self.batches.append((ptrs, lens))
+            self.regions.append((mem.data_ptr(), int(offs[-1] + L[-1]) // 16 * 16))
             self.n_local = len(L)
             self.n_total = 100000
             self.bytes_local = int(L.sum())
@@ -117,6 +119,7 @@ class Workload:
                              seed=PAYLOAD_SEED)
             self.mem.append(mem)
             self.batches.append((ptrs, lens))
+            self.regions.append((mem.data_ptr(), n * L))
         self.n_local = n
         self.n_total = n * self.world
         self.bytes_local = n * L
@@ -386,9 +389,11 @@ def main() -> None:
                          "RCCL path on a one-GPU box: init_process_group, all_gather on the device)")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="nccl = RCCL over xGMI (default); gloo only to rehearse ranks sharing one GPU")
-    ap.add_argument("--cpu-budget-s", type=float, default=12.0)
-    ap.add_argument("--cpu-sample-gib", type=float, default=4.0,
-                    help="host-resident CPU-baseline sample (>= 2x the host L3)")
+    ap.add_argument("--cpu-budget-s", type=float, default=None,
+                    help="CPU-baseline wall-clock budget (default 12 s at one rank, 24 s at N > 1)")
+    ap.add_argument("--cpu-sample-gib", type=float, default=None,
+                    help="host-resident CPU-baseline sample, >= 2x the host L3 (default 4 GiB at one rank; "
+                         "16 GiB of config 5 at N > 1, SURVEY 8(d))")
     ap.add_argument("--no-read-ceiling", action="store_true",
                     help="skip the same-process read ceiling (profiling runs: only the product kernel launches)")
     ap.add_argument("--host-resident-gib", type=float, default=4.0,
@@ -508,51 +513,89 @@ def main() -> None:
         except Exception as e:
             ceiling = {"error": f"{type(e).__name__}: {e}", "read_ceiling_gbs": None}
         extra_res = extra(wl, out.cpu().numpy().view(np.uint32)) if extra else None
+        per_rank = rank_spread(avg_kernel_ms, ceiling) if use_dist else None
         # the device path runs in one batch-kernel launch per step (the split
         # plan's small list, when it splits, runs inside it: zcrc_kernels.hip)
         res = {"wl_desc": wl.desc, "n_local": wl.n_local, "kernel": z.kernel_name_for(wl.n_local),
                "bytes_local": wl.bytes_local, "elapsed": elapsed, "bytes_all": bytes_all,
                "avg_kernel_ms": avg_kernel_ms, "kernel_timing": timing, "launches": launches, "parity": parity,
                "gathered_on": gathered_on, "bytes_main": wl.bytes_local, "small": None, "ceiling": ceiling,
-               "extra": extra_res}
+               "extra": extra_res, "per_rank": per_rank}
         del wl, out, result
         torch.cuda.empty_cache()
         return res
 
+    def rank_spread(avg_kernel_ms: float, ceiling: dict) -> dict:
+        """Min/max over ranks of each rank's own kernel time and read ceilings
+        (VERDICT r5 next #1): a straggling GPU shows in the one line rank 0
+        prints.  One all_gather of 3 float64 per rank."""
+        rdev = dev if args.dist_backend == "nccl" else torch.device("cpu")
+        nan = float("nan")
+        mine = torch.tensor([avg_kernel_ms, ceiling.get("read_ceiling_gbs") or nan,
+                             ceiling.get("stream_read_gbs") or nan], dtype=torch.float64, device=rdev)
+        allr = torch.empty(world * 3, dtype=torch.float64, device=rdev)
+        dist.all_gather_into_tensor(allr, mine)
+        a = allr.cpu().numpy().reshape(world, 3)
+        out = {}
+        for j, key in enumerate(("avg_kernel_ms", "read_ceiling_gbs", "stream_read_gbs")):
+            col = a[:, j]
+            if np.isnan(col).all():
+                out[key] = None
+                continue
+            out[key] = {"min": round(float(np.nanmin(col)), 4), "max": round(float(np.nanmax(col)), 4),
+                        "argmin_rank": int(np.nanargmin(col)), "argmax_rank": int(np.nanargmax(col))}
+        return out
+
     def read_ceiling(wl, out, steps: int) -> dict:
-        """The same-shape read ceiling: interleaved pairs
-        of `k` CRC launches and `k` launches of the ablated kernel
-        (zcrc32_batch_device_read_ceiling: the same plan, workgroups, loads and
-        fold, one VALU op per dword instead of the table lookups) over the same
-        batches, each block timed by one HIP event pair on the launch stream.
-        Judging the CRC by its ratio to the ceiling measured minutes apart in
-        the same process makes an A/B independent of the box's HBM rate."""
+        """Two ceilings over the same bytes, interleaved with the CRC in one
+        process: 3 rounds of k CRC launches,
+        k launches of the same-shape ceiling (zcrc32_batch_device_read_ceiling:
+        the same plan, workgroups, loads and fold, one VALU op per dword
+        instead of the table lookups) and k plain stream reads of the batch's
+        contiguous region (zcrc_read_sweep_device: one grid-stride sweep, no
+        per-buffer structure -- the chip's stream-read peak on these bytes),
+        each block timed by one HIP event pair on the launch stream, medians.
+        same-shape / stream-read is the access pattern's own loss; CRC /
+        same-shape what the CRC costs over its loads.  Ratios measured minutes
+        apart in one process make an A/B independent of the box's HBM rate."""
         k = max(5, steps // 2)
-        sink = torch.empty_like(out)
+        sink = torch.empty(max(out.numel(), 1024), dtype=torch.int32, device=out.device)
 
         def block(fn) -> float:
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
             for s in range(k):
-                ptrs, lens = wl.batches[s % len(wl.batches)]
-                fn(ptrs, lens)
+                b = s % len(wl.batches)
+                fn(b)
             e1.record()
             torch.cuda.synchronize()
             return e0.elapsed_time(e1) / k
 
-        crc = lambda p, l: z.crc32_batch_device(p, l, out=sink)
-        ceil = lambda p, l: z.batch_device_read_ceiling(p, l, out=sink)
-        block(ceil)  # warm the ablated kernel's code object
-        pairs = [(block(crc), block(ceil)) for _ in range(3)]
-        crc_ms = float(np.median([a for a, _ in pairs]))
-        ceil_ms = float(np.median([b for _, b in pairs]))
+        crc = lambda b: z.crc32_batch_device(*wl.batches[b], out=sink[:wl.n_local])
+        ceil = lambda b: z.batch_device_read_ceiling(*wl.batches[b], out=sink[:wl.n_local])
+        sweep = lambda b: z.read_sweep_device(wl.regions[b][0], wl.regions[b][1], sink)
+        block(ceil)  # warm both measurement kernels' code objects
+        block(sweep)
+        rounds = [(block(crc), block(ceil), block(sweep)) for _ in range(3)]
+        crc_ms = float(np.median([a for a, _, _ in rounds]))
+        ceil_ms = float(np.median([b for _, b, _ in rounds]))
+        sweep_ms = float(np.median([c for _, _, c in rounds]))
+        region = float(np.mean([r[1] for r in wl.regions]))
         gbs = wl.bytes_local / (ceil_ms * 1e-3) / 1e9
+        sgbs = region / (sweep_ms * 1e-3) / 1e9
         return {"read_ceiling_gbs": round(gbs, 1), "ceiling_ms": round(ceil_ms, 4),
+                "stream_read_gbs": round(sgbs, 1), "stream_read_ms": round(sweep_ms, 4),
+                "stream_read_bytes": int(region),
+                "ceiling_frac_of_stream_read": round(gbs / sgbs, 4),
                 "crc_ms_interleaved": round(crc_ms, 4), "frac_of_ceiling_interleaved": round(ceil_ms / crc_ms, 4),
-                "pairs_ms": [[round(a, 4), round(b, 4)] for a, b in pairs], "launches_per_block": k,
-                "method": "3 interleaved pairs of k CRC launches and k read-ceiling launches "
+                "frac_of_stream_read_interleaved": round((wl.bytes_local / (crc_ms * 1e-3) / 1e9) / sgbs, 4),
+                "rounds_ms": [[round(a, 4), round(b, 4), round(c, 4)] for a, b, c in rounds],
+                "launches_per_block": k,
+                "method": "3 interleaved rounds of k CRC launches, k same-shape read-ceiling launches "
                           "(zcrc32_batch_device_read_ceiling: same plan, loads and fold, table lookups "
-                          "replaced by one VALU op), HIP events per block, medians"}
+                          "replaced by one VALU op) and k stream reads of the batch's contiguous region "
+                          "(zcrc_read_sweep_device: grid-stride sweep, 1024-thread workgroup per CU, nt 16-B "
+                          "loads), HIP events per block, medians"}
 
     def host_resident(wl, crcs, n_host: int, reps: int) -> dict:
         """SURVEY 8(d)/north_star: the path starts and ends in host memory.
@@ -652,6 +695,8 @@ def main() -> None:
                 "workload": r["wl_desc"], "value": round(r["bytes_all"] * ks / r["elapsed"] / GiB, 2),
                 "read_ceiling_gbs": ce["read_ceiling_gbs"],
                 "frac_of_ceiling": round(ach / ce["read_ceiling_gbs"], 4) if ce["read_ceiling_gbs"] else None,
+                "stream_read_gbs": ce.get("stream_read_gbs"),
+                "frac_of_stream_read": round(ach / ce["stream_read_gbs"], 4) if ce.get("stream_read_gbs") else None,
                 "read_ceiling": ce,
                 "unit": "GiB/s", "steps": ks, "ms_per_step": round(r["elapsed"] / ks * 1e3, 4),
                 "avg_kernel_ms": round(r["avg_kernel_ms"], 4), "achieved": round(ach, 1),
@@ -671,9 +716,23 @@ def main() -> None:
     traffic_src = "--pmc-traffic-bytes" if traffic is not None else None
     if traffic is None:
         traffic, traffic_src = pmc_traffic(args.config, wl.bytes_local)
+    if use_dist:
+        # every rank's GPU work is done: leave the group, so that rank 0's CPU
+        # baseline below runs with the other ranks gone (no rank polling a
+        # barrier on the host cores it measures)
+        barrier()
+        dist.destroy_process_group()
+        use_dist_done = True
+    else:
+        use_dist_done = False
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(args.config, args.cpu_budget_s, args.cpu_sample_gib)
+    if rank == 0 and not args.no_cpu_baseline:
+        # N > 1 too: the reference timed on this box's
+        # host cores in the same run, over a fixed config-5 subset (SURVEY 8(d):
+        # 16 GiB by default at N > 1 -- global buffers 0 .. 16383)
+        sample_gib = args.cpu_sample_gib if args.cpu_sample_gib is not None else (4.0 if world == 1 else 16.0)
+        budget = args.cpu_budget_s if args.cpu_budget_s is not None else (12.0 if world == 1 else 24.0)
+        cpu = cpu_baseline(args.config, budget, sample_gib)
 
     if rank == 0:
         line = {
@@ -720,7 +779,11 @@ def main() -> None:
                 "read_ceiling_gbs": m["ceiling"]["read_ceiling_gbs"],
                 "frac_of_ceiling": (round(achieved / m["ceiling"]["read_ceiling_gbs"], 4)
                                     if m["ceiling"]["read_ceiling_gbs"] else None),
+                "stream_read_gbs": m["ceiling"].get("stream_read_gbs"),
+                "frac_of_stream_read": (round(achieved / m["ceiling"]["stream_read_gbs"], 4)
+                                        if m["ceiling"].get("stream_read_gbs") else None),
                 "read_ceiling": m["ceiling"],
+                "per_rank": m["per_rank"],
             },
             "cpu_baseline": cpu,
             "parity": parity,
@@ -732,7 +795,7 @@ def main() -> None:
             "device": torch.cuda.get_device_name(dev),
         }
         print(json.dumps(line), flush=True)
-    if use_dist:
+    if use_dist and not use_dist_done:
         dist.destroy_process_group()
 
 

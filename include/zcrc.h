@@ -89,11 +89,13 @@ int zcrc32_batch(const void *const *ptrs, const size_t *lens, const uint32_t *se
  * (keyed by handle and, where the runtime has it, hipStreamGetId: a recycled
  * handle gets fresh scratch), so streams may be created and destroyed
  * freely; idle entries above ZCRC_SCRATCH_CACHE_MIB (default 2048) per
- * device are freed after a device synchronize and 2 s idle (stream-ordered
- * allocations under graph capture).  To read the results of work queued on a
- * stream that is then destroyed, wait on an event recorded before the
- * destroy: ROCm 7.2's hipDeviceSynchronize does not always wait for it
- * (DESIGN.md 7e).  Above 8192
+ * device are freed by a library thread, after a device synchronize and 2 s
+ * idle, never on the caller's call (stream-ordered allocations under graph
+ * capture).  To read the results of work queued on a stream that is then
+ * destroyed, wait on an event recorded before the destroy: a plain-HIP
+ * reproducer on ROCm 7.2 read a wrong result after hipStreamDestroy and
+ * hipDeviceSynchronize when it re-allocated its memory between rounds
+ * (DESIGN.md 7e, 7f).  Above 8192
  * buffers the plan may
  * split the batch on the device: when buffers of at most 8 KiB are worth at
  * least two of the CRC kernel's workgroups, some workgroups of the same
@@ -111,8 +113,10 @@ int zcrc32_batch_device_ws(const void *const *d_ptrs, const uint64_t *d_lens,
                            void *d_scratch, size_t scratch_bytes, void *stream);
 
 /* Integrity check of the last zcrc32_batch_device / _ws launch on a scratch
- * (d_scratch, or NULL for the cached one the stream's last call used, while
- * no other stream has taken it since): synchronizes `stream`
+ * (d_scratch, or NULL for the cached scratch of the most recently finished
+ * zcrc32_batch_device call on `stream` -- scratch never changes streams; with
+ * two calls on one stream in flight at once it may be either's, and with
+ * none idle *faults is 0): synchronizes `stream`
  * and sets *faults nonzero when the CRC kernel found inconsistent length-
  * prefix bounds in the scratch (a corrupted scratch -- e.g. written by
  * another stream -- makes the kernel skip those buffers, with result 0,
@@ -309,6 +313,14 @@ int zcrc_cache_info(int dev, uint64_t *scratch_entries, uint64_t *scratch_bytes,
  * NOT receive CRCs. */
 int zcrc32_batch_device_read_ceiling(const void *const *d_ptrs, const uint64_t *d_lens, uint32_t *d_out, size_t n,
                                      void *stream);
+/* Measurement only: the chip's stream-read peak over the same bytes -- one
+ * plain grid-stride read of the contiguous device region [d_base, d_base +
+ * bytes) (16-byte aligned; a final < 16 B is not read), non-temporal 16-B
+ * loads, no CRC and no per-buffer structure (bench.py
+ * roofline.stream_read_gbs).  d_sink: device memory of at least 4096 bytes,
+ * written only in a case that does not matter (it keeps the loads alive).
+ * Asynchronous on `stream`. */
+int zcrc_read_sweep_device(const void *d_base, uint64_t bytes, uint32_t *d_sink, void *stream);
 
 /* Diagnostics / measurement. */
 /* Host staging pool: pinned bytes allocated (all devices), slots leased now,

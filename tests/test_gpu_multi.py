@@ -72,9 +72,38 @@ def test_config5_full_per_gpu_shard_through_rccl():
 @pytest.mark.timeout(300)
 def test_two_ranks_spawned_over_gloo_on_one_gpu():
     d = _bench_line(["--gpus", "2", "--dist-backend", "gloo", "--buffers-per-gpu", "32768",
-                     "--steps", "3", "--warmup", "1"])
+                     "--steps", "3", "--warmup", "1", "--cpu-sample-gib", "1", "--cpu-budget-s", "3"])
     assert d["ranks"] == 2 and d["n_gpus"] == 1
     assert d["collective"]["backend"] == "gloo"
     assert d["config"]["bytes_per_gpu_per_step"] == 32768 << 20
     # global buffers 0..65535, rank r holding i mod 2 == r: 512 fixtures
     assert d["parity"].startswith("512/512"), d["parity"]
+    assert d["cpu_baseline"]["kind"] in ("reference", "port") and d["cpu_baseline"]["value"] > 0
+    pr = d["roofline"]["per_rank"]
+    assert pr["avg_kernel_ms"]["min"] <= pr["avg_kernel_ms"]["max"]
+
+
+@pytest.mark.timeout(400)
+def test_eight_ranks_spawned_over_gloo_on_one_gpu():
+    """The driver's 8-GPU line rehearsed with 8 ranks sharing the one GPU
+    (VERDICT r5 next #1): the 8-way interleave of shard.gather_crcs (global
+    buffer i on rank i mod 8), the config-5 fixtures in global order, the
+    per-rank spread, rank 0's host batch over the device set, and the
+    reference CPU baseline that rank 0 times after the other ranks have left
+    (reference: one core per entry, src/ZIPsFS_preloadfileram.c:243)."""
+    d = _bench_line(["--gpus", "8", "--dist-backend", "gloo", "--buffers-per-gpu", "4096",
+                     "--steps", "2", "--warmup", "1", "--cpu-sample-gib", "2", "--cpu-budget-s", "4",
+                     "--host-resident-gib", "0.5"], timeout=380)
+    assert d["ranks"] == 8 and d["n_gpus"] == 1
+    assert d["collective"]["backend"] == "gloo" and d["collective"]["ranks"] == 8
+    assert d["config"]["buffers_per_gpu"] == 4096
+    # global buffers 0..32767, rank r holding i mod 8 == r: 256 fixtures
+    assert d["parity"].startswith("256/256"), d["parity"]
+    cb = d["cpu_baseline"]
+    assert cb is not None and cb["value"] > 0 and cb["kind"] in ("reference", "port"), cb
+    pr = d["roofline"]["per_rank"]
+    for key in ("avg_kernel_ms", "read_ceiling_gbs", "stream_read_gbs"):
+        assert pr[key] is not None and pr[key]["min"] <= pr[key]["max"], (key, pr)
+    hm = d["secondary"]["host_multi_device"]
+    assert "error" not in hm and hm["parity"].startswith("512/512"), hm
+    print("EIGHT_RANK_LINE " + json.dumps(d))

@@ -11,7 +11,7 @@ from .crc32 import (  # noqa: F401
     Crc32Stream, cg_crc32, crc32_batch, crc32_batch_device, crc32_batch_device_ws, crc32_batch_strided,
     crc32_combine, crc32_tensors, device_info, fhandle_check_crc32, fill_synthetic, profile,
     scratch_bytes, staging_info, prewarm, batch_device_faults, verify_entries, version, kernel_name, kernel_name_for, small_kernel_name, kernel_source_hash, inflate_batch_device, inflate_to_device, inflate_batch, inflate_device, INFLATE_STATUS,
-    device_set, shard_plan, batch_device_read_ceiling, release_cached, cache_info,
+    device_set, shard_plan, batch_device_read_ceiling, read_sweep_device, release_cached, cache_info,
 )
 
 __version__ = "0.1.0"

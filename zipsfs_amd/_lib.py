@@ -39,6 +39,7 @@ _SIGNATURES = {
     "zcrc32_batch_device_strided": (_c_int, [_c_p, _c_u64, _c_u64, _c_sz, _c_p, _c_p, _c_p]),
     "zcrc32_batch_device_faults": (_c_int, [_c_p, _c_p, ctypes.POINTER(_c_u32)]),
     "zcrc32_batch_device_read_ceiling": (_c_int, [_c_p, _c_p, _c_p, _c_sz, _c_p]),
+    "zcrc_read_sweep_device": (_c_int, [_c_p, _c_u64, _c_p, _c_p]),
     "zcrc_release_cached": (_c_int, [ctypes.POINTER(_c_u64)]),
     "zcrc_cache_info": (_c_int, [_c_int] + [ctypes.POINTER(_c_u64)] * 3),
     "zcrc32_combine": (_c_u32, [_c_u32, _c_u32, _c_u64]),

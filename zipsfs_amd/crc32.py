@@ -28,7 +28,7 @@ __all__ = [
     "crc32_batch_strided", "crc32_tensors", "crc32_combine", "fhandle_check_crc32",
     "verify_entries", "fill_synthetic", "profile", "device_info", "version",
     "inflate_batch_device", "inflate_to_device", "inflate_batch", "inflate_device", "INFLATE_STATUS",
-    "device_set", "shard_plan", "batch_device_read_ceiling", "release_cached", "cache_info",
+    "device_set", "shard_plan", "batch_device_read_ceiling", "read_sweep_device", "release_cached", "cache_info",
 ]
 
 
@@ -250,6 +250,18 @@ def batch_device_read_ceiling(ptrs, lens, out=None, stream=None):
     check(lib().zcrc32_batch_device_read_ceiling(ptrs.data_ptr(), lens.data_ptr(), out.data_ptr(), n,
                                                  _stream_ptr(stream)), "zcrc32_batch_device_read_ceiling")
     return out
+
+
+def read_sweep_device(base_ptr: int, nbytes: int, sink, stream=None) -> None:
+    """Measurement only (zcrc_read_sweep_device): one plain grid-stride read
+    of the contiguous device region [base_ptr, base_ptr + nbytes) -- the
+    stream-read peak the CRC and its same-shape ceiling are judged against.
+    ``sink``: a device tensor of >= 4096 bytes (receives nothing useful)."""
+    _check_dev(sink, "sink")
+    if sink.numel() * sink.element_size() < 4096:
+        raise ValueError("sink must hold >= 4096 bytes")
+    check(lib().zcrc_read_sweep_device(ctypes.c_void_p(int(base_ptr)), int(nbytes), sink.data_ptr(),
+                                       _stream_ptr(stream)), "zcrc_read_sweep_device")
 
 
 def release_cached() -> int:

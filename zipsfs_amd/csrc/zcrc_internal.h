@@ -124,6 +124,8 @@ const char *small_kernel_name(int lanes);
 // ablate: the read-ceiling variant (table lookups replaced by one VALU op; no CRCs)
 hipError_t launch_batch(const BatchArgs &args, bool strided, int num_cus, hipStream_t stream,
                         hipEvent_t t0 = nullptr, hipEvent_t t1 = nullptr, bool fused = false, bool ablate = false);
+// measurement only: the plain stream read of [d_base, d_base + bytes) (zcrc_read_sweep_device)
+hipError_t launch_read_sweep(const void *d_base, uint64_t bytes, uint32_t *d_sink, int num_cus, hipStream_t stream);
 inline uint64_t plan_tiles(uint64_t n) { return n == 0 ? 1 : (n + kPlanTile - 1) / kPlanTile; }
 const char *product_kernel_name();
 const char *fused_kernel_name();

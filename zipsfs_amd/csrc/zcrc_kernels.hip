@@ -503,6 +503,47 @@ const char *small_kernel_name(int lanes) {
                     : "zcrc::crc32_small_kernel<false, 16, 8, false, false, 0, 256>";
 }
 
+// ------------------------------------------------------- stream-read peak
+// Measurement only (zcrc_read_sweep_device): the fastest plain read of a
+// contiguous region found on this chip (round 5, tools/ceiling_probe part 3:
+// 4-6% above every CRC-compatible wave mapping on config 3's region).  One
+// 1024-thread workgroup per CU; each step a workgroup reads one 64 KiB chunk,
+// four non-temporal 16-B loads per thread 16 KiB apart, chunks grid-strided.
+// The ISA waits for the first load before issuing the other three, so each
+// wave has 1-3 KiB in flight.  The workgroup after the last whole chunk reads
+// the remaining 16-B granules; a final < 16 B is not read.  The xor of the
+// bytes is stored to sink[tid] only if it equals a constant (it never needs
+// to: the store keeps the loads alive).
+typedef uint32_t sweep_v4u __attribute__((ext_vector_type(4)));
+__global__ __launch_bounds__(1024) void read_sweep_kernel(const uint8_t *base, uint64_t bytes, uint32_t *sink) {
+  typedef const __attribute__((address_space(1))) sweep_v4u *gptr;
+  constexpr uint64_t kChunk = 1024u * 64u;
+  const uint64_t b0 = reinterpret_cast<uint64_t>(base);
+  const uint64_t full = bytes / kChunk;
+  uint32_t acc = 0;
+  for (uint64_t c = blockIdx.x; c < full; c += gridDim.x) {
+    const uint64_t o = c * kChunk + (uint64_t)threadIdx.x * 16u;
+    sweep_v4u v[4];
+#pragma unroll
+    for (int u = 0; u < 4; u++) v[u] = __builtin_nontemporal_load(reinterpret_cast<gptr>(b0 + o + 16384u * u));
+#pragma unroll
+    for (int u = 0; u < 4; u++) acc ^= v[u].x ^ v[u].y ^ v[u].z ^ v[u].w;
+  }
+  if (blockIdx.x == full % gridDim.x) {
+    for (uint64_t o = full * kChunk + (uint64_t)threadIdx.x * 16u; o + 16u <= bytes; o += 1024u * 16u) {
+      const sweep_v4u v = __builtin_nontemporal_load(reinterpret_cast<gptr>(b0 + o));
+      acc ^= v.x ^ v.y ^ v.z ^ v.w;
+    }
+  }
+  if (acc == 0x5EEDF00Du) sink[threadIdx.x] = acc;
+}
+
+hipError_t launch_read_sweep(const void *d_base, uint64_t bytes, uint32_t *d_sink, int num_cus, hipStream_t stream) {
+  hipLaunchKernelGGL(read_sweep_kernel, dim3((unsigned)num_cus), dim3(1024), 0, stream,
+                     static_cast<const uint8_t *>(d_base), bytes, d_sink);
+  return hipGetLastError();
+}
+
 hipError_t launch_plan(const uint64_t *d_lens, uint64_t n, uint64_t *d_prefix, uint64_t *d_tile_sum,
                        uint32_t *d_out, uint32_t *d_ctr, hipStream_t stream) {
   const uint64_t tiles = n == 0 ? 1 : (n + kPlanTile - 1) / kPlanTile;
