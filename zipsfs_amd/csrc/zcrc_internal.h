@@ -12,7 +12,10 @@ constexpr int kThreads = kWaves * 64;          // 1024
 // config: config 3 10.17 -> 10.05 ms, config 4 2.000 -> 1.983, config 2 48.4
 // -> 47.9 us (profiles/r05/depth_ab/); a plain sweep of the same region reads
 // fastest with few loads in flight per wave (profiles/r05/read_patterns/)
-constexpr uint32_t kDepth = 2;
+#ifndef ZCRC_DEPTH
+#define ZCRC_DEPTH 2
+#endif
+constexpr uint32_t kDepth = ZCRC_DEPTH;
 constexpr uint64_t kMinRange = 64ull << 10;    // default minimum bytes per wave range
 constexpr uint64_t kSplitGrain = 64ull << 10;  // split points: end-relative multiples
 constexpr uint64_t kSplitMin = 2 * kSplitGrain;  // buffers below this are never split
