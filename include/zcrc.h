@@ -104,6 +104,19 @@ int zcrc32_batch(const void *const *ptrs, const size_t *lens, const uint32_t *se
 int zcrc32_batch_device(const void *const *d_ptrs, const uint64_t *d_lens,
                         const uint32_t *d_seeds_or_null, uint32_t *d_out, size_t n, void *stream);
 
+/* Same, with a bound the caller knows for every length (max_len >= every
+ * d_lens[i]; 0 = unknown) -- ZIPsFS knows its entries' sizes from the
+ * central directory.  With max_len <= 8192 and more than 8192 buffers the
+ * batch runs in ONE small-buffer kernel launch over the caller's arrays
+ * (8 lanes per buffer up to 2 KiB, else 16), without the split plan's scans
+ * and scratch; otherwise exactly zcrc32_batch_device.  Results never depend
+ * on max_len: a longer buffer is still checksummed right, only slower.  Best
+ * for batches of about equal lengths (each wave takes 4 or 8 buffers in
+ * index order). */
+int zcrc32_batch_device_maxlen(const void *const *d_ptrs, const uint64_t *d_lens,
+                               const uint32_t *d_seeds_or_null, uint32_t *d_out, size_t n, uint64_t max_len,
+                               void *stream);
+
 /* Same, with caller-owned scratch (graph-capturable: no allocation inside).
  * Needs zcrc32_batch_device_scratch_bytes(n) bytes of device memory,
  * 256-byte aligned for best performance.  One scratch per in-flight call. */

@@ -382,3 +382,68 @@ def test_split_plan_lists_equal_the_model(n, shape):
     host = mem.cpu().numpy()
     exp = o.crc32_batch((host.ctypes.data + offs).astype(np.uint64), lens.astype(np.uint64), None, nthreads=16)
     np.testing.assert_array_equal(got, exp)
+
+
+def _device_batch(lead, lens, gap_rnd):
+    """Buffers laid out one after another (random 0-15 B gaps, misaligned
+    starts) in one device allocation: (mem, ptrs, lens tensor, offsets)."""
+    offs, pos = [], lead
+    for L in lens:
+        offs.append(pos)
+        pos += int(L) + gap_rnd.randrange(16)
+    mem = torch.randint(0, 256, (pos + 64,), dtype=torch.uint8, device=DEV)
+    ptrs = mem.data_ptr() + torch.tensor(offs, dtype=torch.int64, device=DEV)
+    return mem, ptrs, torch.tensor([int(x) for x in lens], dtype=torch.int64, device=DEV), offs
+
+
+@pytest.mark.parametrize("max_len", [1024, 2048, 4096, 8192])
+def test_maxlen_hint_mixed_small_lengths(max_len):
+    """zcrc32_batch_device_maxlen (round 6): a caller
+    bound <= 8 KiB runs the batch in one small-kernel launch over the
+    caller's arrays.  Mixed lengths 0..max_len at misaligned starts, with
+    seeds, n > 8192 -- bit-exact against the oracle and against the
+    unhinted call."""
+    rnd = random.Random(max_len)
+    n = 9000
+    lens = [rnd.randrange(max_len + 1) for _ in range(n)]
+    edge = [L for L in LENGTHS if L <= max_len]  # every boundary length up to the bound
+    lens[:len(edge)] = edge
+    mem, ptrs, lt, offs = _device_batch(5, lens, rnd)
+    seeds_np, seeds = _seeds(rnd, n)
+    got = u32(z.crc32_batch_device(ptrs, lt, seeds=seeds, max_len=max_len))
+    ref = u32(z.crc32_batch_device(ptrs, lt, seeds=seeds))
+    exp = _oracle(mem.cpu().numpy(), offs, lens, seeds_np)
+    np.testing.assert_array_equal(got, exp)
+    np.testing.assert_array_equal(ref, exp)
+
+
+def test_maxlen_hint_is_only_a_hint():
+    """Lengths above the caller's bound (up to 300 KiB) are still exact; so
+    are a bound of 0 (unknown), a bound above 8 KiB and n <= 8192 (both the
+    unhinted path)."""
+    rnd = random.Random(77)
+    n = 10000
+    lens = [rnd.randrange(1025) for _ in range(n)]
+    for k in range(0, n, 997):
+        lens[k] = rnd.choice([8193, 20000, 65536, 300000])
+    mem, ptrs, lt, offs = _device_batch(3, lens, rnd)
+    exp = _oracle(mem.cpu().numpy(), offs, lens, np.zeros(n, np.uint32))
+    for ml in (1024, 0, 65536):
+        np.testing.assert_array_equal(u32(z.crc32_batch_device(ptrs, lt, max_len=ml)), exp, err_msg=f"max_len {ml}")
+    np.testing.assert_array_equal(u32(z.crc32_batch_device(ptrs[:5000], lt[:5000], max_len=1024)), exp[:5000])
+
+
+def test_maxlen_uniform_golden_config2_shape():
+    """A whole-chip uniform 1 KiB batch (1 Mi buffers of the generator's
+    payload) through the hint: equal to the strided path everywhere and to
+    the oracle on a sample."""
+    L, n = 1024, 1 << 20
+    mem = torch.empty(n * L + 64, dtype=torch.uint8, device=DEV)
+    ptrs = mem.data_ptr() + torch.arange(n, dtype=torch.int64, device=DEV) * L
+    lens = torch.full((n,), L, dtype=torch.int64, device=DEV)
+    z.fill_synthetic(ptrs, lens, index0=9, seed=o.PAYLOAD_SEED)
+    got = u32(z.crc32_batch_device(ptrs, lens, max_len=L))
+    np.testing.assert_array_equal(got, u32(z.crc32_batch_strided(mem, L, L, n)))
+    sample = np.arange(0, n, 4099)
+    exp = np.array([o.payload_crc(L, 9 + int(i)) for i in sample], dtype=np.uint32)
+    np.testing.assert_array_equal(got[sample], exp)

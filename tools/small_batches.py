@@ -4,7 +4,9 @@ product entry points (measurement only).
 For each length, two distinct 1 GiB batches (rotated, so the MALL cannot serve
 repeats) are checksummed through zcrc32_batch_device (general form: device
 pointer and length arrays; above 8192 buffers the split plan routes buffers
-of <= 8 KiB to the small-buffer kernel) and zcrc32_batch_device_strided, with
+of <= 8 KiB to the small-buffer kernel), zcrc32_batch_device_maxlen (the
+caller's bound: one small-kernel launch, no plan) and
+zcrc32_batch_device_strided, with
 ZCRC_SMALL=1 (default) and 0 (batch kernel only).  Reported per call: the
 GPU time between two events on the stream around `reps` x 2 back-to-back
 calls (plans and launch gaps included; no per-launch events, which leave a
@@ -41,11 +43,16 @@ def main():
         ref = None
         for small in ("1", "0"):
             os.environ["ZCRC_SMALL"] = small
-            for api in ("device", "strided"):
+            for api in ("device", "device_maxlen", "strided"):
+                if api == "device_maxlen" and small == "0":
+                    continue  # (the hint is the small kernel's route)
+
                 def call(b):
                     mem, ptrs, lens = bat[b]
                     if api == "device":
                         return z.crc32_batch_device(ptrs, lens)
+                    if api == "device_maxlen":  # zcrc32_batch_device_maxlen: the caller's bound, no plan
+                        return z.crc32_batch_device(ptrs, lens, max_len=L)
                     return z.crc32_batch_strided(mem, L, L, n)
                 outs = [call(b) for b in range(2)]  # warm (scratch, first use)
                 torch.cuda.synchronize()

@@ -34,6 +34,7 @@ _SIGNATURES = {
     "zcrc_staging_info": (ctypes.c_int, [ctypes.POINTER(_c_u64)] * 4),
     "zcrc32_batch": (_c_int, [_c_p, _c_p, _c_p, _c_p, _c_sz, ctypes.c_uint]),
     "zcrc32_batch_device": (_c_int, [_c_p, _c_p, _c_p, _c_p, _c_sz, _c_p]),
+    "zcrc32_batch_device_maxlen": (_c_int, [_c_p, _c_p, _c_p, _c_p, _c_sz, _c_u64, _c_p]),
     "zcrc32_batch_device_scratch_bytes": (_c_sz, [_c_sz]),
     "zcrc32_batch_device_ws": (_c_int, [_c_p, _c_p, _c_p, _c_p, _c_sz, _c_p, _c_sz, _c_p]),
     "zcrc32_batch_device_strided": (_c_int, [_c_p, _c_u64, _c_u64, _c_sz, _c_p, _c_p, _c_p]),

@@ -214,10 +214,13 @@ def _check_seeds(seeds, n: int):
     return seeds.data_ptr()
 
 
-def crc32_batch_device(ptrs, lens, seeds=None, out=None, stream=None):
+def crc32_batch_device(ptrs, lens, seeds=None, out=None, stream=None, max_len=None):
     """Device-resident batch.  ``ptrs``/``lens``: int64 device tensors of n
     device addresses / byte counts; ``seeds``: optional int32/uint32 device
-    tensor; returns (or fills) an int32 device tensor of CRCs (uint32 bits)."""
+    tensor; returns (or fills) an int32 device tensor of CRCs (uint32 bits).
+    ``max_len``: a bound the caller knows for every length
+    (zcrc32_batch_device_maxlen: <= 8 KiB skips the split plan); results do
+    not depend on it."""
     torch = _torch()
     _check_dev(ptrs, "ptrs", torch.int64)
     _check_dev(lens, "lens", torch.int64)
@@ -228,6 +231,10 @@ def crc32_batch_device(ptrs, lens, seeds=None, out=None, stream=None):
         out = torch.empty(n, dtype=torch.int32, device=ptrs.device)
     _check_results(out, n)
     sp = _check_seeds(seeds, n)
+    if max_len is not None:
+        check(lib().zcrc32_batch_device_maxlen(ptrs.data_ptr(), lens.data_ptr(), sp, out.data_ptr(), n, int(max_len),
+                                               _stream_ptr(stream)), "zcrc32_batch_device_maxlen")
+        return out
     check(lib().zcrc32_batch_device(ptrs.data_ptr(), lens.data_ptr(), sp, out.data_ptr(), n, _stream_ptr(stream)),
           "zcrc32_batch_device")
     return out

@@ -2360,6 +2360,30 @@ int zcrc32_batch_device(const void *const *d_ptrs, const uint64_t *d_lens, const
   return batch_device_ws(d_ptrs, d_lens, d_seeds_or_null, d_out, n, scratch, have, st);
 }
 
+int zcrc32_batch_device_maxlen(const void *const *d_ptrs, const uint64_t *d_lens, const uint32_t *d_seeds_or_null,
+                               uint32_t *d_out, size_t n, uint64_t max_len, void *stream) {
+  // A caller that knows every length is at most 8 KiB (ZIPsFS: from the
+  // central directory) needs no split plan: the general-form small kernel
+  // walks the caller's arrays in one launch -- the plan's two scans and the
+  // gaps between three dependent launches were ~20 us of a 1 Mi x 1 KiB call
+  // (DESIGN.md 7f).  Small batches (n <= kFusedMaxN) keep the one-launch
+  // batch form.  The small body is exact for every length, so a length above
+  // the bound is still checksummed right, only on 8 or 16 lanes.
+  if (n <= kFusedMaxN || max_len == 0 || max_len > kSmallMax || !small_enabled())
+    return zcrc32_batch_device(d_ptrs, d_lens, d_seeds_or_null, d_out, n, stream);
+  if (!d_ptrs || !d_lens || !d_out) return fail(ZCRC_ERR_ARG, "null argument");
+  DeviceCtx *dc = nullptr;
+  if (const int rc = device_ctx(&dc)) return rc;
+  SmallArgs a{};
+  a.ptrs = reinterpret_cast<const uint8_t *const *>(d_ptrs);
+  a.lens = d_lens;
+  a.seeds = d_seeds_or_null;
+  a.out = d_out;
+  a.n = n;
+  a.tab = dc->d_tab;
+  return launch_small_timed(a, false, small_lanes(max_len), *dc, static_cast<hipStream_t>(stream));
+}
+
 int zcrc32_batch_device_read_ceiling(const void *const *d_ptrs, const uint64_t *d_lens, uint32_t *d_out, size_t n,
                                      void *stream) {
   t_read_ceiling = true;
