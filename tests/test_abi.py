@@ -160,6 +160,15 @@ def test_argument_errors_are_reported_not_computed():
     assert lib.zcrc32_batch_device(None, None, None, None, 5, None) == -2
     assert lib.zcrc32_batch(None, None, None, None, 3, 0) == -2
     assert lib.zcrc32_batch_device(None, None, None, None, 0, None) == 0  # empty batch: nothing to do
+    # the caller-bound form: its one-launch route and the unhinted one check alike
+    assert lib.zcrc32_batch_device_maxlen(None, None, None, None, 9000, 1024, None) == -2
+    assert lib.zcrc32_batch_device_maxlen(None, None, None, None, 5, 1024, None) == -2
+    assert lib.zcrc32_batch_device_maxlen(None, None, None, None, 9000, 0, None) == -2
+    # the stream-read measurement: null, misaligned (checked before any device work), empty
+    assert lib.zcrc_read_sweep_device(None, 4096, None, None) == -2
+    assert lib.zcrc_read_sweep_device(ctypes.c_void_p(0x1008), 4096, ctypes.c_void_p(0x2000), None) == -2
+    assert b"aligned" in lib.zcrc_last_error()
+    assert lib.zcrc_read_sweep_device(None, 0, None, None) == 0
     out = ctypes.c_uint32()
     assert lib.zcrc32_checked(None, 10, 0, ctypes.byref(out)) == -2
     assert b"null" in lib.zcrc_last_error()

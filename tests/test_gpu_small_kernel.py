@@ -384,7 +384,7 @@ def test_split_plan_lists_equal_the_model(n, shape):
     np.testing.assert_array_equal(got, exp)
 
 
-def _device_batch(lead, lens, gap_rnd):
+def _packed_batch(lead, lens, gap_rnd):
     """Buffers laid out one after another (random 0-15 B gaps, misaligned
     starts) in one device allocation: (mem, ptrs, lens tensor, offsets)."""
     offs, pos = [], lead
@@ -408,7 +408,7 @@ def test_maxlen_hint_mixed_small_lengths(max_len):
     lens = [rnd.randrange(max_len + 1) for _ in range(n)]
     edge = [L for L in LENGTHS if L <= max_len]  # every boundary length up to the bound
     lens[:len(edge)] = edge
-    mem, ptrs, lt, offs = _device_batch(5, lens, rnd)
+    mem, ptrs, lt, offs = _packed_batch(5, lens, rnd)
     seeds_np, seeds = _seeds(rnd, n)
     got = u32(z.crc32_batch_device(ptrs, lt, seeds=seeds, max_len=max_len))
     ref = u32(z.crc32_batch_device(ptrs, lt, seeds=seeds))
@@ -426,7 +426,7 @@ def test_maxlen_hint_is_only_a_hint():
     lens = [rnd.randrange(1025) for _ in range(n)]
     for k in range(0, n, 997):
         lens[k] = rnd.choice([8193, 20000, 65536, 300000])
-    mem, ptrs, lt, offs = _device_batch(3, lens, rnd)
+    mem, ptrs, lt, offs = _packed_batch(3, lens, rnd)
     exp = _oracle(mem.cpu().numpy(), offs, lens, np.zeros(n, np.uint32))
     for ml in (1024, 0, 65536):
         np.testing.assert_array_equal(u32(z.crc32_batch_device(ptrs, lt, max_len=ml)), exp, err_msg=f"max_len {ml}")
