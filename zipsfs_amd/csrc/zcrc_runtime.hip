@@ -417,6 +417,7 @@ class ScratchCache {
         if (!reaper_started_) {
           reaper_started_ = true;
           std::thread([this] { reaper_main(); }).detach();
+          std::atexit([] { ScratchCache::get().stop_reaper(); });
         }
       }
     }
@@ -653,17 +654,22 @@ class ScratchCache {
 
   // The reaper: trims devices that release() found over budget, and retries
   // those whose entries were still inside their grace (meanwhile release()
-  // does not wake it for them).  A detached thread that lives as long as the
-  // process (the cache is never destroyed).
+  // does not wake it for them).  A detached thread; at exit (atexit, before
+  // the HIP runtime's own teardown, which was registered first) it is stopped
+  // between trims, so that no synchronize or hipFree of it runs while the
+  // runtime is being torn down.
   void reaper_main() {
     std::unique_lock<std::mutex> lk(mu_);
     for (;;) {
+      if (stopping_) return;
       if (retry_.empty()) {
-        cv_.wait(lk, [&] { return !pending_.empty(); });
+        cv_.wait(lk, [&] { return !pending_.empty() || stopping_; });
+        if (stopping_) return;
       } else {
         Clock::time_point first = Clock::time_point::max();
         for (const auto &r : retry_) first = std::min(first, r.second);
-        cv_.wait_until(lk, first, [&] { return !pending_.empty(); });
+        cv_.wait_until(lk, first, [&] { return !pending_.empty() || stopping_; });
+        if (stopping_) return;
         const Clock::time_point now = Clock::now();
         for (auto it = retry_.begin(); it != retry_.end();) {
           if (it->second <= now) {
@@ -677,6 +683,7 @@ class ScratchCache {
       }
       const std::vector<int> devs(pending_.begin(), pending_.end());
       pending_.clear();  // (a release during the trim adds its device again and notifies)
+      trimming_ = true;
       lk.unlock();
       std::vector<std::pair<int, Clock::time_point>> later;
       for (const int d : devs) {
@@ -685,9 +692,22 @@ class ScratchCache {
         if (again != Clock::time_point{}) later.emplace_back(d, again);
       }
       lk.lock();
+      trimming_ = false;
+      cv_.notify_all();  // (stop_reaper may be waiting)
       for (const auto &r : later) retry_[r.first] = r.second;
     }
   }
+
+ public:
+  // process exit: no trim starts any more; one in progress is waited for
+  void stop_reaper() {
+    std::unique_lock<std::mutex> lk(mu_);
+    stopping_ = true;
+    cv_.notify_all();
+    cv_.wait(lk, [&] { return !trimming_; });
+  }
+
+ private:
 
   std::mutex mu_;
   std::condition_variable cv_;
@@ -696,7 +716,7 @@ class ScratchCache {
   std::unordered_map<int, uint64_t> idle_;  // idle bytes per device (a running count)
   std::set<int> pending_;                   // devices the reaper should trim now
   std::map<int, Clock::time_point> retry_;  // ... and later (entries inside their grace)
-  bool reaper_started_ = false;
+  bool reaper_started_ = false, stopping_ = false, trimming_ = false;
   uint64_t tick_ = 0, budget_ = 0;
 };
 
