@@ -90,8 +90,11 @@ int zcrc32_batch(const void *const *ptrs, const size_t *lens, const uint32_t *se
  * handle gets fresh scratch), so streams may be created and destroyed
  * freely; idle entries above ZCRC_SCRATCH_CACHE_MIB (default 2048) per
  * device are freed by a library thread, after a device synchronize and 2 s
- * idle, never on the caller's call (stream-ordered allocations under graph
- * capture).  To read the results of work queued on a stream that is then
+ * idle, never on the caller's call (calls under graph capture take
+ * stream-ordered allocations instead; a process that captures graphs in
+ * global mode while streams come and go should raise the budget or call
+ * zcrc_release_cached outside capture, since that synchronize is
+ * device-wide).  To read the results of work queued on a stream that is then
  * destroyed, wait on an event recorded before the destroy: a plain-HIP
  * reproducer on ROCm 7.2 read a wrong result after hipStreamDestroy and
  * hipDeviceSynchronize when it re-allocated its memory between rounds
