@@ -95,10 +95,10 @@ int zcrc32_batch(const void *const *ptrs, const size_t *lens, const uint32_t *se
  * global mode while streams come and go should raise the budget or call
  * zcrc_release_cached outside capture, since that synchronize is
  * device-wide).  To read the results of work queued on a stream that is then
- * destroyed, wait on an event recorded before the destroy: a plain-HIP
- * reproducer on ROCm 7.2 read a wrong result after hipStreamDestroy and
- * hipDeviceSynchronize when it re-allocated its memory between rounds
- * (DESIGN.md 7e, 7f).  Above 8192
+ * destroyed, wait on an event recorded before the destroy: on ROCm 7.2 a
+ * plain-HIP reproducer read the last kernel's store of a destroyed stream
+ * after hipStreamDestroy and hipDeviceSynchronize had returned, and found it
+ * there 200 ms later (5 reads in 1,400).  Above 8192
  * buffers the plan may
  * split the batch on the device: when buffers of at most 8 KiB are worth at
  * least two of the CRC kernel's workgroups, some workgroups of the same

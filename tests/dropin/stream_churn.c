@@ -71,10 +71,11 @@ static long g_checks = 0, g_fail = 0;
   } while (0)
 
 /* Destroy a stream with its work still queued, after recording `ev` on it.
- * The checks wait on the event, not on hipDeviceSynchronize: on ROCm 7.2
- * neither hipStreamDestroy nor a later hipDeviceSynchronize always waits for
- * work queued on a destroyed stream (round 5: results read after both arrived
- * 200 ms later; profiles/r05/stream_destroy/). */
+ * The checks wait on the event, not on hipDeviceSynchronize: on ROCm 7.2 a
+ * destroyed stream's last store can become visible only after
+ * hipStreamDestroy and a later hipDeviceSynchronize have returned (round 6:
+ * the right value 200 ms later, never another thread's;
+ * profiles/r06/s7/). */
 static int destroy_queued(hipStream_t s, hipEvent_t *ev) {
   if (hipEventCreateWithFlags(ev, hipEventDisableTiming) != hipSuccess) return -1;
   if (hipEventRecord(*ev, s) != hipSuccess) return -1;

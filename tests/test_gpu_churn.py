@@ -8,9 +8,9 @@ library's scratch is leased per call and keyed by the stream's handle and,
 where the HIP runtime has hipStreamGetId (ROCm >= 7.1, as a C process links
 it), its unique id (zcrc_runtime.hip, ScratchCache), so every result must be
 bit-exact (zlib is the checker).  The program waits for each destroyed
-stream's work on an event recorded before the destroy: on ROCm 7.2 neither
-hipStreamDestroy nor hipDeviceSynchronize always waits for it (round 5,
-profiles/r05/stream_destroy/).  With
+stream's work on an event recorded before the destroy: on ROCm 7.2 a
+destroyed stream's last store can become visible only after hipStreamDestroy
+and hipDeviceSynchronize have returned (round 6, profiles/r06/s7/).  With
 ZCRC_TL_EXACT=1 every thread-local device buffer is allocated at exactly the
 size asked, behind a canary the library checks after each call: an
 out-of-bounds write by the split inflate, the batch inflate or the ZIP

@@ -15,6 +15,7 @@
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
+#include <unistd.h>
 
 #define CHK(x)                                                                 \
   do {                                                                         \
@@ -42,6 +43,10 @@ __global__ void spin(unsigned *flag, unsigned tag, unsigned long long ticks) {
 #include <thread>
 #include <vector>
 static std::atomic<long> g_early{0}, g_total{0};
+// round 6: a wrong first read is read again 200 ms later
+// -- its own tag then: the store arrived late; another thread's tag: the
+// allocation was re-used and written; still the memset's 0: never written
+static std::atomic<long> g_late{0}, g_foreign{0}, g_never{0}, g_other{0};
 static std::atomic<long long> g_destroy_max_us{0};
 
 static int g_chain = 1, g_realloc = 0;
@@ -77,7 +82,17 @@ static void thread_rounds(int t, int rounds, double ms, int khz) {
     unsigned got = 0;
     CHK(hipMemcpy(&got, flag, 4, hipMemcpyDeviceToHost));
     g_total++;
-    if (got != tag) g_early++;
+    if (got != tag) {
+      g_early++;
+      usleep(200 * 1000);
+      unsigned again = 0;
+      CHK(hipMemcpy(&again, flag, 4, hipMemcpyDeviceToHost));
+      if (again == tag) g_late++;
+      else if (again == 0) g_never++;
+      else if ((again >> 16) != (unsigned)t) g_foreign++;
+      else g_other++;
+      fprintf(stderr, "thread %d round %d: tag %08x, first read %08x, 200 ms later %08x\n", t, r, tag, got, again);
+    }
   }
   CHK(hipDeviceSynchronize());
   CHK(hipFree(flag));
@@ -97,8 +112,10 @@ int main(int argc, char **argv) {
     for (int t = 0; t < threads && t < 16; t++) th.emplace_back(thread_rounds, t, rounds, ms, khz0);
     for (auto &x : th) x.join();
     printf("{\"threads\": %d, \"rounds\": %d, \"max_spin_ms\": %.1f, \"launches_per_stream\": %d, "
-           "\"realloc\": %d, \"reads\": %ld, \"early\": %ld, \"destroy_max_us\": %lld}\n",
-           threads, rounds, ms, g_chain, g_realloc, g_total.load(), g_early.load(), g_destroy_max_us.load());
+           "\"realloc\": %d, \"reads\": %ld, \"early\": %ld, \"late\": %ld, \"foreign\": %ld, "
+           "\"never\": %ld, \"other\": %ld, \"destroy_max_us\": %lld}\n",
+           threads, rounds, ms, g_chain, g_realloc, g_total.load(), g_early.load(), g_late.load(), g_foreign.load(),
+           g_never.load(), g_other.load(), g_destroy_max_us.load());
     return 0;
   }
   int khz = 0;

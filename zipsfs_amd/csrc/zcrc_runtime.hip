@@ -313,15 +313,15 @@ int launch_small_timed(const SmallArgs &args, bool strided, int lanes, const Dev
 // the caller's stream at the end of each lease -- while the caller still owns
 // it -- and are freed when it has completed; the device-batch entries (small
 // scratch; an event per call costs config 2 ~4 us, above) after a device
-// synchronize and kFreeGraceMs after their last lease.  The grace is a margin,
-// not a proof: round 5's plain-HIP reproducer (tools/stream_reuse_probe.hip,
-// s42) read a wrong flag after hipStreamDestroy + hipDeviceSynchronize only
-// when each round freed and re-allocated the flag (5 in 300 reads; 0 in 300
-// without), which does not tell late completion of a destroyed stream's work
-// from a write into a re-used allocation.  Round 6 queued 2.5 s of device
-// batches on a stream, destroyed it and freed its scratch at once
-// (tests/dropin/destroy_release.c): hipStreamDestroy itself waited for the
-// queued work, and every result was right.
+// synchronize and kFreeGraceMs after their last lease.  Why both: round 6's
+// plain-HIP reproducer (tools/stream_reuse_probe.hip,
+// profiles/r06/s7/) read the last kernel's store of a destroyed stream only
+// after hipStreamDestroy and hipDeviceSynchronize had returned (the memset's
+// value first, the kernel's own value 200 ms later; 5 reads in 1,400) -- the
+// synchronize does not cover a destroyed stream's last store, a grace much
+// longer than that window does.  hipStreamDestroy itself waits for the
+// queued work (2.5 s of queued batches: the destroy took 2,484 ms and every
+// result was right, tests/dropin/destroy_release.c).
 // Why cache at all: a hipMallocAsync/hipFreeAsync pair per call blocked the
 // host until the previous launch had finished (tools/host_overhead.py: 56 us
 // of host time per config-2 call, 8.6 us with reused scratch).
