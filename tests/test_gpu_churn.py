@@ -61,6 +61,16 @@ def test_streams_destroyed_between_calls_three_threads(tmp_path):
 
 
 @pytest.mark.timeout(300)
+def test_streams_destroyed_with_the_reaper_trimming_throughout(tmp_path):
+    """The same churn with a scratch budget of 0: every release wakes the
+    library's reaper thread, which synchronizes the device and frees the idle
+    scratch past its grace while three threads keep calling on fresh streams
+    (round 6: the trim left the callers' path)."""
+    d = _run(_build(tmp_path), 2, 3, {"ZCRC_SCRATCH_CACHE_MIB": "0"})
+    assert d["release_rc"] == 0 and d["entries_left"] == 0, d
+
+
+@pytest.mark.timeout(300)
 def test_exact_size_thread_local_buffers_with_canaries(tmp_path):
     """The same calls with exactly sized thread-local buffers and canaries."""
     _run(_build(tmp_path), 1, 2, {"ZCRC_TL_EXACT": "1"})

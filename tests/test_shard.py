@@ -1,4 +1,4 @@
-"""Multi-rank sharding + results gather on CPU (gloo, world_size 2 and 3)."""
+"""Multi-rank sharding + results gather on CPU (gloo, world_size 2, 3 and 8)."""
 import os
 import socket
 
@@ -37,7 +37,7 @@ def _worker(rank, world, port, n_total, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,n_total", [(2, 10), (2, 7), (3, 1000), (2, 1)])
+@pytest.mark.parametrize("world,n_total", [(2, 10), (2, 7), (3, 1000), (2, 1), (8, 32768), (8, 1003)])
 def test_gather_global_order(world, n_total):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
@@ -127,3 +127,19 @@ def test_bench_spawn_ranks_exit_codes(tmp_path):
         assert b.spawn_ranks(2, [str(tmp_path), "7"]) == 7
     finally:
         b.__file__ = orig
+
+
+def test_bench_n_gt_1_cpu_baseline_sample_and_8_rank_goldens():
+    """At N > 1 rank 0 times the reference over a fixed config-5 subset,
+    16 GiB by default: global buffers 0..16383 of the same payload (SURVEY
+    8(d)); 8 ranks x 4096 buffers (the GPU suite's rehearsal) hold 256
+    config-5 fixtures."""
+    b = _bench()
+    lens, idx, what = b.baseline_sample(5, 16 << 30)
+    assert len(lens) == 16384 and (lens == 1 << 20).all() and (idx == np.arange(16384)).all(), what
+    g = np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "configs.npz"))
+    n_total = 8 * 4096
+    glob = np.zeros(n_total, dtype=np.uint32)
+    keep = g["cfg5_idx"] < n_total
+    glob[g["cfg5_idx"][keep].astype(np.int64)] = g["cfg5"][keep]
+    assert b.golden_check(5, glob) == "256/256 sampled CRCs equal the reference golden vectors"
