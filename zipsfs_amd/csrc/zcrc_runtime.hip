@@ -474,14 +474,22 @@ class ScratchCache {
       for (const Snap &s : snap)
         if (all_.count(s.e) && !s.e->busy && s.e->tick == s.tick) take_locked(s.e, &victims);
     }
-    if (victims.empty()) return 0;
-    if (!device_quiet(dev)) {
-      give_back(victims);
-      return 0;
+    size_t freed = 0;
+    if (!victims.empty()) {
+      if (!device_quiet(dev)) {
+        give_back(victims);
+      } else {
+        for (ScratchEntry *x : victims)
+          if (x->done_ok && hipEventSynchronize(x->done) != hipSuccess) (void)hipGetLastError();  // (grace passed)
+        freed = free_entries(dev, victims);
+      }
     }
-    for (ScratchEntry *x : victims)
-      if (x->done_ok && hipEventSynchronize(x->done) != hipSuccess) (void)hipGetLastError();  // (grace passed)
-    return free_entries(dev, victims);
+    // entries of the snapshot the reaper took meanwhile are freed by the end
+    // of its current trim: wait for it, so that what was idle on entry is
+    // gone on return
+    std::unique_lock<std::mutex> lk(mu_);
+    cv_.wait(lk, [&] { return !trimming_; });
+    return freed;
   }
 
   void info(int dev, uint64_t *entries, uint64_t *bytes) {
