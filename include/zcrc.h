@@ -94,7 +94,9 @@ int zcrc32_batch(const void *const *ptrs, const size_t *lens, const uint32_t *se
  * stream-ordered allocations instead; a process that captures graphs in
  * global mode while streams come and go should raise the budget or call
  * zcrc_release_cached outside capture, since that synchronize is
- * device-wide).  To read the results of work queued on a stream that is then
+ * device-wide: measured, ~30 trims invalidated 8 of ~790 global-mode captures
+ * held open next to them, with or without the library thread in relaxed
+ * capture mode; without trims none).  To read the results of work queued on a stream that is then
  * destroyed, wait on an event recorded before the destroy: on ROCm 7.2 a
  * plain-HIP reproducer read the last kernel's store of a destroyed stream
  * after hipStreamDestroy and hipDeviceSynchronize had returned, and found it

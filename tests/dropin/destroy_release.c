@@ -19,6 +19,16 @@
  *   ~0.5 s of queued batches while 48 fresh streams each run a batch and are
  *   destroyed; the library's reaper must free their idle scratch by itself,
  *   and no call may wait for the device (each returns in milliseconds).
+ * Mode "capture": 48 fresh streams each run a batch and are destroyed, 30 ms
+ *   apart; then, for `seconds` (default 3.5, past the scratch grace), the
+ *   main thread captures graphs back to back in GLOBAL capture mode
+ *   (torch.cuda.graph's default) -- each a memset and a
+ *   zcrc32_batch_device_ws with caller scratch, the capture held open 4 ms --
+ *   and replays them.  Counts the captures that fail (a synchronize or
+ *   hipFree of another thread invalidates a global-mode capture), checks
+ *   every replay.  With ZCRC_SCRATCH_CACHE_MIB=1 the reaper trims the
+ *   destroyed streams' scratch some 30 times during the loop
+ *   (tools/capture_ab.sh); with the default budget it never trims.
  * Output: one JSON line; exit status 1 on any mismatch or error.  The
  * reference's call site: src/ZIPsFS_preloadfileram.c:243 (ZIPsFS runs up to
  * 32 preload threads, src/ZIPsFS_async.c:468). */
@@ -291,8 +301,115 @@ static int mode_trim(void) {
   return bad ? 1 : 0;
 }
 
+static int mode_capture(double seconds) {
+  hipStream_t s0;
+  HIPCHK(hipStreamCreateWithFlags(&s0, hipStreamNonBlocking));
+  Batch mid;
+  batch_make(&mid, 8192, 65536, s0);
+  int dev = 0;
+  HIPCHK(hipGetDevice(&dev));
+  uint32_t *d_m = NULL, *h = malloc(4 * mid.n);
+  HIPCHK(hipMalloc((void **)&d_m, 4 * mid.n * 48));
+  /* 48 destroyed streams' scratch, released 30 ms apart: their graces end
+     one after another inside the capture loop below, so the reaper trims
+     (device synchronize + hipFree) some 30 times while graphs are captured */
+  for (int i = 0; i < 48; i++) {
+    hipStream_t s;
+    HIPCHK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    ZCHK(zcrc32_batch_device((const void *const *)mid.ptrs, mid.lens, NULL, d_m + (size_t)i * mid.n, mid.n, s));
+    hipEvent_t ev;
+    HIPCHK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+    HIPCHK(hipEventRecord(ev, s));
+    HIPCHK(hipStreamDestroy(s));
+    HIPCHK(hipEventSynchronize(ev));
+    HIPCHK(hipEventDestroy(ev));
+    usleep(30 * 1000);
+  }
+  uint64_t bytes_before = 0;
+  ZCHK(zcrc_cache_info(dev, NULL, &bytes_before, NULL));
+  /* graphs captured back to back in global mode while the reaper works */
+  const size_t sb = zcrc32_batch_device_scratch_bytes(mid.n);
+  void *d_scr = NULL;
+  uint32_t *d_g = NULL;
+  HIPCHK(hipMalloc(&d_scr, sb));
+  HIPCHK(hipMalloc((void **)&d_g, 4 * mid.n));
+  hipStream_t sc;
+  HIPCHK(hipStreamCreateWithFlags(&sc, hipStreamNonBlocking));
+  long captures = 0, capture_fail = 0, replays = 0;
+  size_t bad = 0;
+  double trimmed_at = -1, first_fail_at = -1;
+  hipError_t first_err = hipSuccess;
+  const char *first_what = "";
+  const double t0 = now_ms();
+  while (now_ms() - t0 < seconds * 1e3) {
+    hipGraph_t g = NULL;
+    hipGraphExec_t ge = NULL;
+    const hipError_t eb = hipStreamBeginCapture(sc, hipStreamCaptureModeGlobal);
+    if (eb != hipSuccess) {
+      captures++, capture_fail++;
+      if (first_fail_at < 0) first_fail_at = now_ms() - t0, first_err = eb, first_what = "begin";
+      (void)hipGetLastError();
+      hipGraph_t gx = NULL;
+      (void)hipStreamEndCapture(sc, &gx);
+      (void)hipGetLastError();
+      if (gx) (void)hipGraphDestroy(gx);
+      (void)hipStreamDestroy(sc);
+      HIPCHK(hipStreamCreateWithFlags(&sc, hipStreamNonBlocking));
+      continue;
+    }
+    const hipError_t em = hipMemsetAsync(d_g, 0, 4 * mid.n, sc);
+    const int zr = zcrc32_batch_device_ws((const void *const *)mid.ptrs, mid.lens, NULL, d_g, mid.n, d_scr, sb, sc);
+    usleep(4000); /* the capture stays open most of the loop's time */
+    const hipError_t ee = hipStreamEndCapture(sc, &g);
+    captures++;
+    if (em != hipSuccess || zr || ee != hipSuccess || !g) {
+      capture_fail++;
+      if (first_fail_at < 0) {
+        first_fail_at = now_ms() - t0;
+        first_err = em != hipSuccess ? em : ee;
+        first_what = em != hipSuccess ? "memset" : zr ? zcrc_last_error() : "end";
+      }
+      (void)hipGetLastError();
+      if (g) (void)hipGraphDestroy(g);
+      continue;
+    }
+    HIPCHK(hipGraphInstantiate(&ge, g, NULL, NULL, 0));
+    HIPCHK(hipGraphLaunch(ge, sc));
+    HIPCHK(hipStreamSynchronize(sc));
+    HIPCHK(hipMemcpy(h, d_g, 4 * mid.n, hipMemcpyDeviceToHost));
+    bad += count_bad(h, mid.href, mid.n);
+    replays++;
+    HIPCHK(hipGraphExecDestroy(ge));
+    HIPCHK(hipGraphDestroy(g));
+    uint64_t b = 0;
+    ZCHK(zcrc_cache_info(dev, NULL, &b, NULL));
+    if (trimmed_at < 0 && b <= (2u << 20)) trimmed_at = now_ms() - t0;
+  }
+  const double loop_ms = now_ms() - t0;
+  /* the reaper may have had to wait for a gap between captures: let it finish */
+  uint64_t entries = 0, bytes = 0;
+  for (int k = 0; k < 60; k++) {
+    ZCHK(zcrc_cache_info(dev, &entries, &bytes, NULL));
+    if (bytes <= (2u << 20)) break;
+    usleep(100 * 1000);
+  }
+  HIPCHK(hipDeviceSynchronize());
+  for (int i = 0; i < 48; i++) {
+    HIPCHK(hipMemcpy(h, d_m + (size_t)i * mid.n, 4 * mid.n, hipMemcpyDeviceToHost));
+    bad += count_bad(h, mid.href, mid.n);
+  }
+  free(h);
+  printf("{\"mode\": \"capture\", \"loop_ms\": %.0f, \"captures\": %ld, \"capture_fail\": %ld, "
+         "\"first_fail_ms\": %.0f, \"first_error\": \"%s\", \"first_fail_in\": \"%s\", \"replays\": %ld, \"bytes_before\": %llu, "
+         "\"trimmed_during_loop_ms\": %.0f, \"bytes_after\": %llu, \"entries_after\": %llu, \"mismatches\": %zu}\n",
+         loop_ms, captures, capture_fail, first_fail_at, hipGetErrorName(first_err), first_what, replays,
+         (unsigned long long)bytes_before, trimmed_at, (unsigned long long)bytes, (unsigned long long)entries, bad);
+  return bad || capture_fail ? 1 : 0;
+}
+
 int main(int argc, char **argv) {
   const char *mode = argc > 1 ? argv[1] : "destroy";
   if (!strcmp(mode, "trim")) return mode_trim();
+  if (!strcmp(mode, "capture")) return mode_capture(argc > 2 ? atof(argv[2]) : 3.5);
   return mode_destroy(argc > 2 ? atof(argv[2]) : 2.5);
 }

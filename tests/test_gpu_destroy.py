@@ -13,7 +13,13 @@ preload threads: src/ZIPsFS_async.c:468).
 * hipStreamPerThread and the null stream as the caller's stream.
 * With a 1 MiB budget, 48 destroyed streams' scratch is freed by the
   library's own reaper thread while a live stream holds ~0.5 s of queued
-  work, and no call waits for the device."""
+  work, and no call waits for the device.
+* Graphs captured back to back in global capture mode (torch.cuda.graph's
+  default), each holding a zcrc32_batch_device_ws, next to 48 destroyed
+  streams' idle scratch: below the idle budget (no trims) no capture is
+  invalidated and every replay is bit-exact.  (Above it, a trim's
+  synchronize and hipFree do invalidate a concurrent global-mode capture:
+  measured in tools/capture_ab.sh)"""
 import json
 import os
 import subprocess
@@ -63,3 +69,11 @@ def test_reaper_trims_destroyed_streams_without_blocking_callers(tmp_path):
     assert d["bytes_after"] <= (2 << 20), d  # the reaper freed the destroyed streams' scratch by itself
     assert d["peak_entries"] > 4, d
     assert d["worst_call_ms"] < 250, d  # no call waited for the ~0.5 s queued on the live stream
+
+
+@pytest.mark.timeout(200)
+def test_global_mode_captures_next_to_the_cache(tmp_path):
+    d = _run([_build(tmp_path), "capture", "3.5"], {"ZCRC_SCRATCH_CACHE_MIB": "2048"})
+    assert d["capture_fail"] == 0 and d["replays"] == d["captures"] > 100, d
+    assert d["mismatches"] == 0, d
+    assert d["entries_after"] >= 48, d  # below the budget: nothing trimmed, the destroyed streams' scratch kept
