@@ -1,0 +1,344 @@
+// tools/sweepcrc_probe.hip -- the CRC in the stream-read sweep's mapping, with
+// a fold the LDS can afford (measurement only; round 6).
+//
+// The sweep (zcrc_read_sweep_device) reads config 3's 64 GiB 2-5% faster
+// than every per-wave mapping the CRC can use: one
+// 1024-thread workgroup per CU takes 64 KiB chunks grid-strided, wave w the
+// 1 KiB blocks w, w+16, w+32, w+48 of the chunk, first block alone, a wait,
+// then the other three.  Session 3's probe put the product's fold on that
+// mapping (every wave folds its 256 dword streams per 4 KiB) and ran 34%
+// slower: the fold's combine tables are not replicated, so their lookups of
+// random values conflict ~3.5-way in the LDS banks and the fold alone needed
+// more LDS cycles than the stream.
+//
+// This probe's fold is conflict-free by layout:
+//   * braid MCT(x^(8*16384)) (streams advance 16 KiB per block) replicated
+//     16x with lanes 16-31 of each LDS group looking up byte j^1 through
+//     table j^1 (tools/lean_probe's layout): 64 KiB;
+//   * in-lane fold as Horner in x^-32 through a 4-bit table replicated for
+//     the 32 banks (lane l reads bank l & 31): 16 KiB;
+//   * the lane's register moved by x^(-128 l) through a per-lane 4-bit
+//     table in lane l's bank: 32 KiB;
+//   * the cross-lane sum by DPP/readlane; the wave's share moved to its
+//     buffer's end by a per-wave constant (wave w of workgroup g always
+//     takes the same place of the same chunk index g mod 16 of a 1 MiB
+//     buffer) through a 4-bit table read with a uniform address: 8 KiB;
+//   * one atomicXor per wave and chunk into the zeroed result (the buffer's
+//     seed ~0 injected in its first word, the final complement folded into
+//     one wave's share).
+// Variants, config 3's 64 GiB (65,536 x 1 MiB, synthetic payload), same
+// process, dispatch-packet timestamps:
+//   sweep        the stream-read sweep (pure read)
+//   crc-product  the product's strided config-3 kernel (+ its result memset)
+//   sweep-crc    this kernel (+ its result memset)
+// sweep-crc's 65,536 results are compared with the product's.
+//
+//   make -C tools sweepcrc_probe && tools/sweepcrc_probe [reps]
+#include <hip/hip_ext.h>
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+
+#include <algorithm>
+#include <vector>
+
+#include "../zipsfs_amd/csrc/zcrc_batch_kernel.h"
+#include "../zipsfs_amd/csrc/zcrc_tables.h"
+
+#define CHECK(x)                                                                               \
+  do {                                                                                         \
+    hipError_t e_ = (x);                                                                       \
+    if (e_ != hipSuccess) {                                                                    \
+      fprintf(stderr, "%s:%d %s: %s\n", __FILE__, __LINE__, #x, hipGetErrorString(e_));        \
+      exit(1);                                                                                 \
+    }                                                                                          \
+  } while (0)
+
+using namespace zcrc;
+
+typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+typedef const __attribute__((address_space(1))) v4u *gv4u;
+
+constexpr uint64_t kN = 65536, kLen = 1u << 20, kBytes = kN * kLen;
+constexpr uint32_t kChunk = 65536, kChunksPerBuf = kLen / kChunk;  // 16
+
+// global table blob of the probe (host-built)
+struct SweepTabs {
+  uint32_t braid[4 * 256];          // MCT(x^(8*16384))
+  uint32_t in32[8 * 16];            // 4-bit tables of x^-32
+  uint32_t cross[64][8 * 16];       // lane l: 4-bit tables of x^(-8*16*l)
+  uint32_t kw[16][16][8 * 16];      // [chunk index m][wave w]: x^(-8*1024*w) * x^(8*65536*(15-m))
+};
+
+// LDS layout (dwords)
+constexpr uint32_t kLB = 0;                  // braid x16: 16,384
+constexpr uint32_t kLC = 16384;              // cross, per lane: 2 x 128 x 32 = 8,192
+constexpr uint32_t kLI = kLC + 8192;         // in32, per bank: 128 x 32 = 4,096
+constexpr uint32_t kLK = kLI + 4096;         // kw for this workgroup's m: 16 x 128 = 2,048
+constexpr uint32_t kLdsDw = kLK + 2048;      // 30,720 dwords = 120 KiB
+
+// r * c through 4-bit tables at LDS dword base t: entry (i, nib) at t + (i*16+nib)*stride
+template <uint32_t kStride>
+__device__ __forceinline__ uint32_t nib_mul(const uint32_t *lds, uint32_t t, uint32_t r) {
+  uint32_t a = 0;
+#pragma unroll
+  for (uint32_t i = 0; i < 8; i++) a ^= lds[t + (i * 16u + ((r >> (4 * i)) & 15u)) * kStride];
+  return a;
+}
+
+template <bool kCrc, bool kEarly = false>
+__global__ __launch_bounds__(1024) void sweep_crc(const uint8_t *base, const SweepTabs *tabs, uint32_t *out) {
+  __shared__ __attribute__((aligned(16))) uint32_t s_lds[kLdsDw];
+  const uint32_t tid = threadIdx.x, lane = tid & 63u, wv = uni32(tid >> 6);
+  const uint32_t m = blockIdx.x % kChunksPerBuf;  // this workgroup's chunk index in every buffer (256 % 16 == 0)
+  if (kCrc) {
+    // braid x16 (byte v*256 + j*64 + r*4), four replicas per 16-B write
+    uint4 *dst = reinterpret_cast<uint4 *>(s_lds + kLB);
+#pragma unroll
+    for (uint32_t k = 0; k < 4; k++) {
+      const uint32_t c = tid + 1024u * k;
+      const uint32_t v = tabs->braid[((c >> 2) & 3u) * 256u + (c >> 4)];
+      dst[c] = make_uint4(v, v, v, v);
+    }
+    // cross: dword kLC + (l>>5)*4096 + e*32 + (l&31), e = i*16+nib; thread t
+    // writes 8 of the 8,192
+#pragma unroll
+    for (uint32_t k = 0; k < 8; k++) {
+      const uint32_t d = tid + 1024u * k, hi = d >> 12, e = (d >> 5) & 127u, l = (hi << 5) | (d & 31u);
+      s_lds[kLC + d] = tabs->cross[l][e];
+    }
+#pragma unroll
+    for (uint32_t k = 0; k < 4; k++) {
+      const uint32_t d = tid + 1024u * k;
+      s_lds[kLI + d] = tabs->in32[d >> 5];
+    }
+#pragma unroll
+    for (uint32_t k = 0; k < 2; k++) {
+      const uint32_t d = tid + 1024u * k;
+      s_lds[kLK + d] = tabs->kw[m][d >> 7][d & 127u];
+    }
+    __syncthreads();
+  }
+  const uint32_t sw = (lane >> 4) & 1u, rep = (lane & 15u) * 4u;
+  uint32_t o[4], sel[4];
+#pragma unroll
+  for (int j = 0; j < 4; j++) {
+    const uint32_t jj = (uint32_t)j ^ sw;
+    o[j] = jj * 64u + rep;
+    sel[j] = 0x0C020400u + (jj << 8);
+  }
+  const uint32_t cl = kLC + (lane >> 5) * 4096u + (lane & 31u);
+  const uint32_t ci = kLI + (lane & 31u);
+  const uint32_t ck = kLK + wv * 128u;
+  const uint64_t b0 = reinterpret_cast<uint64_t>(base) + 1024u * wv + 16u * lane;
+  const uint64_t nchunks = kBytes / kChunk;
+  uint32_t acc = 0;
+  auto step = [&](uint32_t &s, uint32_t &q, uint32_t d) {
+    const uint32_t x = __builtin_amdgcn_bitop3_b32(s, q, d, 0x96);
+    const uint32_t t0 = lds_u32(s_lds, __builtin_amdgcn_perm(x, o[0], sel[0]));
+    const uint32_t t1 = lds_u32(s_lds, __builtin_amdgcn_perm(x, o[1], sel[1]));
+    const uint32_t t2 = lds_u32(s_lds, __builtin_amdgcn_perm(x, o[2], sel[2]));
+    q = lds_u32(s_lds, __builtin_amdgcn_perm(x, o[3], sel[3]));
+    s = __builtin_amdgcn_bitop3_b32(t0, t1, t2, 0x96);
+  };
+  uint64_t c = blockIdx.x;
+  v4u v0 = c < nchunks ? __builtin_nontemporal_load(reinterpret_cast<gv4u>(b0 + c * kChunk)) : v4u{0, 0, 0, 0};
+  // The share of chunk c is xored into its result during the NEXT chunk,
+  // just before that chunk's successor's first block is requested: a
+  // wait for the first block (vmcnt(0): the compiler cannot count past the
+  // lane-0 branch) then also covers the atomic, which has long completed --
+  // round 1 of this probe issued the atomic last and every chunk's first
+  // wait waited for its round trip.
+  uint32_t prev_share = 0;
+  uint64_t prev_b = ~0ull;
+  v4u v0n = v4u{0, 0, 0, 0};
+  for (; c < nchunks; c += gridDim.x) {
+    const uint64_t a = b0 + c * kChunk;
+    if (!kCrc) __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the chunk's first block has landed
+    uint32_t s0 = 0, s1 = 0, s2 = 0, s3 = 0, q0 = 0, q1 = 0, q2 = 0, q3 = 0;
+    if (kCrc) {
+      // consuming the first block waits for it; only then do the other
+      // three go out (the sweep's issue order).  The buffer's seed (~0) in
+      // its first word: chunk 0, wave 0, lane 0, block 0.
+      if (m == 0 && wv == 0 && lane == 0) v0.x ^= 0xFFFFFFFFu;
+      step(s0, q0, v0.x);
+      step(s1, q1, v0.y);
+      step(s2, q2, v0.z);
+      step(s3, q3, v0.w);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    v4u v[3];
+#pragma unroll
+    for (int u = 0; u < 3; u++) v[u] = __builtin_nontemporal_load(reinterpret_cast<gv4u>(a + 16384u * (u + 1)));
+    const uint64_t cn = c + gridDim.x;
+    const uint64_t cnext = cn < nchunks ? cn : c;  // (re-read at the end: keeps the load unconditional)
+    if (kCrc && kEarly) {
+      // kEarly: the next chunk's first block goes out right behind this
+      // chunk's other three (up to 4 KiB in flight per wave), so the braid
+      // steps and the fold overlap its latency too
+      if (prev_b != ~0ull && lane == 0) atomicXor(out + prev_b, prev_share);
+      prev_b = ~0ull;
+      v0n = __builtin_nontemporal_load(reinterpret_cast<gv4u>(b0 + cnext * kChunk));
+      __asm__ volatile("" ::: "memory");
+    }
+    if (!kCrc) {
+      acc ^= v0.x ^ v0.y ^ v0.z ^ v0.w;
+#pragma unroll
+      for (int u = 0; u < 3; u++) acc ^= v[u].x ^ v[u].y ^ v[u].z ^ v[u].w;
+      v0 = __builtin_nontemporal_load(reinterpret_cast<gv4u>(b0 + cnext * kChunk));
+      continue;
+    }
+#pragma unroll
+    for (int u = 0; u < 3; u++) {
+      step(s0, q0, v[u].x);
+      step(s1, q1, v[u].y);
+      step(s2, q2, v[u].z);
+      step(s3, q3, v[u].w);
+    }
+    if (!kEarly) {
+      if (prev_b != ~0ull && lane == 0) atomicXor(out + prev_b, prev_share);
+      v0 = __builtin_nontemporal_load(reinterpret_cast<gv4u>(b0 + cnext * kChunk));
+      // keep the load here, in front of the fold (the compiler otherwise sinks
+      // it to the loop head, right before its wait)
+      __asm__ volatile("" ::: "memory");
+    } else {
+      v0 = v0n;
+    }
+    s0 ^= q0, s1 ^= q1, s2 ^= q2, s3 ^= q3;
+    // stream (l, k) sits at chunk end + 1024 w + 16 l + 4 k
+    uint32_t r = nib_mul<32>(s_lds, ci, s3) ^ s2;
+    r = nib_mul<32>(s_lds, ci, r) ^ s1;
+    r = nib_mul<32>(s_lds, ci, r) ^ s0;  // at + 16 l
+    r = nib_mul<32>(s_lds, cl, r);        // at + 0 (chunk end + 1024 w)
+    r ^= row_shl<1>(r);
+    r ^= row_shl<2>(r);
+    r ^= row_shl<4>(r);
+    r ^= row_shl<8>(r);
+    const uint32_t x = uni32(r) ^ (uint32_t)__builtin_amdgcn_readlane((int)r, 16) ^
+                       (uint32_t)__builtin_amdgcn_readlane((int)r, 32) ^
+                       (uint32_t)__builtin_amdgcn_readlane((int)r, 48);
+    prev_share = uni32(nib_mul<1>(s_lds, ck, x));  // at the buffer's end
+    if (m == kChunksPerBuf - 1 && wv == 0) prev_share ^= 0xFFFFFFFFu;  // the final complement, once per buffer
+    prev_b = c / kChunksPerBuf;
+  }
+  if (kCrc && prev_b != ~0ull && lane == 0) atomicXor(out + prev_b, prev_share);
+  if (!kCrc && acc == 0x12345678u) out[tid] = acc;
+}
+
+static void build_probe_tabs(SweepTabs &t) {
+  XPowTable xp;
+  build_xpow_table(xp);
+  build_mct(gf2_xpow8(xp, 16384), t.braid);
+  auto nib = [](uint32_t c, uint32_t *dst) {
+    for (uint32_t i = 0; i < 8; i++)
+      for (uint32_t v = 0; v < 16; v++) dst[i * 16 + v] = gf2_mul(c, v << (4 * i));
+  };
+  nib(gf2_xinvpow8_small(4), t.in32);
+  for (uint32_t l = 0; l < 64; l++) nib(gf2_xinvpow8_small(16 * l), t.cross[l]);
+  for (uint32_t m = 0; m < 16; m++)
+    for (uint32_t w = 0; w < 16; w++)
+      nib(gf2_mul(gf2_xinvpow8_small(1024 * w), gf2_xpow8(xp, (uint64_t)65536 * (15 - m))), t.kw[m][w]);
+}
+
+static double avg(const std::vector<double> &v) {
+  double s = 0;
+  for (double x : v) s += x;
+  return s / v.size();
+}
+
+int main(int argc, char **argv) {
+  const int reps = argc > 1 ? atoi(argv[1]) : 8;
+  int cus = 0;
+  CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));
+  static TableBlob tb;
+  build_tables(tb);
+  static SweepTabs st;
+  build_probe_tabs(st);
+  TableBlob *d_tab;
+  SweepTabs *d_st;
+  CHECK(hipMalloc(&d_tab, sizeof(TableBlob)));
+  CHECK(hipMalloc(&d_st, sizeof(SweepTabs)));
+  CHECK(hipMemcpy(d_tab, &tb, sizeof(TableBlob), hipMemcpyHostToDevice));
+  CHECK(hipMemcpy(d_st, &st, sizeof(SweepTabs), hipMemcpyHostToDevice));
+  uint8_t *mem;
+  CHECK(hipMalloc(&mem, kBytes));
+  {
+    std::vector<uint64_t> hp(kN), hl(kN, kLen);
+    for (uint64_t i = 0; i < kN; i++) hp[i] = (uint64_t)(mem + i * kLen);
+    uint64_t *dp, *dl;
+    CHECK(hipMalloc(&dp, 8 * kN));
+    CHECK(hipMalloc(&dl, 8 * kN));
+    CHECK(hipMemcpy(dp, hp.data(), 8 * kN, hipMemcpyHostToDevice));
+    CHECK(hipMemcpy(dl, hl.data(), 8 * kN, hipMemcpyHostToDevice));
+    CHECK(launch_fill_synthetic(dp, dl, kN, 0, 1, 0xC0FFEE, 0));
+    CHECK(hipDeviceSynchronize());
+    CHECK(hipFree(dp));
+    CHECK(hipFree(dl));
+  }
+  uint32_t *o_ref, *o_new, *scratch;
+  CHECK(hipMalloc(&o_ref, 4 * kN));
+  CHECK(hipMalloc(&o_new, 4 * kN));
+  CHECK(hipMalloc(&scratch, 1 << 16));
+  hipEvent_t a, z, a2;
+  CHECK(hipEventCreate(&a));
+  CHECK(hipEventCreate(&z));
+  CHECK(hipEventCreate(&a2));
+  auto product = [&](hipEvent_t e0, hipEvent_t e1) {
+    BatchArgs x{};
+    x.base = mem;
+    x.stride = kLen;
+    x.len = kLen;
+    x.n = kN;
+    x.out = o_ref;
+    x.tab = d_tab;
+    x.ctr = scratch;
+    x.dyn_shift = kDynAuto;
+    CHECK(hipMemsetAsync(o_ref, 0, 4 * kN, 0));
+    CHECK(hipMemsetAsync(scratch, 0, 256, 0));
+    hipExtLaunchKernelGGL((crc32_batch_kernel<true, kDepth, 0>), dim3(cus), dim3(kThreads), 0, 0, e0, e1, 0, x);
+    CHECK(hipGetLastError());
+  };
+  auto newk = [&](hipEvent_t e0, hipEvent_t e1, bool early) {
+    CHECK(hipMemsetAsync(o_new, 0, 4 * kN, 0));
+    if (early)
+      hipExtLaunchKernelGGL((sweep_crc<true, true>), dim3(cus), dim3(1024), 0, 0, e0, e1, 0, mem, d_st, o_new);
+    else
+      hipExtLaunchKernelGGL((sweep_crc<true, false>), dim3(cus), dim3(1024), 0, 0, e0, e1, 0, mem, d_st, o_new);
+    CHECK(hipGetLastError());
+  };
+  // parity first
+  product(nullptr, nullptr);
+  newk(nullptr, nullptr, false);
+  CHECK(hipDeviceSynchronize());
+  std::vector<uint32_t> r1(kN), r2(kN), r3(kN);
+  CHECK(hipMemcpy(r1.data(), o_ref, 4 * kN, hipMemcpyDeviceToHost));
+  CHECK(hipMemcpy(r2.data(), o_new, 4 * kN, hipMemcpyDeviceToHost));
+  newk(nullptr, nullptr, true);
+  CHECK(hipDeviceSynchronize());
+  CHECK(hipMemcpy(r3.data(), o_new, 4 * kN, hipMemcpyDeviceToHost));
+  uint64_t bad = 0;
+  for (uint64_t i = 0; i < kN; i++) bad += (r1[i] != r2[i]) + (r1[i] != r3[i]);
+  printf("sweepcrc_probe: %d CUs, config 3 (%llu B); parity sweep-crc vs product: %s (%llu of %llu differ; [0] %08x vs %08x)\n",
+         cus, (unsigned long long)kBytes, bad ? "DIFFER" : "equal", (unsigned long long)bad,
+         (unsigned long long)kN, r2[0], r1[0]);
+  fflush(stdout);
+  const char *nm[] = {"sweep", "crc-product", "sweep-crc", "sweep-crc-early"};
+  std::vector<std::vector<double>> tk(4), tw(4);
+  for (int r = 0; r < reps; r++)
+    for (int v = 0; v < 4; v++) {
+      CHECK(hipEventRecord(a2, 0));
+      if (v == 0) hipExtLaunchKernelGGL(sweep_crc<false>, dim3(cus), dim3(1024), 0, 0, a, z, 0, mem, d_st, o_new);
+      else if (v == 1) product(a, z);
+      else newk(a, z, v == 3);
+      CHECK(hipEventSynchronize(z));
+      float ms = 0, ms2 = 0;
+      CHECK(hipEventElapsedTime(&ms, a, z));
+      CHECK(hipEventElapsedTime(&ms2, a2, z));
+      if (r > 0) tk[v].push_back(ms), tw[v].push_back(ms2);
+    }
+  for (int v = 0; v < 4; v++)
+    printf("  %-15s kernel avg %8.3f ms (%7.1f GB/s, best %8.3f)   with its memsets %8.3f ms\n", nm[v], avg(tk[v]),
+           kBytes / (avg(tk[v]) * 1e-3) / 1e9, *std::min_element(tk[v].begin(), tk[v].end()), avg(tw[v]));
+  return bad ? 1 : 0;
+}
