@@ -69,6 +69,10 @@ struct SweepTabs {
   uint32_t in32[8 * 16];            // 4-bit tables of x^-32
   uint32_t cross[64][8 * 16];       // lane l: 4-bit tables of x^(-8*16*l)
   uint32_t kw[16][16][8 * 16];      // [chunk index m][wave w]: x^(-8*1024*w) * x^(8*65536*(15-m))
+  // the row form (sweep_rows): one dword stream per lane, 4 KiB apart
+  uint32_t braid4k[4 * 256];        // MCT(x^(8*4096))
+  uint32_t cross4[64][8 * 16];      // lane l: x^(-8*4*l)
+  uint32_t kw4[16][16][8 * 16];     // [m][w]: x^(-8*256*w) * x^(8*65536*(15-m))
 };
 
 // LDS layout (dwords)
@@ -226,6 +230,115 @@ __global__ __launch_bounds__(1024) void sweep_crc(const uint8_t *base, const Swe
   if (!kCrc && acc == 0x12345678u) out[tid] = acc;
 }
 
+// The row form: wave w of the chunk's workgroup reads the 256-B rows w, w+16,
+// ..., w+240 of the 64 KiB chunk (row k of the wave at 4096 k + 256 w), one
+// dword per lane per row -- the first row alone, a wait, then the other 15.
+// Lane l's dwords are 4 KiB apart, so each lane runs ONE stream (braid for
+// x^(8*4096)) and the fold has no in-lane part: one per-lane product by
+// x^(-32 l), the DPP sum, the per-wave move to the buffer end.
+constexpr uint32_t kRB = 0;              // braid x16: 16,384 dwords
+constexpr uint32_t kRC = 16384;          // cross4 per lane: 8,192
+constexpr uint32_t kRK = kRC + 8192;     // kw4: 2,048
+constexpr uint32_t kRowsLdsDw = kRK + 2048;  // 104 KiB
+
+template <bool kCrc>
+__global__ __launch_bounds__(1024) void sweep_rows(const uint8_t *base, const SweepTabs *tabs, uint32_t *out) {
+  __shared__ __attribute__((aligned(16))) uint32_t s_lds[kRowsLdsDw];
+  const uint32_t tid = threadIdx.x, lane = tid & 63u, wv = uni32(tid >> 6);
+  const uint32_t m = blockIdx.x % kChunksPerBuf;
+  if (kCrc) {
+    uint4 *dst = reinterpret_cast<uint4 *>(s_lds + kRB);
+#pragma unroll
+    for (uint32_t k = 0; k < 4; k++) {
+      const uint32_t c = tid + 1024u * k;
+      const uint32_t v = tabs->braid4k[((c >> 2) & 3u) * 256u + (c >> 4)];
+      dst[c] = make_uint4(v, v, v, v);
+    }
+#pragma unroll
+    for (uint32_t k = 0; k < 8; k++) {
+      const uint32_t d = tid + 1024u * k, hi = d >> 12, e = (d >> 5) & 127u, l = (hi << 5) | (d & 31u);
+      s_lds[kRC + d] = tabs->cross4[l][e];
+    }
+#pragma unroll
+    for (uint32_t k = 0; k < 2; k++) {
+      const uint32_t d = tid + 1024u * k;
+      s_lds[kRK + d] = tabs->kw4[m][d >> 7][d & 127u];
+    }
+    __syncthreads();
+  }
+  const uint32_t sw = (lane >> 4) & 1u, rep = (lane & 15u) * 4u;
+  uint32_t o[4], sel[4];
+#pragma unroll
+  for (int j = 0; j < 4; j++) {
+    const uint32_t jj = (uint32_t)j ^ sw;
+    o[j] = jj * 64u + rep;
+    sel[j] = 0x0C020400u + (jj << 8);
+  }
+  const uint32_t cl = kRC + (lane >> 5) * 4096u + (lane & 31u);
+  const uint32_t ck = kRK + wv * 128u;
+  typedef const __attribute__((address_space(1))) uint32_t *gu32;
+  const uint64_t b0 = reinterpret_cast<uint64_t>(base) + 256u * wv + 4u * lane;
+  const uint64_t nchunks = kBytes / kChunk;
+  uint32_t acc = 0, prev_share = 0;
+  uint64_t prev_b = ~0ull;
+  uint64_t c = blockIdx.x;
+  uint32_t d0 = c < nchunks ? __builtin_nontemporal_load(reinterpret_cast<gu32>(b0 + c * kChunk)) : 0u;
+  for (; c < nchunks; c += gridDim.x) {
+    const uint64_t a = b0 + c * kChunk;
+    uint32_t s = 0, q = 0;
+    if (kCrc) {
+      if (m == 0 && wv == 0 && lane == 0) d0 ^= 0xFFFFFFFFu;  // the buffer's seed
+      const uint32_t x = d0;
+      const uint32_t t0 = lds_u32(s_lds, __builtin_amdgcn_perm(x, o[0], sel[0]));
+      const uint32_t t1 = lds_u32(s_lds, __builtin_amdgcn_perm(x, o[1], sel[1]));
+      const uint32_t t2 = lds_u32(s_lds, __builtin_amdgcn_perm(x, o[2], sel[2]));
+      q = lds_u32(s_lds, __builtin_amdgcn_perm(x, o[3], sel[3]));
+      s = __builtin_amdgcn_bitop3_b32(t0, t1, t2, 0x96);
+      __builtin_amdgcn_sched_barrier(0);
+    } else {
+      __builtin_amdgcn_s_waitcnt(0x0F70);
+      acc ^= d0;
+    }
+    uint32_t d[15];
+#pragma unroll
+    for (int k = 0; k < 15; k++) d[k] = __builtin_nontemporal_load(reinterpret_cast<gu32>(a + 4096u * (k + 1)));
+    const uint64_t cn = c + gridDim.x;
+    const uint64_t cnext = cn < nchunks ? cn : c;
+    if (!kCrc) {
+#pragma unroll
+      for (int k = 0; k < 15; k++) acc ^= d[k];
+      d0 = __builtin_nontemporal_load(reinterpret_cast<gu32>(b0 + cnext * kChunk));
+      continue;
+    }
+#pragma unroll
+    for (int k = 0; k < 15; k++) {
+      const uint32_t x = __builtin_amdgcn_bitop3_b32(s, q, d[k], 0x96);
+      const uint32_t t0 = lds_u32(s_lds, __builtin_amdgcn_perm(x, o[0], sel[0]));
+      const uint32_t t1 = lds_u32(s_lds, __builtin_amdgcn_perm(x, o[1], sel[1]));
+      const uint32_t t2 = lds_u32(s_lds, __builtin_amdgcn_perm(x, o[2], sel[2]));
+      q = lds_u32(s_lds, __builtin_amdgcn_perm(x, o[3], sel[3]));
+      s = __builtin_amdgcn_bitop3_b32(t0, t1, t2, 0x96);
+    }
+    if (prev_b != ~0ull && lane == 0) atomicXor(out + prev_b, prev_share);
+    d0 = __builtin_nontemporal_load(reinterpret_cast<gu32>(b0 + cnext * kChunk));
+    __asm__ volatile("" ::: "memory");
+    // lane l's stream sits at chunk end + 256 w + 4 l
+    uint32_t r = nib_mul<32>(s_lds, cl, s ^ q);  // at chunk end + 256 w
+    r ^= row_shl<1>(r);
+    r ^= row_shl<2>(r);
+    r ^= row_shl<4>(r);
+    r ^= row_shl<8>(r);
+    const uint32_t x = uni32(r) ^ (uint32_t)__builtin_amdgcn_readlane((int)r, 16) ^
+                       (uint32_t)__builtin_amdgcn_readlane((int)r, 32) ^
+                       (uint32_t)__builtin_amdgcn_readlane((int)r, 48);
+    prev_share = uni32(nib_mul<1>(s_lds, ck, x));
+    if (m == kChunksPerBuf - 1 && wv == 0) prev_share ^= 0xFFFFFFFFu;
+    prev_b = c / kChunksPerBuf;
+  }
+  if (kCrc && prev_b != ~0ull && lane == 0) atomicXor(out + prev_b, prev_share);
+  if (!kCrc && acc == 0x12345678u) out[tid] = acc;
+}
+
 static void build_probe_tabs(SweepTabs &t) {
   XPowTable xp;
   build_xpow_table(xp);
@@ -239,6 +352,11 @@ static void build_probe_tabs(SweepTabs &t) {
   for (uint32_t m = 0; m < 16; m++)
     for (uint32_t w = 0; w < 16; w++)
       nib(gf2_mul(gf2_xinvpow8_small(1024 * w), gf2_xpow8(xp, (uint64_t)65536 * (15 - m))), t.kw[m][w]);
+  build_mct(gf2_xpow8(xp, 4096), t.braid4k);
+  for (uint32_t l = 0; l < 64; l++) nib(gf2_xinvpow8_small(4 * l), t.cross4[l]);
+  for (uint32_t m = 0; m < 16; m++)
+    for (uint32_t w = 0; w < 16; w++)
+      nib(gf2_mul(gf2_xinvpow8_small(256 * w), gf2_xpow8(xp, (uint64_t)65536 * (15 - m))), t.kw4[m][w]);
 }
 
 static double avg(const std::vector<double> &v) {
@@ -307,6 +425,11 @@ int main(int argc, char **argv) {
       hipExtLaunchKernelGGL((sweep_crc<true, false>), dim3(cus), dim3(1024), 0, 0, e0, e1, 0, mem, d_st, o_new);
     CHECK(hipGetLastError());
   };
+  auto rows = [&](hipEvent_t e0, hipEvent_t e1) {
+    CHECK(hipMemsetAsync(o_new, 0, 4 * kN, 0));
+    hipExtLaunchKernelGGL(sweep_rows<true>, dim3(cus), dim3(1024), 0, 0, e0, e1, 0, mem, d_st, o_new);
+    CHECK(hipGetLastError());
+  };
   // parity first
   product(nullptr, nullptr);
   newk(nullptr, nullptr, false);
@@ -317,19 +440,28 @@ int main(int argc, char **argv) {
   newk(nullptr, nullptr, true);
   CHECK(hipDeviceSynchronize());
   CHECK(hipMemcpy(r3.data(), o_new, 4 * kN, hipMemcpyDeviceToHost));
-  uint64_t bad = 0;
-  for (uint64_t i = 0; i < kN; i++) bad += (r1[i] != r2[i]) + (r1[i] != r3[i]);
+  std::vector<uint32_t> r4(kN);
+  rows(nullptr, nullptr);
+  CHECK(hipDeviceSynchronize());
+  CHECK(hipMemcpy(r4.data(), o_new, 4 * kN, hipMemcpyDeviceToHost));
+  uint64_t bad = 0, bad_rows = 0;
+  for (uint64_t i = 0; i < kN; i++) bad += (r1[i] != r2[i]) + (r1[i] != r3[i]), bad_rows += r1[i] != r4[i];
+  printf("parity rows-crc vs product: %s (%llu differ; [0] %08x)\n", bad_rows ? "DIFFER" : "equal",
+         (unsigned long long)bad_rows, r4[0]);
+  bad += bad_rows;
   printf("sweepcrc_probe: %d CUs, config 3 (%llu B); parity sweep-crc vs product: %s (%llu of %llu differ; [0] %08x vs %08x)\n",
          cus, (unsigned long long)kBytes, bad ? "DIFFER" : "equal", (unsigned long long)bad,
          (unsigned long long)kN, r2[0], r1[0]);
   fflush(stdout);
-  const char *nm[] = {"sweep", "crc-product", "sweep-crc", "sweep-crc-early"};
-  std::vector<std::vector<double>> tk(4), tw(4);
+  const char *nm[] = {"sweep", "crc-product", "sweep-crc", "sweep-crc-early", "rows-read", "rows-crc"};
+  std::vector<std::vector<double>> tk(6), tw(6);
   for (int r = 0; r < reps; r++)
-    for (int v = 0; v < 4; v++) {
+    for (int v = 0; v < 6; v++) {
       CHECK(hipEventRecord(a2, 0));
       if (v == 0) hipExtLaunchKernelGGL(sweep_crc<false>, dim3(cus), dim3(1024), 0, 0, a, z, 0, mem, d_st, o_new);
       else if (v == 1) product(a, z);
+      else if (v == 4) hipExtLaunchKernelGGL(sweep_rows<false>, dim3(cus), dim3(1024), 0, 0, a, z, 0, mem, d_st, o_new);
+      else if (v == 5) rows(a, z);
       else newk(a, z, v == 3);
       CHECK(hipEventSynchronize(z));
       float ms = 0, ms2 = 0;
@@ -337,7 +469,7 @@ int main(int argc, char **argv) {
       CHECK(hipEventElapsedTime(&ms2, a2, z));
       if (r > 0) tk[v].push_back(ms), tw[v].push_back(ms2);
     }
-  for (int v = 0; v < 4; v++)
+  for (int v = 0; v < 6; v++)
     printf("  %-15s kernel avg %8.3f ms (%7.1f GB/s, best %8.3f)   with its memsets %8.3f ms\n", nm[v], avg(tk[v]),
            kBytes / (avg(tk[v]) * 1e-3) / 1e9, *std::min_element(tk[v].begin(), tk[v].end()), avg(tw[v]));
   return bad ? 1 : 0;
