@@ -21,6 +21,9 @@
 //   wave-phase4K   the same at 4 KiB granularity
 //   wave-rangephase range entered at a hashed 64 KiB offset of the whole 16
 //                  MiB range, wrapping (buffers in order from there)
+//   deep-Nw-GK     N waves per CU (one workgroup), each a contiguous range,
+//                  buffers rotated, G KiB groups, two in flight: fewer,
+//                  deeper streams (deep-16w-2K is the product's shape)
 //
 //   make -C tools phase_probe && tools/phase_probe [reps]
 #include <hip/hip_ext.h>
@@ -115,6 +118,46 @@ __global__ __launch_bounds__(1024) void k_wave(const uint8_t *base, uint64_t byt
   if (acc == 0x12345678u) out[threadIdx.x] = acc;
 }
 
+// fewer, deeper streams: kWv waves per workgroup (one workgroup per CU), each
+// a contiguous range of bytes / (CUs * kWv), buffers rotated as the product,
+// groups of kG KiB, two groups in flight
+template <int kWv, int kG>
+__global__ __launch_bounds__(kWv * 64) void k_deep(const uint8_t *base, uint64_t bytes, uint32_t *out) {
+  const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+  const uint32_t w = blockIdx.x * kWv + wv, W = gridDim.x * kWv;
+  const uint64_t per = bytes / W;
+  const uint32_t nbuf = (uint32_t)(per / kBuf);
+  const uint64_t b0 = reinterpret_cast<uint64_t>(base) + (uint64_t)w * per;
+  const uint32_t rot = hash32(w * 0x9E3779B1u + 7u) % nbuf;
+  constexpr uint32_t gb_bytes = 1024u * kG;
+  const uint32_t gpb = (uint32_t)(kBuf / gb_bytes), ng = nbuf * gpb;
+  auto addr = [&](uint32_t g) -> uint64_t {
+    return (uint64_t)((g / gpb + rot) % nbuf) * kBuf + (uint64_t)(g % gpb) * gb_bytes;
+  };
+  uint32_t acc = 0;
+  v4u ga[kG], gb[kG];
+  auto ld = [&](v4u *G, uint32_t g) {
+    const uint64_t a = b0 + addr(g) + 16u * lane;
+#pragma unroll
+    for (int u = 0; u < kG; u++) G[u] = __builtin_nontemporal_load(reinterpret_cast<gv4u>(a + 1024u * u));
+  };
+  auto use = [&](const v4u *G) {
+#pragma unroll
+    for (int u = 0; u < kG; u++) acc ^= xr(G[u]);
+  };
+  ld(ga, 0);
+  ld(gb, 1);
+  for (uint32_t g = 0; g + 2 < ng; g += 2) {
+    use(ga);
+    ld(ga, g + 2);
+    use(gb);
+    if (g + 3 < ng) ld(gb, g + 3);
+  }
+  use(ga);
+  use(gb);
+  if (acc == 0x12345678u) out[threadIdx.x] = acc;
+}
+
 int main(int argc, char **argv) {
   const int reps = argc > 1 ? atoi(argv[1]) : 8;
   int cus = 0;
@@ -126,8 +169,9 @@ int main(int argc, char **argv) {
   CHECK(hipMalloc(&out, 1 << 20));
   CHECK(hipMemset(mem, 1, bytes));
   CHECK(hipDeviceSynchronize());
-  const char *nm[] = {"sweep", "wave-inorder", "wave-bufrot", "wave-phase64K", "wave-phase4K", "wave-rangephase"};
-  constexpr int kV = 6;
+  const char *nm[] = {"sweep", "wave-inorder", "wave-bufrot", "wave-phase64K", "wave-phase4K", "wave-rangephase",
+                      "deep-16w-2K", "deep-8w-4K", "deep-4w-8K", "deep-8w-2K", "deep-4w-4K"};
+  constexpr int kV = 11;
   std::vector<std::vector<double>> t(kV);
   hipEvent_t a, z;
   CHECK(hipEventCreate(&a));
@@ -141,6 +185,11 @@ int main(int argc, char **argv) {
         case 3: hipExtLaunchKernelGGL(k_wave<2>, dim3(cus), dim3(1024), 0, 0, a, z, 0, mem, bytes, out); break;
         case 4: hipExtLaunchKernelGGL(k_wave<3>, dim3(cus), dim3(1024), 0, 0, a, z, 0, mem, bytes, out); break;
         case 5: hipExtLaunchKernelGGL(k_wave<4>, dim3(cus), dim3(1024), 0, 0, a, z, 0, mem, bytes, out); break;
+        case 6: hipExtLaunchKernelGGL((k_deep<16, 2>), dim3(cus), dim3(1024), 0, 0, a, z, 0, mem, bytes, out); break;
+        case 7: hipExtLaunchKernelGGL((k_deep<8, 4>), dim3(cus), dim3(512), 0, 0, a, z, 0, mem, bytes, out); break;
+        case 8: hipExtLaunchKernelGGL((k_deep<4, 8>), dim3(cus), dim3(256), 0, 0, a, z, 0, mem, bytes, out); break;
+        case 9: hipExtLaunchKernelGGL((k_deep<8, 2>), dim3(cus), dim3(512), 0, 0, a, z, 0, mem, bytes, out); break;
+        case 10: hipExtLaunchKernelGGL((k_deep<4, 4>), dim3(cus), dim3(256), 0, 0, a, z, 0, mem, bytes, out); break;
       }
       CHECK(hipGetLastError());
       CHECK(hipEventSynchronize(z));
