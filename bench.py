@@ -654,6 +654,80 @@ def main() -> None:
             return pm["traffic_bytes_per_launch"], pm["source"]
         return None, None
 
+    def small_batches() -> dict:
+        """Uniform batches of small buffers -- the ZIP-entry regime (config 4's
+        median entry is 3,971 B): 1 GiB of L-byte
+        buffers (buffer i = payload(L, i)), two batches rotated, through
+        zcrc32_batch_device (no bound: the split plan's two scans and the CRC
+        launch), zcrc32_batch_device_maxlen (the caller's bound L: one launch)
+        and zcrc32_batch_device_strided; k calls per API between one HIP event
+        pair queued behind >= 15 ms of warm calls, the stream read of the same region
+        beside them; every API's results checked against reference-generated
+        samples (tests/golden/small.npz) and against each other."""
+        g = np.load(os.path.join(ROOT, "tests", "golden", "small.npz"))
+        res = {}
+        for L in (1024, 4096):
+            n = (1 << 30) // L
+            bat = []
+            for b in range(2):
+                mem = torch.empty(n * L + 64, dtype=torch.uint8, device=dev)
+                ptrs = mem.data_ptr() + torch.arange(n, dtype=torch.int64, device=dev) * L
+                lens = torch.full((n,), L, dtype=torch.int64, device=dev)
+                z.fill_synthetic(ptrs, lens, index0=b * n, seed=PAYLOAD_SEED)
+                bat.append((mem, ptrs, lens, torch.empty(n, dtype=torch.int32, device=dev)))
+            sink = torch.empty(1024, dtype=torch.int32, device=dev)
+            apis = {
+                "device": lambda b: z.crc32_batch_device(bat[b][1], bat[b][2], out=bat[b][3]),
+                "device_maxlen": lambda b: z.crc32_batch_device(bat[b][1], bat[b][2], out=bat[b][3], max_len=L),
+                "strided": lambda b: z.crc32_batch_strided(bat[b][0], L, L, n, out=bat[b][3]),
+                "stream_read": lambda b: z.read_sweep_device(bat[b][0].data_ptr(), n * L, sink),
+            }
+            idx = g[f"len{L}_idx"].astype(np.int64)
+            first = None
+            row = {"buffers": n, "bytes_per_call": n * L}
+            # timed back to back, the parity checks after all of them: an idle
+            # GPU between blocks (a host-side check) left the next block's
+            # calls up to 15% slower after 40 warm calls (session 15:
+            # tools/small_timing_ab.py agrees with tools/small_batches.py once
+            # the blocks follow each other)
+            for name, fn in apis.items():
+                for s in range(100):  # >= 15 ms of work in front of the timed calls
+                    fn(s % 2)
+                k = 40
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                for s in range(k):
+                    fn(s % 2)
+                e1.record()
+                e1.synchronize()
+                ms = e0.elapsed_time(e1) / k
+                row[f"{name}_us_per_call"] = round(ms * 1e3, 1)
+                row[f"{name}_tbs"] = round(n * L / (ms * 1e-3) / 1e12, 3)
+            for name, fn in apis.items():
+                if name == "stream_read":
+                    continue
+                fn(0)
+                torch.cuda.synchronize()
+                got = bat[0][3].cpu().numpy().view(np.uint32)
+                ok = int((got[idx] == g[f"len{L}"]).sum())
+                if ok != len(idx) or (first is not None and not np.array_equal(got, first)):
+                    raise SystemExit(f"PARITY FAILURE: small buffers {L} B through {name}: "
+                                     f"{len(idx) - ok} of {len(idx)} samples differ, or differs from another API")
+                first = got.copy() if first is None else first
+            for name in ("device", "device_maxlen", "strided"):
+                row[f"{name}_frac_of_stream_read"] = round(row[f"{name}_tbs"] / row["stream_read_tbs"], 4)
+            row["parity"] = (f"{len(idx)}/{len(idx)} reference samples equal on every API; the three APIs' "
+                             f"{n} results equal")
+            res[f"len{L}"] = row
+            del bat, sink
+            torch.cuda.empty_cache()
+        res["method"] = ("uniform L-byte buffers, 2 x 1 GiB batches rotated, k = 40 calls per API between one "
+                         "HIP event pair on the launch stream, queued behind 100 warm calls; device = zcrc32_batch_device "
+                         "(split plan: 2 scan kernels + the CRC launch), device_maxlen = "
+                         "zcrc32_batch_device_maxlen(max_len = L) (one small-kernel launch), strided = "
+                         "zcrc32_batch_device_strided; stream_read = zcrc_read_sweep_device over the batch")
+        return res
+
     host_extra = None
     if args.config in (3, 5) and args.host_resident_gib > 0:
         n_host = int(args.host_resident_gib * 1024)
@@ -676,7 +750,8 @@ def main() -> None:
     parity = m["parity"]
 
     # Secondary configs (N = 1 only): SURVEY 8(d) configs 2 and 4, timed the
-    # same way in the same run, so that they too carry the driver's clock.
+    # same way in the same run, so that they too carry the driver's clock, and
+    # uniform batches of 1 KiB / 4 KiB buffers through the three device APIs.
     secondary = None
     if world == 1 and args.config == 3 and not args.no_secondary:
         secondary = {}
@@ -703,6 +778,13 @@ def main() -> None:
                 "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None if tr is None else int(tr),
                 "algorithmic_bytes_per_launch": r["bytes_main"], "kernel": r["kernel"], "small_kernel": r["small"],
                 "parity": r["parity"]}
+
+        try:
+            secondary["small_buffers"] = small_batches()
+        except SystemExit:
+            raise
+        except Exception as e:  # measurement beside the line: reported, never failing the run
+            secondary["small_buffers"] = {"error": f"{type(e).__name__}: {e}"}
 
     if m["extra"] is not None:  # host-resident rate (N = 1) / host batch over the device set (N > 1)
         secondary = secondary or {}

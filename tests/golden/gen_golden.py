@@ -7,7 +7,7 @@ value is cross-checked against Python's zlib.crc32 before it is written.
 Inputs are the counter-based payload of SURVEY.md 8(d) (oracle.payload), so
 the fixtures hold parameters + expected CRCs, never copied source.
 
-    python tests/golden/gen_golden.py
+    python tests/golden/gen_golden.py [--small-only]
 """
 from __future__ import annotations
 
@@ -36,7 +36,30 @@ def ref(data: bytes, crc: int = 0) -> int:
     return r
 
 
+SMALL_LENS = (1024, 4096)
+
+
+def gen_small() -> None:
+    """small.npz: uniform batches of small buffers, the ZIP-entry regime
+    (config 4's median entry is 3,971 B): 1 GiB of L-byte buffers, buffer i
+    = payload(L, i), for L in SMALL_LENS -- 256 sampled indices each, for the
+    bench line's small-buffer secondary (bench.py) and its tests."""
+    rnd = random.Random(20261018)
+    out = {}
+    for L in SMALL_LENS:
+        n = (1 << 30) // L
+        idx = np.array(sorted(rnd.sample(range(n), 255) + [n - 1]), dtype=np.uint64)
+        out[f"len{L}_idx"] = idx
+        out[f"len{L}"] = np.array([ref(o.payload(L, int(i)).tobytes()) for i in idx], dtype=np.uint32)
+    np.savez_compressed(os.path.join(HERE, "small.npz"), **out)
+
+
 def main() -> None:
+    if "--small-only" in sys.argv:  # (the other fixtures stay as they are)
+        o.build()
+        gen_small()
+        print("wrote tests/golden/small.npz")
+        return
     o.build()
     assert o.ref_available(), "oracle/_ref not built: /root/reference missing?"
     rnd = random.Random(20261015)
@@ -110,6 +133,7 @@ def main() -> None:
     }
     with open(os.path.join(HERE, "golden.json"), "w") as f:
         json.dump(meta, f, indent=1)
+    gen_small()
     print("wrote golden fixtures:", sorted(os.listdir(HERE)))
 
 

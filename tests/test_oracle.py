@@ -68,6 +68,18 @@ def test_configs(golden):
         assert o.payload_crc(1 << 20, int(i)) == c
 
 
+def test_small_buffer_fixtures():
+    """tests/golden/small.npz (uniform 1 KiB / 4 KiB batches, bench.py's
+    small-buffer secondary): every sample against the oracle."""
+    import os
+    g = np.load(os.path.join(os.path.dirname(__file__), "golden", "small.npz"))
+    for L in (1024, 4096):
+        idx, crc = g[f"len{L}_idx"], g[f"len{L}"]
+        assert len(idx) == 256 and int(idx.max()) == (1 << 30) // L - 1
+        for i, c in zip(idx, crc):
+            assert o.payload_crc(L, int(i)) == c
+
+
 def test_zipf_pinned_totals(golden):
     L = o.zipf_lens(100000)
     assert int(L.sum()) == 13_123_505_587 == golden["meta"]["config4_sum_len"]
