@@ -83,7 +83,7 @@ int zcrc32_batch(const void *const *ptrs, const size_t *lens, const uint32_t *se
  * NULL; d_out: device array of n results.  Asynchronous on `stream`; its
  * scratch (work counter, length prefix, plan tile sums: 256 + 8*(n+1) +
  * 8*ceil(n/8192) bytes; above 8192 buffers the split plan's layout instead,
- * 16*n + (312 + 24*n + 96*T rounded up to 16) bytes with T = ceil(n/(1024*p))
+ * 16*n + (320 + 24*n + 112*T rounded up to 16) bytes with T = ceil(n/(1024*p))
  * tiles, p the smallest of 1, 2, 4, 8 for which T <= 256) is a grow-only
  * buffer from a cache, leased per call and never shared between streams
  * (keyed by handle and, where the runtime has it, hipStreamGetId: a recycled

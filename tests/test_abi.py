@@ -173,13 +173,13 @@ def test_argument_errors_are_reported_not_computed():
     assert lib.zcrc32_checked(None, 10, 0, ctypes.byref(out)) == -2
     assert b"null" in lib.zcrc_last_error()
     assert lib.zcrc32_batch_device_scratch_bytes(8192) == 256 + 8 * 8193 + 8  # counter line | prefix | one plan tile
-    # above kFusedMaxN the split plan's layout: counters | prefix | 6 tile words x T tiles | tile prefixes
-    # 6 x (T + 1) | ptrs | seeds, oidx | small-list descriptors (16 B, 16-B aligned)
+    # above kFusedMaxN the split plan's layout: counters | prefix | 7 tile words x T tiles | tile prefixes
+    # 7 x (T + 1) | ptrs | seeds, oidx | small-list descriptors (16 B, 16-B aligned)
     # (T = the split plan's tiles: tests/kernel_model.py split_tile mirrors split_per_thread)
     import kernel_model as km
     for n in (8193, 100_000, 262_144, 262_145, 600_000, 1_048_577, 4_200_000):
         T = -(-n // km.split_tile(n))
-        head = 256 + 8 * (n + 1) + 8 * 6 * T + 8 * 6 * (T + 1) + 8 * n + 8 * n
+        head = 256 + 8 * (n + 1) + 8 * 7 * T + 8 * 7 * (T + 1) + 8 * n + 8 * n
         assert lib.zcrc32_batch_device_scratch_bytes(n) == (head + 15) // 16 * 16 + 16 * n, n
 
 

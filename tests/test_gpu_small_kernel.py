@@ -317,19 +317,20 @@ def _split_lists(scratch, n):
     T = -(-n // km.split_tile(n))
     prefix = 256
     tiles = prefix + 8 * (n + 1)
-    tile_pre = tiles + 48 * T  # kTileWords = 6
-    ptrs = tile_pre + 48 * (T + 1)
+    tile_pre = tiles + 56 * T  # kTileWords = 7
+    ptrs = tile_pre + 56 * (T + 1)
     seeds = ptrs + 8 * n
     oidx = seeds + 4 * n
     sdesc = (oidx + 4 * n + 15) // 16 * 16
-    counts = raw[128:168].view(np.uint64)
+    counts = raw[128:176].view(np.uint64)
     return (counts, raw[prefix:prefix + 8 * (n + 1)].view(np.uint64), raw[oidx:oidx + 4 * n].view(np.uint32),
             raw[sdesc:sdesc + 16 * n].view(np.uint32).reshape(n, 4))
 
 
 @pytest.mark.parametrize("n,shape", [(20_000, "mixed"), (50_000, "all_small"), (4_200_000, "mixed"),
                                      (4_300_000, "all_small"), (20_000, "mixed_big"), (60_000, "mixed_big"),
-                                     (30_000, "uniform_small"), (600_000, "near_uniform_small")])
+                                     (30_000, "uniform_small"), (600_000, "near_uniform_small"),
+                                     (20_000, "uniform_medium"), (20_000, "uniform_medium_but_one")])
 def test_split_plan_lists_equal_the_model(n, shape):
     """The plan's decision, the compacted batch (order and byte prefix) and the
     small list (tile by tile, by size class, index order within a class) equal
@@ -344,6 +345,10 @@ def test_split_plan_lists_equal_the_model(n, shape):
         lens = np.full(n, 1024)
     elif shape == "near_uniform_small":
         lens = rng.integers(1000, 1300, n)
+    elif shape.startswith("uniform_medium"):  # unsplit, equal (counts[5] = 1) -- or all but the last
+        lens = np.full(n, 70_001)
+        if shape.endswith("one"):
+            lens[-1] = 70_000
     elif shape == "mixed":  # ZIP-entry-like: most small, some large
         lens = np.where(rng.random(n) < 0.995, rng.integers(0, top, n), rng.integers(SMALL_MAX + 1, 40_000, n))
     else:  # mixed_big: medium and big (>= 1 MiB, kBigMin) batch-kernel buffers interleaved (round-4 order)
@@ -363,6 +368,8 @@ def test_split_plan_lists_equal_the_model(n, shape):
     model = km.split_plan(lens.tolist(), grid=z.device_info()["num_cus"])
     assert bool(counts[2]) == model["split"], counts
     assert (int(counts[2]) == 2) == model.get("direct", False), counts
+    # every length equal and unsplit: the batch kernel's window order may apply
+    assert int(counts[5]) == int(not model["split"] and len(set(lens.tolist())) == 1), counts
     if model.get("direct"):
         assert int(counts[1]) == n and int(counts[0]) == 0 and int(counts[4]) == z.device_info()["num_cus"]
     elif model["split"]:

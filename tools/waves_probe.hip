@@ -38,7 +38,7 @@ using namespace zcrc;
 
 constexpr uint64_t kN = 65536, kLen = 1u << 20, kBytes = kN * kLen;
 
-template <int kWv, int kG>
+template <int kWv, int kG, bool kRR = false>
 __global__ __launch_bounds__(kWv * 64) void simple_crc(const uint8_t *base, const TableBlob *tab, uint32_t *out) {
   __shared__ __attribute__((aligned(16))) uint32_t s_lds[kLdsBytes / 4];
   constexpr uint32_t kT = kWv * 64;
@@ -57,7 +57,9 @@ __global__ __launch_bounds__(kWv * 64) void simple_crc(const uint8_t *base, cons
   const uint32_t nb = (uint32_t)(kN / W);  // buffers per wave
   const uint32_t rot = hash32(w) % nb;
   for (uint32_t k = 0; k < nb; k++) {
-    const uint32_t bi = w * nb + (k + rot) % nb;
+    // kRR: round-robin buffers (wave w: buffers w, w + W, ...): the waves'
+    // current buffers form one contiguous window (tools/region_probe)
+    const uint32_t bi = kRR ? k * W + w : w * nb + (k + rot) % nb;
     const __amdgpu_buffer_rsrc_t rs =
         __builtin_amdgcn_make_buffer_rsrc((void *)(base + (uint64_t)bi * kLen), (short)0, (int)kLen, 0x00020000);
     uint32_t s0 = 0, s1 = 0, s2 = 0, s3 = 0, q0 = 0, q1 = 0, q2 = 0, q3 = 0;

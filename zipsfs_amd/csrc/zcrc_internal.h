@@ -74,7 +74,8 @@ struct BatchArgs {
   uint32_t dyn_shift;
   uint64_t dyn_unit;
   uint32_t ab_flags;  // A/B knobs (0 in the product; ZCRC_AB_FLAGS): bit 0 = split shifts bit by bit (rounds
-                      // 1-3), bit 2 = the split plan's small-list workgroups do not join the dynamic part
+                      // 1-3), bit 2 = the split plan's small-list workgroups do not join the dynamic part,
+                      // bit 3 = no window order for equal buffers (BatchView::wperm: the round-5 range order)
   // fused small batches (kFusedMaxN): lengths to scan in-kernel (the scan is
   // written to `prefix`), split-piece accumulators (n words) and the
   // finished-wave counter; acc, *ctr and *done are zero at launch and left
@@ -152,7 +153,7 @@ struct SplitPlan {
   const uint32_t *seeds;  // nullable
   uint64_t n;
   uint64_t *tile_sum;     // kTileWords per tile: medium, big, small bytes, medium | big << 32 counts, small count,
-                          // small lengths' sum of squares
+                          // small lengths' sum of squares, buffers whose length differs from lens[0]
   uint64_t *tile_pre;     // kTileWords x (tiles + 1): exclusive tile prefixes + totals (above kPlanDirectTiles)
   uint64_t *prefix_c;     // n + 1
   const uint8_t **ptrs_c;
@@ -160,7 +161,8 @@ struct SplitPlan {
   uint32_t *oidx, *out;
   uint4 *sdesc;           // the small list, one 16-B descriptor per entry (SmallArgs::sdesc)
   uint64_t *counts;       // [0] n_large, [1] n_small, [2] split (1; 2: direct, the small body walks ptrs/lens in
-                          // index order), [3] small lanes per buffer, [4] small workgroups
+                          // index order), [3] small lanes per buffer, [4] small workgroups, [5] every length
+                          // equal (unsplit batches only: the batch kernel's window order, BatchView::wperm)
   uint32_t grid;          // the batch kernel's workgroups
   uint32_t small_cost;    // CU time of a small-list byte, in quarters of a batch-kernel byte
   uint32_t force;
@@ -171,7 +173,7 @@ struct SplitPlan {
 };
 hipError_t launch_plan_split(const SplitPlan &p, hipStream_t stream);
 constexpr uint32_t kSizeClasses = kSmallMax / 256 + 1;  // small list order: 256-B block count
-constexpr uint32_t kTileWords = 6;
+constexpr uint32_t kTileWords = 7;
 constexpr uint64_t kBigMin = 1ull << 20;  // split plan: buffers of at least this go last in the batch kernel's order
 constexpr uint64_t kPlanDirectTiles = 512;  // up to this many tiles each scatter workgroup sums the tile words itself
 // split plan tiles: 1024 x per buffers per plan_split_count / plan_split_scatter

@@ -124,7 +124,9 @@ __global__ __launch_bounds__(1024) void plan_one_tile(const uint64_t *lens, uint
 // (kTileWords): medium bytes, big bytes, small bytes, the medium and big
 // counts packed (low / high half), the small count and the small lengths'
 // sum of squares (round 4: a batch of about equal small buffers is walked in
-// place by the small body, without lists -- mode 2).  The scatter decides
+// place by the small body, without lists -- mode 2), and the buffers whose
+// length differs from lens[0] (round 6: an unsplit batch of equal buffers
+// is read in the batch kernel's window order, BatchView::wperm).  The scatter decides
 // for the whole launch (every workgroup reads the same tile sums, so all
 // decide alike): split when the small list is worth at least two of the batch
 // kernel's workgroups (or p.force and there is any small buffer); otherwise
@@ -156,11 +158,13 @@ __global__ __launch_bounds__(1024) void plan_split_count(SplitPlan p) {
     const uint64_t idx = base + 64u * k;
     lv[k] = idx < p.n ? p.lens[idx] : ~0ull;  // ~0: absent
   }
-  uint64_t bm = 0, bb = 0, bs = 0, cmb = 0, cs = 0, sq = 0;
+  const uint64_t L0 = p.lens[0];  // (n > kFusedMaxN here)
+  uint64_t bm = 0, bb = 0, bs = 0, cmb = 0, cs = 0, sq = 0, mis = 0;
 #pragma unroll
   for (uint32_t k = 0; k < kPer; k++) {
     const uint64_t L = lv[k];
     if (L == ~0ull) continue;
+    mis += L != L0;
     if (L <= kSmallMax) bs += L, cs += 1, sq += L * L;
     else if (L >= p.big_min) bb += L, cmb += 1ull << 32;
     else bm += L, cmb += 1;
@@ -172,7 +176,10 @@ __global__ __launch_bounds__(1024) void plan_split_count(SplitPlan p) {
   cmb = rdlane64(wave_incl_scan(cmb), 63);
   cs = rdlane64(wave_incl_scan(cs), 63);
   sq = rdlane64(wave_incl_scan(sq), 63);
-  if (lane == 0) s_w[wv][0] = bm, s_w[wv][1] = bb, s_w[wv][2] = bs, s_w[wv][3] = cmb, s_w[wv][4] = cs, s_w[wv][5] = sq;
+  mis = rdlane64(wave_incl_scan(mis), 63);
+  if (lane == 0)
+    s_w[wv][0] = bm, s_w[wv][1] = bb, s_w[wv][2] = bs, s_w[wv][3] = cmb, s_w[wv][4] = cs, s_w[wv][5] = sq,
+    s_w[wv][6] = mis;
   __syncthreads();
   if (threadIdx.x < kTileWords) {
     uint64_t v = 0;
@@ -278,6 +285,7 @@ __global__ __launch_bounds__(1024) void plan_split_scatter(SplitPlan p) {
       p.counts[2] = mode;
       p.counts[3] = mode && as <= 2048 * n_small ? 8 : 16;  // mean small length <= 2 KiB: 8 lanes
       p.counts[4] = wgs;
+      p.counts[5] = !mode && s_tw[6][1] == 0;  // unsplit and every length equal: the window order
     }
   }
   __syncthreads();

@@ -846,7 +846,7 @@ struct SplitScratch {
     total = sdesc + 16 * n;
   }
 };
-static_assert(kCtrBytes >= 128 + 5 * 8, "the five split counts share the counter area");
+static_assert(kCtrBytes >= 128 + 6 * 8 && 128 + 6 * 8 <= kFaultByte, "the six split counts share the counter area");
 
 bool split_batch(size_t n) { return n > kFusedMaxN && n < (1ull << 31) && small_enabled(); }
 
@@ -2524,6 +2524,7 @@ int zcrc32_batch_device_strided(const void *d_base, uint64_t stride, uint64_t le
     a.out = d_out + first;
     a.n = cnt;
     a.tab = dc->d_tab;
+    a.ab_flags = ab_flags_setting();
     if (len >= kSplitMin) ZCRC_HIP_TRY(hipMemsetAsync(a.out, 0, 4 * cnt, st));
     rc = launch_main(a, true, *dc, st);
     if (rc) break;
