@@ -12,7 +12,8 @@ plan finds the lengths equal) and through zcrc32_batch_device_strided, and
 (--shard) config 5's per-GPU shard, 131,072 x 1 MiB.  Every block's results
 are compared with the reference-generated golden samples.
 
-  python tools/order_ab.py [rounds] [--shard]
+  python tools/order_ab.py [rounds] [--shard] [--dyn]   (--dyn: also the
+  window order with an eighth, half or none of the bytes dynamic)
 """
 import json
 import os
@@ -51,14 +52,17 @@ def main():
     }
     k = 5
     res = {}
+    # orders x dynamic shares (ZCRC_AB_FLAGS bits 3 and 4-5, read per call)
+    variants = (("window", "0"), ("range", "8"), ("window-dyn1/8", "16"), ("window-dyn1/2", "32"),
+                ("window-nodyn", "48")) if "--dyn" in sys.argv else (("window", "0"), ("range", "8"))
     for api, fn in apis.items():
-        for order, flags in (("window", "0"), ("range", "8")):
+        for order, flags in variants:
             os.environ["ZCRC_AB_FLAGS"] = flags
             for _ in range(3):
                 fn()
         torch.cuda.synchronize()
         for r in range(rounds):
-            for order, flags in (("window", "0"), ("range", "8")):
+            for order, flags in variants:
                 os.environ["ZCRC_AB_FLAGS"] = flags
                 out.zero_()
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)

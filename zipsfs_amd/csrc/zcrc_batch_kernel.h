@@ -1362,8 +1362,11 @@ __global__ __launch_bounds__(kThreads) void crc32_batch_kernel(BatchArgs args) {
   // kDynAuto: half the bytes dynamic for batches of small ragged buffers
   // (per-piece latency varies), a quarter for large buffers (every unit
   // boundary inside a buffer costs a split piece).
-  const uint32_t shift = args.dyn_shift != kDynAuto ? args.dyn_shift
-                         : (args.n && total / args.n < kDynSmallAvg) ? 1u : 2u;
+  uint32_t shift = args.dyn_shift != kDynAuto ? args.dyn_shift
+                   : (args.n && total / args.n < kDynSmallAvg) ? 1u : 2u;
+  // A/B (ab_flags bits 4-5, read per call: tools/order_ab.py): 1 -> an eighth
+  // dynamic, 2 -> half, 3 -> none
+  if (const uint32_t ds = (args.ab_flags >> 4) & 3u) shift = ds == 1 ? 3u : ds == 2 ? 1u : 0u;
   uint64_t Td = (args.ctr && shift) ? (total >> shift) : 0;
   if (Td / W < unit) Td = 0;  // fewer units than waves: static only
   const uint64_t Ts = total - Td;

@@ -75,7 +75,8 @@ struct BatchArgs {
   uint64_t dyn_unit;
   uint32_t ab_flags;  // A/B knobs (0 in the product; ZCRC_AB_FLAGS): bit 0 = split shifts bit by bit (rounds
                       // 1-3), bit 2 = the split plan's small-list workgroups do not join the dynamic part,
-                      // bit 3 = no window order for equal buffers (BatchView::wperm: the round-5 range order)
+                      // bit 3 = no window order for equal buffers (BatchView::wp: the round-5 range order),
+                      // bits 4-5 = the dynamic share (1: an eighth, 2: half, 3: none; 0: as configured)
   // fused small batches (kFusedMaxN): lengths to scan in-kernel (the scan is
   // written to `prefix`), split-piece accumulators (n words) and the
   // finished-wave counter; acc, *ctr and *done are zero at launch and left
@@ -162,7 +163,7 @@ struct SplitPlan {
   uint4 *sdesc;           // the small list, one 16-B descriptor per entry (SmallArgs::sdesc)
   uint64_t *counts;       // [0] n_large, [1] n_small, [2] split (1; 2: direct, the small body walks ptrs/lens in
                           // index order), [3] small lanes per buffer, [4] small workgroups, [5] every length
-                          // equal (unsplit batches only: the batch kernel's window order, BatchView::wperm)
+                          // equal (unsplit batches only: the batch kernel's window order, BatchView::wp)
   uint32_t grid;          // the batch kernel's workgroups
   uint32_t small_cost;    // CU time of a small-list byte, in quarters of a batch-kernel byte
   uint32_t force;

@@ -126,7 +126,7 @@ __global__ __launch_bounds__(1024) void plan_one_tile(const uint64_t *lens, uint
 // sum of squares (round 4: a batch of about equal small buffers is walked in
 // place by the small body, without lists -- mode 2), and the buffers whose
 // length differs from lens[0] (round 6: an unsplit batch of equal buffers
-// is read in the batch kernel's window order, BatchView::wperm).  The scatter decides
+// is read in the batch kernel's window order, BatchView::wp).  The scatter decides
 // for the whole launch (every workgroup reads the same tile sums, so all
 // decide alike): split when the small list is worth at least two of the batch
 // kernel's workgroups (or p.force and there is any small buffer); otherwise
