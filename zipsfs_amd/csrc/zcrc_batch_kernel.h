@@ -1386,13 +1386,24 @@ __global__ __launch_bounds__(kThreads) void crc32_batch_kernel(BatchArgs args) {
     }
   }
 
-  // nominal boundary of wave k: floor(k * Ts / W), without 128-bit math
-  const uint64_t q_tot = Ts / W, r_tot = Ts % W;
-  bool last = (w + 1 == W) && !Td;
+  // Chunked window order (ab_flags bit 6, A/B): the static part cut into
+  // W * wc chunks of ~kWinChunk bytes, wave w taking chunks w, w + W, ...
+  // (the byte-level form of BatchView::wp, for any lengths)
+  uint64_t wc = 1;
+  if ((args.ab_flags & 64u) && !kFused && !join) {
+    const uint64_t cb = kWinChunk >> ((args.ab_flags >> 7) & 3u);  // bits 7-8: 1 MiB >> k
+    wc = (Ts / W + cb / 2) / cb;
+    wc = wc < 1 ? 1 : (wc > 1024 ? 1024 : wc);
+    bv.wp = 0;
+  }
+  const uint64_t C = W * wc;  // chunks; wave w's k-th is chunk k * W + w
+  // nominal boundary of chunk j: floor(j * Ts / C), without 128-bit math
+  const uint64_t q_tot = Ts / C, r_tot = Ts % C;
+  auto nominal = [&](uint64_t j) -> uint64_t { return j >= C ? Ts : q_tot * j + (r_tot * j) / C; };
+  uint64_t kc = 0;  // the wave's static chunk
+  bool last = (w + 1 == W) && !Td && wc == 1;
   uint64_t S0 = 0, S1 = 0, f0 = 0, lb1 = 0;  // f0: first buffer overlapping [S0, S1)
-  if (w < W)
-    bv.range(q_tot * w + (r_tot * w) / W, (w + 1 == W) ? Ts : q_tot * (w + 1) + (r_tot * (w + 1)) / W, last, S0,
-             S1, f0, lb1);
+  if (w < W) bv.range(nominal(w), nominal(w + 1), last, S0, S1, f0, lb1);
   const uint64_t t_search = kStamp ? __builtin_amdgcn_s_memrealtime() : 0;
   if (kFused) {
     __syncthreads();  // every wave's search is done with the LDS prefix
@@ -1442,6 +1453,12 @@ __global__ __launch_bounds__(kThreads) void crc32_batch_kernel(BatchArgs args) {
     if (S0 < S1 || last)
       npieces += process_range<kStrided, kD, kAblate, kRotate, kPrio, kAux, kStamp, kFused, kWin>(
           args, bv, s_lds, tab, S0, S1, last, salt, lane, band, f0, lb1, &t_tail, perbuf_done);
+    if (band && ++kc < wc) {  // the wave's next static chunk
+      const uint64_t j = kc * W + w;
+      last = (j + 1 == C) && !Td;
+      bv.range(nominal(j), nominal(j + 1), last, S0, S1, f0, lb1);
+      continue;
+    }
     if (kStamp && first_claim) t_static_end = __builtin_amdgcn_s_memrealtime();
     if (!units) break;
     const uint64_t tc0 = kStamp ? __builtin_amdgcn_s_memrealtime() : 0;

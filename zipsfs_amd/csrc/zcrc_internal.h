@@ -76,7 +76,9 @@ struct BatchArgs {
   uint32_t ab_flags;  // A/B knobs (0 in the product; ZCRC_AB_FLAGS): bit 0 = split shifts bit by bit (rounds
                       // 1-3), bit 2 = the split plan's small-list workgroups do not join the dynamic part,
                       // bit 3 = no window order for equal buffers (BatchView::wp: the round-5 range order),
-                      // bits 4-5 = the dynamic share (1: an eighth, 2: half, 3: none; 0: as configured)
+                      // bits 4-5 = the dynamic share (1: an eighth, 2: half, 3: none; 0: as configured),
+                      // bit 6 = chunked window order (the static part in W x ~kWinChunk chunks, round-robin),
+                      // bits 7-8 = its chunk kWinChunk >> k
   // fused small batches (kFusedMaxN): lengths to scan in-kernel (the scan is
   // written to `prefix`), split-piece accumulators (n words) and the
   // finished-wave counter; acc, *ctr and *done are zero at launch and left
@@ -175,6 +177,7 @@ struct SplitPlan {
 hipError_t launch_plan_split(const SplitPlan &p, hipStream_t stream);
 constexpr uint32_t kSizeClasses = kSmallMax / 256 + 1;  // small list order: 256-B block count
 constexpr uint32_t kTileWords = 7;
+constexpr uint64_t kWinChunk = 1ull << 20;  // chunked window order (ab_flags bit 6): static chunk size
 constexpr uint64_t kBigMin = 1ull << 20;  // split plan: buffers of at least this go last in the batch kernel's order
 constexpr uint64_t kPlanDirectTiles = 512;  // up to this many tiles each scatter workgroup sums the tile words itself
 // split plan tiles: 1024 x per buffers per plan_split_count / plan_split_scatter
