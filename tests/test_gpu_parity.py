@@ -775,20 +775,24 @@ def test_corrupted_prefix_is_caught_not_walked(n, monkeypatch):
 
 
 @pytest.mark.parametrize("api", ["device", "strided"])
-def test_window_order_equal_buffers(api, monkeypatch):
+@pytest.mark.parametrize("n,L", [(16384, 1 << 20), (20011, (1 << 20) + 24)])
+def test_window_order_equal_buffers(api, n, L, monkeypatch):
     """The batch kernel's window order (BatchView::wp, round 6): 16,384 equal
     1 MiB buffers -- 12 GiB static over 4,096 waves = 3 buffers per wave, so
     logical buffer i is read as physical buffer (i % 3) * 4096 + i / 3 --
-    at odd addresses (stride 1 MiB + 13) with random seeds, through the
-    pointer API (the split plan finds the lengths equal) and the strided
-    API.  Every result equal to the range order's (ZCRC_AB_FLAGS=8) and,
-    on 64 sampled buffers, to the oracle."""
-    n, L, stride = 16384, 1 << 20, (1 << 20) + 13
+    and 20,011 buffers of 1 MiB + 24 B, whose static part (three quarters)
+    is not a whole number of buffers per wave: it is cut to 3 x 4,096 and
+    the rest read as dynamic units from a buffer boundary; at odd addresses
+    (stride L + 13) with random seeds, through the pointer API (the split
+    plan finds the lengths equal) and the strided API.  Every result equal
+    to the range order's (ZCRC_AB_FLAGS=8) and, on 64 sampled buffers, to
+    the oracle."""
+    stride = L + 13
     mem = torch.empty(n * stride + 64, dtype=torch.uint8, device=DEV)
     ptrs = mem.data_ptr() + 5 + torch.arange(n, dtype=torch.int64, device=DEV) * stride
     lens = torch.full((n,), L, dtype=torch.int64, device=DEV)
     z.fill_synthetic(ptrs, lens, index0=333, seed=SEED)
-    rnd = np.random.default_rng(16384)
+    rnd = np.random.default_rng(n)
     seeds_np = rnd.integers(0, 1 << 32, n, dtype=np.uint64).astype(np.uint32)
     seeds = torch.from_numpy(seeds_np.view(np.int32)).to(DEV)
 
@@ -801,7 +805,7 @@ def test_window_order_equal_buffers(api, monkeypatch):
     ref = run()
     monkeypatch.delenv("ZCRC_AB_FLAGS")
     np.testing.assert_array_equal(got, ref)
-    for i in rnd.choice(n, 64, replace=False):
+    for i in np.concatenate([rnd.choice(n, 60, replace=False), [0, 4095, 12288, n - 1]]):
         assert int(got[i]) == o.payload_crc(L, 333 + int(i), crc=int(seeds_np[i])), i
     del mem
     torch.cuda.empty_cache()

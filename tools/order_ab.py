@@ -12,7 +12,7 @@ plan finds the lengths equal) and through zcrc32_batch_device_strided, and
 (--shard) config 5's per-GPU shard, 131,072 x 1 MiB.  Every block's results
 are compared with the reference-generated golden samples.
 
-  python tools/order_ab.py [rounds] [--shard | --c4] [--dyn | --chunk]
+  python tools/order_ab.py [rounds] [--shard | --c4 | --n=N] [--dyn | --chunk]
   (--dyn: also the window order with an eighth, half or none of the bytes
   dynamic; --chunk: the chunked window order, ab_flags bit 6; --c4: config
   4's 100k Zipf-sized buffers instead of config 3)
@@ -37,6 +37,9 @@ def main():
     g = np.load(os.path.join(ROOT, "tests", "golden", "configs.npz"))
     c4 = "--c4" in sys.argv
     n = 131072 if shard else (100000 if c4 else 65536)
+    for a in sys.argv:  # --n=N: N x 1 MiB instead (config 3's goldens below N)
+        if a.startswith("--n="):
+            n = int(a[4:])
     L = 1 << 20
     if c4:  # config 4: bench.py's Zipf lengths, 16-B aligned, one allocation
         sys.path.insert(0, ROOT)
@@ -65,6 +68,8 @@ def main():
         idx, exp = idx[keep], exp[keep]
     else:
         idx, exp = g["cfg3_idx"].astype(np.int64), g["cfg3"]
+        keep = idx < n
+        idx, exp = idx[keep], exp[keep]
     apis = {"device": lambda: z.crc32_batch_device(ptrs, lens, out=out)}
     if not c4:
         apis["strided"] = lambda: z.crc32_batch_strided(mem, L, L, n, out=out)
@@ -98,7 +103,7 @@ def main():
     os.environ.pop("ZCRC_AB_FLAGS", None)
     for (api, order), v in res.items():
         ms = [a for a, _ in v]
-        print(json.dumps({"workload": "config4" if c4 else "config5-shard" if shard else "config3", "api": api,
+        print(json.dumps({"workload": "config4" if c4 else "config5-shard" if shard else f"{n}x1MiB", "api": api,
                           "order": order,
                           "ms_median": round(float(np.median(ms)), 4), "ms": [round(a, 4) for a in ms],
                           "gbs_median": round(total / (float(np.median(ms)) * 1e-3) / 1e9, 1),

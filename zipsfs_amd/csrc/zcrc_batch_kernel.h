@@ -1369,22 +1369,25 @@ __global__ __launch_bounds__(kThreads) void crc32_batch_kernel(BatchArgs args) {
   if (const uint32_t ds = (args.ab_flags >> 4) & 3u) shift = ds == 1 ? 3u : ds == 2 ? 1u : 0u;
   uint64_t Td = (args.ctr && shift) ? (total >> shift) : 0;
   if (Td / W < unit) Td = 0;  // fewer units than waves: static only
-  const uint64_t Ts = total - Td;
+  uint64_t Ts = total - Td;
   // (Round 4: the last units halved -- ZCRC_DYN_TAIL, an A/B knob -- ran
   // 0.4-1.5% slower on config 4 and was dropped: DESIGN.md 7d.)
-  const uint64_t units = Td ? (Td + unit - 1) / unit : 0;
-  if (join && units <= W) return;  // no claims to join: every unit is pre-assigned (uniform per workgroup)
   // Window order (BatchView::wp): equal buffers whose static wave ranges are
   // whole runs of p >= 2 of them (config 3: 48 GiB static over 4,096 waves =
-  // 12 buffers of 1 MiB each; config 5's shard: 24).  ab_flags bit 3 (A/B):
-  // the range order.
+  // 12 buffers of 1 MiB each; config 5's shard: 24).  When the static part
+  // is not such a multiple but there is a dynamic part, the static part is
+  // cut down to p W whole buffers and the rest joins the dynamic units
+  // (which then start on a buffer boundary).  ab_flags bit 3 (A/B): the
+  // range order.
   if (equal && !kFused && !(args.ab_flags & 8u) && args.n && args.n < (1ull << 32)) {
     const uint64_t L = kStrided ? args.len : total / args.n;
-    if (L && (kStrided || L * args.n == total) && Ts % (W * L) == 0) {
+    if (L && (kStrided || L * args.n == total) && (Td || Ts % (W * L) == 0)) {
       const uint64_t p = Ts / (W * L);
-      if (p >= 2 && p * W <= args.n) bv.wp = p, bv.wW = W;
+      if (p >= 2 && p * W <= args.n) bv.wp = p, bv.wW = W, Ts = p * W * L, Td = total - Ts;
     }
   }
+  const uint64_t units = Td ? (Td + unit - 1) / unit : 0;
+  if (join && units <= W) return;  // no claims to join: every unit is pre-assigned (uniform per workgroup)
 
   // Chunked window order (ab_flags bit 6, A/B): the static part cut into
   // W * wc chunks of ~kWinChunk bytes, wave w taking chunks w, w + W, ...
