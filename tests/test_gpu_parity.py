@@ -809,3 +809,40 @@ def test_window_order_equal_buffers(api, n, L, monkeypatch):
         assert int(got[i]) == o.payload_crc(L, 333 + int(i), crc=int(seeds_np[i])), i
     del mem
     torch.cuda.empty_cache()
+
+
+@pytest.mark.parametrize("n,L", [(40000, 100000), (14000, 777777), (50000, 65544), (12000, (1 << 20) - 16)])
+def test_window_order_cut_static_part(n, L, monkeypatch):
+    """The window order with the static part cut to p x W whole buffers
+    (round 6): equal lengths that are no power of two, half (mean < 512 KiB)
+    or a quarter dynamic, p = 4, 2, 6 and 2 buffers per wave on 4,096 waves;
+    odd addresses, random seeds, both APIs.  Every result equal to the range
+    order's (ZCRC_AB_FLAGS=8) and to the other API's; the first and last
+    buffers of the window, the first dynamic ones and 16 random ones equal
+    to the oracle."""
+    stride = L + 7
+    mem = torch.empty(n * stride + 64, dtype=torch.uint8, device=DEV)
+    ptrs = mem.data_ptr() + 3 + torch.arange(n, dtype=torch.int64, device=DEV) * stride
+    lens = torch.full((n,), L, dtype=torch.int64, device=DEV)
+    z.fill_synthetic(ptrs, lens, index0=77, seed=SEED)
+    rnd = np.random.default_rng(L)
+    seeds_np = rnd.integers(0, 1 << 32, n, dtype=np.uint64).astype(np.uint32)
+    seeds = torch.from_numpy(seeds_np.view(np.int32)).to(DEV)
+    res = {}
+    for flags in ("0", "8"):
+        monkeypatch.setenv("ZCRC_AB_FLAGS", flags)
+        res["device", flags] = u32(z.crc32_batch_device(ptrs, lens, seeds=seeds))
+        res["strided", flags] = u32(z.crc32_batch_strided(mem, stride, L, n, seeds=seeds, base_offset=3))
+    monkeypatch.delenv("ZCRC_AB_FLAGS")
+    got = res["device", "0"]
+    for k, v in res.items():
+        np.testing.assert_array_equal(v, got, err_msg=str(k))
+    total = n * L
+    Ts = total - (total >> (1 if L < (512 << 10) else 2))
+    p = Ts // (4096 * L)
+    assert p >= 2
+    edge = [0, 4095, 4096, p * 4096 - 1, p * 4096, p * 4096 + 1, n - 1]
+    for i in np.concatenate([rnd.choice(n, 16, replace=False), edge]):
+        assert int(got[i]) == o.payload_crc(L, 77 + int(i), crc=int(seeds_np[i])), i
+    del mem
+    torch.cuda.empty_cache()
