@@ -805,7 +805,9 @@ uint64_t dyn_unit_override() {
 
 // Measurement knob: ZCRC_AB_FLAGS (read per call) = BatchArgs::ab_flags for
 // device batches: bit 0 split shifts bit by bit, bit 2 the split plan's
-// small-list workgroups stay out of the dynamic part (rounds 1-3 forms)
+// small-list workgroups stay out of the dynamic part (rounds 1-3 forms),
+// bit 3 the range order instead of the window order, bits 4-5 the dynamic
+// share, bits 6-8 the chunked window order (zcrc_internal.h, BatchArgs)
 uint32_t ab_flags_setting() {
   const char *e = getenv("ZCRC_AB_FLAGS");
   return e ? (uint32_t)strtoul(e, nullptr, 0) : 0u;
